@@ -1,0 +1,242 @@
+"""Generate the golden parity fixtures under tests/golden/ from the reference itself.
+
+Runs ONLY in the build container, where the read-only reference checkout lives at
+/root/reference.  It imports the reference's canonical solver module
+``python/flow_over_cylinder (Fischer)/v5.py`` with two absent third-party
+modules stubbed:
+
+* ``numba`` -> ``njit`` is an identity decorator and ``prange`` is ``range``
+  (so every ``@njit`` kernel runs as serial, interpreted NumPy-scalar code;
+  see SURVEY.md section 8c for what that means for fidelity), and
+* ``h5py`` -> an empty module (only used for snapshots, never called here).
+
+Nothing from the reference is copied: this script only CALLS the reference's
+functions and methods on seeded synthetic inputs and stores the inputs and the
+outputs as ``.npz`` data.  The fixtures travel to the GPU box; this script and
+the reference do not need to.
+
+Usage:  python tests/golden/make_golden.py            (regenerates every fixture)
+"""
+from __future__ import annotations
+
+import contextlib
+import importlib.util
+import os
+import sys
+import tempfile
+import types
+from pathlib import Path
+
+import numpy as np
+
+REF_FILE = Path("/root/reference/python/flow_over_cylinder (Fischer)/v5.py")
+OUT = Path(__file__).resolve().parent
+
+
+def _install_stubs() -> None:
+    numba = types.ModuleType("numba")
+
+    def njit(*args, **kwargs):
+        if len(args) == 1 and callable(args[0]) and not kwargs:
+            return args[0]
+        return lambda f: f
+
+    numba.njit = njit
+    numba.prange = range
+    sys.modules["numba"] = numba
+    sys.modules["h5py"] = types.ModuleType("h5py")
+
+
+def load_reference():
+    """Import v5.py (module name ``ref_v5``) from a scratch cwd: its import
+    creates ``logs/`` in the working directory (v5.py:27-34)."""
+    _install_stubs()
+    scratch = tempfile.mkdtemp(prefix="ref_v5_")
+    cwd = os.getcwd()
+    os.chdir(scratch)
+    try:
+        spec = importlib.util.spec_from_file_location("ref_v5", REF_FILE)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    finally:
+        os.chdir(cwd)
+    # keep the reference's logger quiet and away from the repo
+    import logging
+    mod.logger.handlers.clear()
+    mod.logger.addHandler(logging.NullHandler())
+    mod.logger.propagate = False
+    return mod
+
+
+def disk_mask(ny: int, nx: int, cy: float, cx: float, r: float) -> np.ndarray:
+    yy, xx = np.mgrid[0:ny, 0:nx]
+    return (yy - cy) ** 2 + (xx - cx) ** 2 <= r * r
+
+
+@contextlib.contextmanager
+def _quiet_cwd():
+    scratch = tempfile.mkdtemp(prefix="ref_v5_run_")
+    cwd = os.getcwd()
+    os.chdir(scratch)
+    try:
+        yield
+    finally:
+        os.chdir(cwd)
+
+
+def make_cfg(ref, **kw):
+    with _quiet_cwd():
+        return ref.OptimizedTurbulentConfig(**kw)
+
+
+def gen_jacobi(ref) -> None:
+    """Reference Jacobi branch, OptimizedTurbulentSolver.solve_pressure_fast
+    with use_fast_pressure=False (v5.py:336-346), 128x128, 500 iterations."""
+    n, iters = 128, 500
+    for dtype, mem_eff in ((np.float32, True), (np.float64, False)):
+        for masked in (False, True):
+            cfg = make_cfg(ref, nx=n, ny=n, x_min=0.0, x_max=1.0, y_min=0.0, y_max=1.0,
+                           dt_base=5e-5, use_fast_pressure=False, pressure_iterations=iters,
+                           memory_efficient=mem_eff, cylinder_center=(0.3, 0.55), R_cylinder=0.12)
+            with _quiet_cwd():
+                solver = ref.OptimizedTurbulentSolver(cfg)
+            rng = np.random.default_rng(1234)
+            div = rng.standard_normal((n, n)).astype(dtype)
+            mask = solver.cylinder_mask.copy() if masked else np.zeros((n, n), dtype=bool)
+            solver.cylinder_mask = mask
+            phi = solver.solve_pressure_fast(div).copy()
+            tag = "f32" if dtype is np.float32 else "f64"
+            name = f"jacobi2d_{tag}_{n}x{n}_it{iters}_seed1234{'_mask' if masked else ''}.npz"
+            np.savez_compressed(OUT / name, div=div, mask=mask, phi=phi,
+                                dx=np.float64(cfg.dx), dt=np.float32(cfg.dt), iters=np.int64(iters))
+            print("wrote", name, phi.dtype, float(np.abs(phi).max()))
+
+
+def gen_jacobi_rect(ref) -> None:
+    """Non-square, dx != dy Jacobi case (the branch uses dx only, v5.py:343)."""
+    ny, nx, iters = 40, 72, 60
+    cfg = make_cfg(ref, nx=nx, ny=ny, dt_base=5e-5, use_fast_pressure=False,
+                   pressure_iterations=iters, memory_efficient=True,
+                   cylinder_center=(4.0, 2.0), R_cylinder=0.5)
+    with _quiet_cwd():
+        solver = ref.OptimizedTurbulentSolver(cfg)
+    rng = np.random.default_rng(99)
+    div = (rng.standard_normal((ny, nx)) * 3).astype(np.float32)
+    phi = solver.solve_pressure_fast(div).copy()
+    np.savez_compressed(OUT / "jacobi2d_f32_40x72_it60_cyl.npz", div=div, mask=solver.cylinder_mask,
+                        phi=phi, dx=np.float64(cfg.dx), dt=np.float32(cfg.dt), iters=np.int64(iters))
+    print("wrote jacobi2d_f32_40x72_it60_cyl.npz")
+
+
+def gen_rbgs(ref) -> None:
+    """Module-level solve_pressure_gauss_seidel_fast (v5.py:202-226), serial."""
+    ny, nx = 64, 64
+    dx, dy = 1.0 / 63.0, 1.0 / 63.0
+    dt = np.float32(5e-5)
+    rng = np.random.default_rng(7)
+    div = rng.standard_normal((ny, nx)).astype(np.float32)
+    cases = [("rbgs2d_f32_64x64_it20_seed7.npz", 20, 1e-8, np.zeros((ny, nx), bool), dx, dy)]
+    mask = disk_mask(ny, nx, 30.0, 22.0, 9.0)
+    cases.append(("rbgs2d_f32_64x64_it20_seed7_mask.npz", 20, 1e-8, mask, dx, dy))
+    # anisotropic spacing, 48x80
+    cases.append(("rbgs2d_f32_48x80_it15_aniso.npz", 15, 1e-8, np.zeros((48, 80), bool), 20 / 79, 4 / 47))
+    for name, iters, tol, m, ddx, ddy in cases:
+        d = div if m.shape == div.shape else rng.standard_normal(m.shape).astype(np.float32)
+        phi = np.zeros(m.shape, np.float32)
+        out = ref.solve_pressure_gauss_seidel_fast(phi, d, ddx, ddy, dt, m, iters, tol)
+        assert out is phi  # in place, same object (v5.py:223,226)
+        np.savez_compressed(OUT / name, div=d, mask=m, phi=phi, dx=np.float64(ddx), dy=np.float64(ddy),
+                            dt=dt, iters=np.int64(iters), tol=np.float64(tol))
+        print("wrote", name)
+    # early-exit case: tolerance reached after a few iterations on a small RHS
+    ny2, nx2 = 24, 24
+    d2 = rng.standard_normal((ny2, nx2)).astype(np.float32)
+    hist = [np.zeros((ny2, nx2), np.float32)]
+    for k in range(1, 41):
+        p = np.zeros((ny2, nx2), np.float32)
+        ref.solve_pressure_gauss_seidel_fast(p, d2, 1.0, 1.0, np.float32(1.0), np.zeros((ny2, nx2), bool), k, 0.0)
+        hist.append(p)
+    # per-iteration max |change| (each cell is written once per iteration)
+    mc = [float(np.abs(hist[k] - hist[k - 1]).max()) for k in range(1, 41)]
+    tol = float(np.sqrt(mc[11] * mc[12]))  # break lands mid-way through the run
+    hist = hist[1:]
+    p = np.zeros((ny2, nx2), np.float32)
+    ref.solve_pressure_gauss_seidel_fast(p, d2, 1.0, 1.0, np.float32(1.0), np.zeros((ny2, nx2), bool), 400, tol)
+    done = next(k + 1 for k in range(40) if np.array_equal(hist[k], p))
+    np.savez_compressed(OUT / "rbgs2d_f32_24x24_earlyexit.npz", div=d2, mask=np.zeros((ny2, nx2), bool), phi=p,
+                        dx=np.float64(1.0), dy=np.float64(1.0), dt=np.float32(1.0), iters=np.int64(400),
+                        tol=np.float64(tol), iters_done=np.int64(done))
+    print("wrote rbgs2d_f32_24x24_earlyexit.npz iters_done", done)
+
+
+def gen_predictor(ref) -> None:
+    """Predictor a6-a10: time_step lines v5.py:380-403 driven through the
+    reference's own kernel functions, SUPG and upwind variants."""
+    ny, nx = 40, 56
+    cfg = make_cfg(ref, nx=nx, ny=ny)
+    rng = np.random.default_rng(3)
+    u = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+    v = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+    u[5, 7] = 0.0
+    v[5, 7] = 0.0  # exercises the |V| <= 1e-10 branch of tau (v5.py:160-161)
+    dt = np.float32(0.00002)
+    nu_t = np.zeros((ny, nx), np.float32)
+    nu_eff = cfg.nu + nu_t + cfg.artificial_viscosity
+    tau = ref.compute_supg_stabilization_fast(u, v, cfg.dx, cfg.dy, dt, nu_eff)
+    cu = ref.compute_convection_supg_fast(u, v, u, cfg.dx, cfg.dy, tau)
+    cv = ref.compute_convection_supg_fast(u, v, v, cfg.dx, cfg.dy, tau)
+    lu = ref.compute_laplacian_fast(u, cfg.dx, cfg.dy, nu_eff)
+    lv = ref.compute_laplacian_fast(v, cfg.dx, cfg.dy, nu_eff)
+    us = u + dt * (-cu + lu)
+    vs = v + dt * (-cv + lv)
+    uc = ref.compute_convection_fast(u, v, u, cfg.dx, cfg.dy)
+    vc = ref.compute_convection_fast(u, v, v, cfg.dx, cfg.dy)
+    us_up = u + dt * (-uc + lu)
+    vs_up = v + dt * (-vc + lv)
+    div = ref.compute_divergence_fast(us, vs, cfg.dx, cfg.dy)
+    gx, gy = ref.compute_gradient_fast(us, cfg.dx, cfg.dy)
+    np.savez_compressed(OUT / "predictor2d_f32_40x56_seed3.npz", u=u, v=v, dt=dt, dx=np.float64(cfg.dx),
+                        dy=np.float64(cfg.dy), nu_eff=nu_eff, tau=tau, conv_u=cu, conv_v=cv, lap_u=lu,
+                        lap_v=lv, u_star=us, v_star=vs, conv_u_upwind=uc, conv_v_upwind=vc,
+                        u_star_upwind=us_up, v_star_upwind=vs_up, div=div, grad_x=gx, grad_y=gy)
+    print("wrote predictor2d_f32_40x56_seed3.npz")
+
+
+def gen_steps(ref) -> None:
+    """Three full OptimizedTurbulentSolver.time_step() calls (v5.py:375-441)
+    from the potential-flow initial condition, for both pressure branches."""
+    for fast in (True, False):
+        cfg = make_cfg(ref, nx=120, ny=36, pressure_iterations=200, use_fast_pressure=fast)
+        with _quiet_cwd():
+            solver = ref.OptimizedTurbulentSolver(cfg)
+        rec = {"u0": solver.u.copy(), "v0": solver.v.copy(), "cylinder_mask": solver.cylinder_mask,
+               "ibm_mask": solver.ibm_mask}
+        for s in range(3):
+            dt = solver.time_step()
+            rec[f"dt{s}"] = np.float32(dt)
+            rec[f"u{s + 1}"] = solver.u.copy()
+            rec[f"v{s + 1}"] = solver.v.copy()
+            rec[f"phi{s + 1}"] = solver.phi.copy()
+            rec[f"u_star{s + 1}"] = solver.u_star.copy()
+            rec[f"v_star{s + 1}"] = solver.v_star.copy()
+            rec[f"div{s + 1}"] = solver.div_u_star.copy()
+            rec[f"tau{s + 1}"] = solver.tau_supg.copy()
+        rec["energy"] = np.array([e for _, e in solver.energy_history], np.float64)
+        name = f"step_v5_120x36_n3_{'gs' if fast else 'jacobi'}.npz"
+        np.savez_compressed(OUT / name, **rec)
+        print("wrote", name)
+
+
+def main() -> None:
+    if not REF_FILE.exists():
+        raise SystemExit(f"reference not found at {REF_FILE}; fixtures are generated in the build container only")
+    ref = load_reference()
+    gen_jacobi(ref)
+    gen_jacobi_rect(ref)
+    gen_rbgs(ref)
+    gen_predictor(ref)
+    gen_steps(ref)
+
+
+if __name__ == "__main__":
+    main()
