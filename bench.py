@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Benchmark: Gcell-updates/s of the pressure-Poisson Jacobi sweep on MI355X.
+
+Default workload (north_star, BASELINE.json): 7-point Jacobi on a 1024^3 fp32
+grid, one "step" = one pressure solve = zero-fill phi + ITERS (200) Jacobi
+sweeps, inputs resident in HBM.  N GPUs: z-slab decomposition with RCCL halo
+exchange overlapped with the interior sweep; strong scaling (the grid is
+fixed, each rank owns 1024/N planes).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  `value` = all ranks' interior cell-updates / the
+max-over-ranks wall time of the K timed steps.  `roofline` prices the
+dominant kernel (the sweep) at 12 algorithmic bytes per fp32 cell-update
+(read phi, read div, write phi') using HIP events recorded on the sweep's own
+stream around its launches.  `cpu_baseline` times the NumPy restatement of the
+reference's Jacobi branch (oracle/, bit-exact to v5.py:336-346) on a bounded
+sample of the same grid, on this host, at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Gcell-updates/s on pressure-Poisson Jacobi; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # name: (shape, dtype, iters per step, bytes per cell-update)
+    "jacobi3d_1024": ((1024, 1024, 1024), "f32", 200, 12),
+    "jacobi3d_512": ((512, 512, 512), "f32", 200, 12),
+    "jacobi2d_8192_f64": ((8192, 8192), "f64", 1000, 24),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="jacobi3d_1024", choices=sorted(WORKLOADS))
+    ap.add_argument("--iters", type=int, default=0, help="Jacobi sweeps per step (0 = workload default)")
+    ap.add_argument("--variant", type=int, default=0, help="3-D kernel: 0 auto, 1 LDS, 2 cache")
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--zchunk", type=int, default=0)
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-planes", type=int, default=256)
+    ap.add_argument("--sweep-tiles", action="store_true", help="print a tile-size sweep (N=1, 3-D)")
+    return ap.parse_args()
+
+
+def load_traffic(workload: str, n_gpus: int):
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950
+    correction), or None when no matching profile is committed."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        e = d.get(workload)
+        if e and int(e.get("n_gpus", 1)) == n_gpus:
+            return float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
+def cpu_baseline(shape, iters_total_hint):
+    """NumPy restatement timed on this host (1 thread: NumPy ufuncs)."""
+    import oracle
+    if len(shape) == 3:
+        nz = min(shape[0], ARGS.cpu_sample_planes)
+        sample = (nz, shape[1], shape[2])
+        rng = np.random.default_rng(1234)
+        div = rng.standard_normal(sample, dtype=np.float32)
+        it = 2
+        t0 = time.perf_counter()
+        oracle.jacobi3d_numpy(div, h=1.0 / (shape[2] - 1), dt=np.float32(5e-5), iters=it)
+        t = time.perf_counter() - t0
+        cells = (sample[0] - 2) * (sample[1] - 2) * (sample[2] - 2) * it
+        desc = f"{sample[0]}x{sample[1]}x{sample[2]} slab of the grid, {it} sweeps, jacobi3d_numpy"
+    else:
+        ny = min(shape[0], 2048)
+        sample = (ny, shape[1])
+        rng = np.random.default_rng(1234)
+        div = rng.standard_normal(sample)
+        it = 6
+        t0 = time.perf_counter()
+        oracle.jacobi2d_numpy(div, dx=1.0 / (shape[1] - 1), dt=np.float32(5e-5), iters=it)
+        t = time.perf_counter() - t0
+        cells = (sample[0] - 2) * (sample[1] - 2) * it
+        desc = f"{sample[0]}x{sample[1]} rows of the grid, {it} sweeps, jacobi2d_numpy (v5.py:336-346 form)"
+    return {"value": cells / t / 1e9, "unit": "Gcell-updates/s", "cores": 1, "kind": "port",
+            "sample": desc + f"; {t:.2f} s; host has {os.cpu_count()} logical CPUs, NumPy uses 1"}
+
+
+def main():
+    global ARGS
+    ARGS = parse()
+    import torch
+    import torch.distributed as dist
+    import _pkgpath
+    _pkgpath.load()
+    from cfd_simulations_amd import kernels as K
+    from cfd_simulations_amd import slab as S
+    from cfd_simulations_amd._lib import call, lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != ARGS.gpus:
+        if world == 1 and ARGS.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    shape, dt_name, iters_default, bpc = WORKLOADS[ARGS.workload]
+    iters = ARGS.iters or iters_default
+    call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
+    dt = np.float32(5e-5)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+
+    if len(shape) == 3:
+        nz, ny, nx = shape
+        h = 1.0 / (nx - 1)
+        plan = S.SlabPlan(nz, world, rank)
+        if world == 1:
+            div = torch.randn(shape, generator=g, device=dev, dtype=torch.float32)
+            phi = torch.zeros_like(div)
+            tmp = torch.zeros_like(div)
+
+            def step():
+                phi.zero_()
+                K.solve_pressure_jacobi3d(phi, div, h, dt, None, iters, phi_tmp=tmp)
+        else:
+            comm = S.RcclComm(rank, world)
+            sj = S.SlabJacobi3D(plan, ny, nx, h, dt, comm, device=dev)
+            sj.div.copy_(torch.randn(sj.div.shape, generator=g, device=dev, dtype=torch.float32))
+
+            def step():
+                sj.solve(iters, overlap=not ARGS.no_overlap)
+        cells_all = (nz - 2) * (ny - 2) * (nx - 2) * iters
+        cells_rank = (plan.z_update_end - plan.z_update_begin) * (ny - 2) * (nx - 2)
+        workload = f"jacobi3d_7pt_{nz}x{ny}x{nx}_f32"
+        dtype = "f32"
+    else:
+        if world > 1:
+            raise SystemExit("the 2-D workload is single-GPU (config 2); use jacobi3d_1024 for N>1")
+        ny, nx = shape
+        div = torch.randn(shape, generator=g, device=dev, dtype=torch.float64)
+        phi = torch.zeros_like(div)
+        tmp = torch.zeros_like(div)
+        h = 1.0 / (nx - 1)
+
+        def step():
+            phi.zero_()
+            K.solve_pressure_jacobi(phi, div, h, dt, None, iters, phi_tmp=tmp)
+        cells_all = (ny - 2) * (nx - 2) * iters
+        cells_rank = (ny - 2) * (nx - 2)
+        workload = f"jacobi2d_5pt_{ny}x{nx}_f64"
+        dtype = "f64"
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    if ARGS.sweep_tiles and world == 1 and len(shape) == 3:
+        tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells_rank)
+
+    for _ in range(ARGS.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    call("cfd_timing_enable", 1)
+    t0 = time.perf_counter()
+    for _ in range(ARGS.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = ctypes.c_double()
+    nsw = ctypes.c_longlong()
+    call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(nsw), 1)
+    call("cfd_timing_enable", 0)
+    sweep_ms = ms.value / max(nsw.value, 1)
+
+    if world > 1:
+        t = torch.tensor([elapsed, sweep_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, sweep_ms_max = float(t[0]), float(t[1])
+    else:
+        sweep_ms_max = sweep_ms
+
+    value = cells_all * ARGS.steps / elapsed / 1e9
+    # roofline of the dominant kernel: this rank's sweep (per launch)
+    alg_bytes = cells_rank * bpc
+    achieved = alg_bytes / (sweep_ms * 1e-3) / 1e9
+    traffic = load_traffic(ARGS.workload, world)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Gcell-updates/s",
+        "n_gpus": world,
+        "steps": ARGS.steps,
+        "warmup": ARGS.warmup,
+        "ms_per_step": round(elapsed / ARGS.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic (div ~ N(0,1), seeded; phi zero-filled each step like v5.py:337)",
+        "config": {"workload": workload, "grid": list(shape), "iters_per_step": iters,
+                   "decomposition": "z-slab" if len(shape) == 3 else "none",
+                   "halo": ("rccl send/recv, overlapped" if not ARGS.no_overlap else "rccl send/recv")
+                   if world > 1 else "none",
+                   "kernel_variant": ARGS.variant, "waves": ARGS.waves, "zchunk": ARGS.zchunk},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "kernel": "jacobi3d_march" if len(shape) == 3 else "jacobi2d_march",
+                     "bytes_per_cell_update": bpc, "cell_updates_per_launch": cells_rank,
+                     "avg_launch_ms": round(sweep_ms, 4), "max_rank_avg_launch_ms": round(sweep_ms_max, 4)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not ARGS.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(shape, iters)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        sj.comm.close()
+        dist.destroy_process_group()
+
+
+def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells):
+    """Config 3: time every (variant, waves, zchunk) tile on this grid."""
+    import torch
+    res = []
+    for variant in (1, 2):
+        for waves in (1, 2, 4, 8, 16):
+            for zchunk in (0, 64, 128):
+                call("cfd_set_jacobi3d_config", variant, waves, zchunk)
+                phi.zero_()
+                K.solve_pressure_jacobi3d(phi, div, h, dt, None, 4, phi_tmp=tmp)
+                torch.cuda.synchronize()
+                call("cfd_timing_enable", 1)
+                K.solve_pressure_jacobi3d(phi, div, h, dt, None, 20, phi_tmp=tmp)
+                ms = ctypes.c_double()
+                n = ctypes.c_longlong()
+                call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(n), 1)
+                call("cfd_timing_enable", 0)
+                per = ms.value / n.value
+                res.append({"variant": variant, "waves": waves, "zchunk": zchunk, "ms": round(per, 4),
+                            "GBps": round(cells * bpc / per / 1e6, 1)})
+                print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
+    call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
+    return res
+
+
+if __name__ == "__main__":
+    main()

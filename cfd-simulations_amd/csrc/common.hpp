@@ -1,0 +1,101 @@
+// common.hpp -- shared helpers for the cfdsim HIP library (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/cfdsim.h"
+
+// Every kernel in this library is written so that the compiler has nothing to
+// contract: the reference never fuses a multiply-add, and bit-exact parity with
+// the Jacobi branch depends on it.  The Makefile also passes -ffp-contract=off.
+#pragma clang fp contract(off)
+
+namespace cfd {
+
+constexpr int kWave = 64;  // CDNA wavefront
+constexpr int kNumXcd = 8; // MI355X: 8 XCDs, blocks dealt round-robin
+
+void set_error(const char *fmt, ...);
+// bench timing hooks (capi.hip): event pair around a solve's sweep launches
+int timing_begin(hipStream_t s);
+void timing_end(int k, hipStream_t s, long long sweeps);
+
+#define CFD_CHECK_HIP(expr)                                                          \
+    do {                                                                             \
+        hipError_t _e = (expr);                                                      \
+        if (_e != hipSuccess) {                                                      \
+            ::cfd::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                             __FILE__, __LINE__);                                    \
+            return CFD_E_HIP;                                                        \
+        }                                                                            \
+    } while (0)
+
+#define CFD_REQUIRE(cond, ...)               \
+    do {                                     \
+        if (!(cond)) {                       \
+            ::cfd::set_error(__VA_ARGS__);   \
+            return CFD_E_INVALID;            \
+        }                                    \
+    } while (0)
+
+#define CFD_LAUNCH_CHECK()                                                             \
+    do {                                                                               \
+        hipError_t _e = hipGetLastError();                                             \
+        if (_e != hipSuccess) {                                                        \
+            ::cfd::set_error("kernel launch failed: %s (%s:%d)", hipGetErrorString(_e), \
+                             __FILE__, __LINE__);                                      \
+            return CFD_E_HIP;                                                          \
+        }                                                                              \
+    } while (0)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Wave-wide max of a non-negative float, then one atomic per wave.
+// Non-negative IEEE floats order like their bit patterns as unsigned ints.
+// NaN never wins: callers fold with `if (c > m) m = c`, like the reference
+// (v5.py:220-222), before calling this.
+__device__ inline float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+__device__ inline double wave_max(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+__device__ inline void atomic_max_nonneg(float *dst, float v) {
+    atomicMax(reinterpret_cast<unsigned int *>(dst), __float_as_uint(v));
+}
+__device__ inline void atomic_max_nonneg(double *dst, double v) {
+    atomicMax(reinterpret_cast<unsigned long long *>(dst),
+              static_cast<unsigned long long>(__double_as_longlong(v)));
+}
+template <typename T>
+__device__ inline void wave_reduce_max_store(T local, T *dst) {
+    T m = wave_max(local);
+    if ((threadIdx.x & (kWave - 1)) == 0 && m > T(0)) atomic_max_nonneg(dst, m);
+}
+
+// XCD-aware remap of a linear block id: blocks b and b+8 share an XCD (observed
+// round-robin dealing, speed only -- never relied on for correctness).  Gives
+// each XCD a contiguous run of logical tiles so neighbouring tiles (which share
+// halo rows) hit the same L2.  Bijective; the tail beyond a multiple of 8 maps
+// to itself.
+__device__ inline int xcd_swizzle(int bid, int nblocks) {
+    const int full = (nblocks / kNumXcd) * kNumXcd;
+    if (bid >= full) return bid;
+    const int per = full / kNumXcd;
+    return (bid % kNumXcd) * per + bid / kNumXcd;
+}
+
+inline int ceil_div(long a, long b) { return static_cast<int>((a + b - 1) / b); }
+
+}  // namespace cfd

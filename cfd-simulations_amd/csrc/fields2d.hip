@@ -1,0 +1,603 @@
+// fields2d.hip -- predictor (advection-diffusion), divergence, projection,
+// step epilogue and diagnostic reductions of the v5 cylinder solver's
+// time_step(), v5.py:375-441, for gfx950.
+//
+// Arithmetic follows the reference as it executes in NumPy-scalar form: every
+// Python-float constant is rounded to float32 where it meets float32 data
+// (NEP 50), operations run in float32 in the source order, nothing is fused
+// (-ffp-contract=off).  The only intended deviation: |V| = sqrtf(u^2+v^2)
+// (correctly rounded) where the stubbed reference evaluates float32 `** 0.5`
+// through powf; they differ by at most 1 ulp on ~0.07% of inputs, which the
+// tests bound with a relative tolerance.
+//
+// These kernels are one-pass per cell and HBM-bound; the fused predictor
+// reads u, v once (5-point neighbourhoods from L1/L2) and writes u*, v*, tau.
+#include "common.hpp"
+
+namespace cfd {
+
+struct PredConst {
+    float c1x, c1y;  // SUPG first derivative: 0.5 * (0.5/dx)   (v5.py:131,137)
+    float c2x, c2y;  // SUPG second derivative: (0.5/dx)^2       (v5.py:141)
+    float ux, uy;    // upwind: 1/dx                              (v5.py:116)
+    float lx, ly;    // laplacian: 1/(dx*dx)                      (v5.py:168)
+    float h;         // min(dx, dy) as float32                    (v5.py:156)
+    float eps;       // float32(1e-10)
+};
+
+static PredConst make_pred_const(double dx, double dy) {
+    PredConst k;
+    const double sdx = 0.5 / dx, sdy = 0.5 / dy;
+    k.c1x = (float)(0.5 * sdx);
+    k.c1y = (float)(0.5 * sdy);
+    k.c2x = (float)(sdx * sdx);
+    k.c2y = (float)(sdy * sdy);
+    k.ux = (float)(1.0 / dx);
+    k.uy = (float)(1.0 / dy);
+    k.lx = (float)(1.0 / (dx * dx));
+    k.ly = (float)(1.0 / (dy * dy));
+    k.h = (float)(dx < dy ? dx : dy);
+    k.eps = (float)1e-10;
+    return k;
+}
+
+// compute_supg_stabilization_fast body, v5.py:155-161
+__device__ inline float supg_tau(float u, float v, float nu, float dt, const PredConst &k) {
+    const float vm = sqrtf(u * u + v * v);
+    if (vm > k.eps) {
+        const float pe = (vm * k.h) / (nu + k.eps);
+        const float half = pe / 2.0f;
+        const float lim = half < 1.0f ? half : 1.0f;  // Python min(1.0, Pe/2.0)
+        return (k.h / (2.0f * vm)) * lim;
+    }
+    return dt / 2.0f;
+}
+
+// compute_convection_supg_fast body, v5.py:135-146
+__device__ inline float conv_supg(float uc, float vc, float C, float E, float W, float N, float S,
+                                  float t, const PredConst &k) {
+    const float ddx = (E - W) * k.c1x;
+    const float ddy = (N - S) * k.c1y;
+    const float cs = uc * ddx + vc * ddy;
+    if (t > 0.0f) {
+        const float d2x = ((E - 2.0f * C) + W) * k.c2x;
+        const float d2y = ((N - 2.0f * C) + S) * k.c2y;
+        return cs - t * (uc * d2x + vc * d2y);
+    }
+    return cs;
+}
+
+// compute_convection_fast body (first-order upwind), v5.py:120-124
+__device__ inline float conv_upwind(float uc, float vc, float C, float E, float W, float N,
+                                    float S, const PredConst &k) {
+    const float ddx = uc > 0.0f ? (C - W) * k.ux : (E - C) * k.ux;
+    const float ddy = vc > 0.0f ? (C - S) * k.uy : (N - C) * k.uy;
+    return uc * ddx + vc * ddy;
+}
+
+// compute_laplacian_fast body, v5.py:172-175
+__device__ inline float laplacian(float nu, float C, float E, float W, float N, float S,
+                                  const PredConst &k) {
+    const float l1 = ((E - 2.0f * C) + W) * k.lx;
+    const float l2 = ((N - 2.0f * C) + S) * k.ly;
+    return nu * (l1 + l2);
+}
+
+__device__ inline bool interior(int i, int j, int ny, int nx) {
+    return i >= 1 && i < ny - 1 && j >= 1 && j < nx - 1;
+}
+
+#define CFD_2D_INDEX                                     \
+    const int j = blockIdx.x * blockDim.x + threadIdx.x; \
+    const int i = blockIdx.y;                            \
+    if (j >= nx) return;                                 \
+    const size_t c = (size_t)i * nx + j;
+
+__global__ void k_supg_tau(const float *__restrict__ u, const float *__restrict__ v,
+                           const float *__restrict__ nu_eff, float nu_s, float *__restrict__ tau,
+                           int ny, int nx, float dt, PredConst k) {
+    CFD_2D_INDEX
+    float t = 0.0f;  // np.zeros_like boundary ring
+    if (interior(i, j, ny, nx)) t = supg_tau(u[c], v[c], nu_eff ? nu_eff[c] : nu_s, dt, k);
+    tau[c] = t;
+}
+
+__global__ void k_conv_supg(const float *__restrict__ u, const float *__restrict__ v,
+                            const float *__restrict__ f, const float *__restrict__ tau,
+                            float *__restrict__ conv, int ny, int nx, PredConst k) {
+    CFD_2D_INDEX
+    float r = 0.0f;
+    if (interior(i, j, ny, nx))
+        r = conv_supg(u[c], v[c], f[c], f[c + 1], f[c - 1], f[c + nx], f[c - nx], tau[c], k);
+    conv[c] = r;
+}
+
+__global__ void k_conv_upwind(const float *__restrict__ u, const float *__restrict__ v,
+                              const float *__restrict__ f, float *__restrict__ conv, int ny, int nx,
+                              PredConst k) {
+    CFD_2D_INDEX
+    float r = 0.0f;
+    if (interior(i, j, ny, nx))
+        r = conv_upwind(u[c], v[c], f[c], f[c + 1], f[c - 1], f[c + nx], f[c - nx], k);
+    conv[c] = r;
+}
+
+__global__ void k_laplacian(const float *__restrict__ f, const float *__restrict__ nu_eff, float nu_s,
+                            float *__restrict__ lap, int ny, int nx, PredConst k) {
+    CFD_2D_INDEX
+    float r = 0.0f;
+    if (interior(i, j, ny, nx))
+        r = laplacian(nu_eff ? nu_eff[c] : nu_s, f[c], f[c + 1], f[c - 1], f[c + nx], f[c - nx], k);
+    lap[c] = r;
+}
+
+// Fused predictor, v5.py:388-403: u* = u + dt*(-conv_u + lap_u), likewise v.
+template <bool SUPG>
+__global__ __launch_bounds__(256) void k_predictor(const float *__restrict__ u,
+                                                   const float *__restrict__ v,
+                                                   const float *__restrict__ nu_eff, float nu_s,
+                                                   float *__restrict__ us, float *__restrict__ vs,
+                                                   float *__restrict__ tau_out, int ny, int nx,
+                                                   float dt, PredConst k) {
+    CFD_2D_INDEX
+    const float uc = u[c], vc = v[c];
+    float cu = 0.0f, cv = 0.0f, lu = 0.0f, lv = 0.0f, t = 0.0f;
+    if (interior(i, j, ny, nx)) {
+        const float nu = nu_eff ? nu_eff[c] : nu_s;
+        const float uE = u[c + 1], uW = u[c - 1], uN = u[c + nx], uS = u[c - nx];
+        const float vE = v[c + 1], vW = v[c - 1], vN = v[c + nx], vS = v[c - nx];
+        if (SUPG) {
+            t = supg_tau(uc, vc, nu, dt, k);
+            cu = conv_supg(uc, vc, uc, uE, uW, uN, uS, t, k);
+            cv = conv_supg(uc, vc, vc, vE, vW, vN, vS, t, k);
+        } else {
+            cu = conv_upwind(uc, vc, uc, uE, uW, uN, uS, k);
+            cv = conv_upwind(uc, vc, vc, vE, vW, vN, vS, k);
+        }
+        lu = laplacian(nu, uc, uE, uW, uN, uS, k);
+        lv = laplacian(nu, vc, vE, vW, vN, vS, k);
+    }
+    us[c] = uc + dt * (-cu + lu);
+    vs[c] = vc + dt * (-cv + lv);
+    if (SUPG && tau_out) tau_out[c] = t;
+}
+
+// compute_divergence_fast, v5.py:178-187 (+ max|div| diagnostic, v5.py:410)
+__global__ __launch_bounds__(256) void k_divergence(const float *__restrict__ u,
+                                                    const float *__restrict__ v,
+                                                    float *__restrict__ div, int ny, int nx,
+                                                    float cx, float cy, float *absmax) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    float m = 0.0f;
+    if (j < nx) {
+        const size_t c = (size_t)i * nx + j;
+        float d = 0.0f;
+        if (interior(i, j, ny, nx)) d = (u[c + 1] - u[c - 1]) * cx + (v[c + nx] - v[c - nx]) * cy;
+        div[c] = d;
+        const float a = fabsf(d);
+        if (a > m) m = a;
+    }
+    if (absmax) wave_reduce_max_store(m, absmax);
+}
+
+// compute_gradient_fast, v5.py:189-200
+__global__ void k_gradient(const float *__restrict__ phi, float *__restrict__ gx,
+                           float *__restrict__ gy, int ny, int nx, float cx, float cy) {
+    CFD_2D_INDEX
+    float a = 0.0f, b = 0.0f;
+    if (interior(i, j, ny, nx)) {
+        a = (phi[c + 1] - phi[c - 1]) * cx;
+        b = (phi[c + nx] - phi[c - nx]) * cy;
+    }
+    gx[c] = a;
+    gy[c] = b;
+}
+
+// v5.py:413-417: gradient of phi, then u = u* - dt*dpdx, v = v* - dt*dpdy;
+// gradmax <- max sqrt(dpdx^2 + dpdy^2) (v5.py:414-415 diagnostic).
+__global__ __launch_bounds__(256) void k_project(const float *__restrict__ phi,
+                                                 const float *__restrict__ us,
+                                                 const float *__restrict__ vs,
+                                                 float *__restrict__ u, float *__restrict__ v,
+                                                 int ny, int nx, float cx, float cy, float dt,
+                                                 float *gradmax) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    float m = 0.0f;
+    if (j < nx) {
+        const size_t c = (size_t)i * nx + j;
+        float a = 0.0f, b = 0.0f;
+        if (interior(i, j, ny, nx)) {
+            a = (phi[c + 1] - phi[c - 1]) * cx;
+            b = (phi[c + nx] - phi[c - nx]) * cy;
+        }
+        u[c] = us[c] - dt * a;
+        v[c] = vs[c] - dt * b;
+        if (gradmax) {
+            const float g = sqrtf(a * a + b * b);
+            if (g > m) m = g;
+        }
+    }
+    if (gradmax) wave_reduce_max_store(m, gradmax);
+}
+
+// ------------------------------------------------------------ epilogue
+// clean_divergence_fast phi sweep (v5.py:250-253) in the serial lexicographic
+// order: a single workgroup walks the anti-diagonals d = i + j; every cell of
+// a diagonal depends only on earlier diagonals (W, S: new) and later ones
+// (E, N: old), so updating one diagonal at a time reproduces the serial loop
+// exactly.  Global memory stays coherent inside one workgroup (one CU).
+__global__ __launch_bounds__(1024) void k_lex_gs_sweep(float *__restrict__ phi,
+                                                       const float *__restrict__ div, int ny,
+                                                       int nx, float cx, float cy, float cd) {
+    const int imax = ny - 2, jmax = nx - 2;
+    for (int d = 2; d <= imax + jmax; ++d) {
+        const int ilo = max(1, d - jmax), ihi = min(imax, d - 1);
+        for (int i = ilo + (int)threadIdx.x; i <= ihi; i += blockDim.x) {
+            const int j = d - i;
+            const size_t c = (size_t)i * nx + j;
+            const float a = cx * (phi[c + 1] + phi[c - 1]);
+            const float b = cy * (phi[c + nx] + phi[c - nx]);
+            phi[c] = ((a + b) - div[c]) * cd;
+        }
+        __syncthreads();
+    }
+}
+
+// u[1:-1,1:-1] -= grad_x[1:-1,1:-1] (no dt: v5.py:255-256)
+__global__ void k_sub_gradient(const float *__restrict__ phi, float *__restrict__ u,
+                               float *__restrict__ v, int ny, int nx, float cx, float cy) {
+    CFD_2D_INDEX
+    if (!interior(i, j, ny, nx)) return;
+    const float a = (phi[c + 1] - phi[c - 1]) * cx;
+    const float b = (phi[c + nx] - phi[c - nx]) * cy;
+    u[c] = u[c] - a;
+    v[c] = v[c] - b;
+}
+
+// apply_boundary_conditions, v5.py:349-360.  Net effect of the eight
+// assignments in order: rows 0 and ny-1 end at 0; other rows get the inlet
+// u = f32(V_inf*(1 + pert_scale*sin(2*pi*y/y_max + 0.02*step))), v = 0 at
+// x = 0 and a zero-gradient outlet copy from x = nx-2.
+__global__ void k_bc(float *__restrict__ u, float *__restrict__ v, const double *__restrict__ y,
+                     int ny, int nx, double y_max, double v_inf, int step) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < nx) {  // top / bottom rows
+        u[t] = 0.0f;
+        v[t] = 0.0f;
+        u[(size_t)(ny - 1) * nx + t] = 0.0f;
+        v[(size_t)(ny - 1) * nx + t] = 0.0f;
+    }
+    const int i = t;
+    if (i >= 1 && i < ny - 1) {
+        const double s = (double)step;
+        double scale = s / 1000.0;
+        scale = (1.0 < scale ? 1.0 : scale) * 0.01;
+        const double two_pi = 2.0 * 3.141592653589793;
+        const double pert = scale * sin(two_pi * y[i] / y_max + 0.02 * s);
+        const size_t r = (size_t)i * nx;
+        u[r] = (float)(v_inf * (1.0 + pert));
+        v[r] = 0.0f;
+        u[r + nx - 1] = u[r + nx - 2];
+        v[r + nx - 1] = v[r + nx - 2];
+    }
+}
+
+// apply_ibm_fast, v5.py:228-237 (float64 mask => float64 arithmetic)
+__global__ void k_ibm(float *__restrict__ u, float *__restrict__ v, const double *__restrict__ m,
+                      int n, double fs) {
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+        const double mv = m[c];
+        if (mv > 0.0) {
+            const double f = 1.0 - mv * fs;
+            u[c] = (float)((double)u[c] * f);
+            v[c] = (float)((double)v[c] * f);
+        }
+    }
+}
+
+__global__ void k_clip(float *__restrict__ a, size_t n, float lo, float hi) {
+    for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < n;
+         c += (size_t)gridDim.x * blockDim.x) {
+        const float x = a[c];
+        a[c] = x < lo ? lo : (x > hi ? hi : x);  // NaN passes through like np.clip
+    }
+}
+
+// ------------------------------------------------------------ reductions
+__global__ void k_absmax(const float *__restrict__ a, const float *__restrict__ b, size_t n,
+                         float *out) {
+    float m = 0.0f;
+    for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < n;
+         c += (size_t)gridDim.x * blockDim.x) {
+        float x = fabsf(a[c]);
+        if (x > m) m = x;
+        if (b) {
+            x = fabsf(b[c]);
+            if (x > m) m = x;
+        }
+    }
+    wave_reduce_max_store(m, out);
+}
+
+// mean of 0.5*(u^2 + v^2) (v5.py:362-363, :431-432); each cell's energy in
+// float32 like NumPy, the sum in float64.
+__global__ void k_energy_sum(const float *__restrict__ u, const float *__restrict__ v, size_t n,
+                             double *out) {
+    double s = 0.0;
+    for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < n;
+         c += (size_t)gridDim.x * blockDim.x) {
+        const float e = 0.5f * (u[c] * u[c] + v[c] * v[c]);
+        s += (double)e;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+
+__global__ void k_scale_double(double *p, double f) { *p = *p * f; }
+
+// compute_vorticity + nanmax(|w|), v5.py:365-373, :427-428: masked cells are
+// NaN (skipped), the boundary ring is 0.
+__global__ void k_vort_absmax(const float *__restrict__ u, const float *__restrict__ v,
+                              const uint8_t *__restrict__ mask, int ny, int nx, float dx2,
+                              float dy2, float *out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    float m = 0.0f;
+    if (j < nx) {
+        const size_t c = (size_t)i * nx + j;
+        if (interior(i, j, ny, nx) && !(mask && mask[c])) {
+            const float w = (v[c + 1] - v[c - 1]) / dx2 - (u[c + nx] - u[c - nx]) / dy2;
+            const float a = fabsf(w);
+            if (a > m) m = a;
+        }
+    }
+    wave_reduce_max_store(m, out);
+}
+
+// compute_vorticity, v5.py:365-373: interior central differences, boundary
+// ring 0, masked cells NaN.
+__global__ void k_vorticity(const float *__restrict__ u, const float *__restrict__ v,
+                            const uint8_t *__restrict__ mask, float *__restrict__ w, int ny,
+                            int nx, float dx2, float dy2) {
+    CFD_2D_INDEX
+    float r = 0.0f;
+    if (interior(i, j, ny, nx)) r = (v[c + 1] - v[c - 1]) / dx2 - (u[c + nx] - u[c - nx]) / dy2;
+    if (mask && mask[c]) r = __builtin_nanf("");
+    w[c] = r;
+}
+
+__global__ void k_nonfinite(const float *__restrict__ a, const float *__restrict__ b, size_t n,
+                            int *out) {
+    int cnt = 0;
+    for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < n;
+         c += (size_t)gridDim.x * blockDim.x) {
+        cnt += !isfinite(a[c]);
+        if (b) cnt += !isfinite(b[c]);
+    }
+    if (cnt) atomicAdd(out, cnt);
+}
+
+static dim3 grid2d(int ny, int nx) { return dim3(ceil_div(nx, 256), ny); }
+static int grid1d(size_t n) {
+    long b = (long)((n + 255) / 256);
+    if (b > 2048) b = 2048;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+}  // namespace cfd
+
+using namespace cfd;
+
+#define CFD_SHAPE2D(ny, nx) CFD_REQUIRE((ny) >= 1 && (nx) >= 1, "bad 2-D shape (%d, %d)", ny, nx)
+
+extern "C" {
+
+int cfd_supg_tau2d_f32(const float *u, const float *v, const float *nu_eff, float nu_eff_scalar,
+                       float *tau, int ny, int nx, double dx, double dy, float dt, void *stream) {
+    CFD_REQUIRE(u && v && tau, "supg_tau2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_supg_tau, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v, nu_eff,
+                       nu_eff_scalar, tau, ny, nx, dt, make_pred_const(dx, dy));
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_convection_supg2d_f32(const float *u, const float *v, const float *phi, const float *tau,
+                              float *conv, int ny, int nx, double dx, double dy, void *stream) {
+    CFD_REQUIRE(u && v && phi && tau && conv, "convection_supg2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_conv_supg, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v, phi, tau,
+                       conv, ny, nx, make_pred_const(dx, dy));
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_convection_upwind2d_f32(const float *u, const float *v, const float *phi, float *conv,
+                                int ny, int nx, double dx, double dy, void *stream) {
+    CFD_REQUIRE(u && v && phi && conv, "convection_upwind2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_conv_upwind, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v, phi,
+                       conv, ny, nx, make_pred_const(dx, dy));
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_laplacian2d_f32(const float *phi, const float *nu_eff, float nu_eff_scalar, float *lap,
+                        int ny, int nx, double dx, double dy, void *stream) {
+    CFD_REQUIRE(phi && lap, "laplacian2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_laplacian, grid2d(ny, nx), dim3(256), 0, as_stream(stream), phi, nu_eff,
+                       nu_eff_scalar, lap, ny, nx, make_pred_const(dx, dy));
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, float nu_eff_scalar,
+                        float *u_star, float *v_star, float *tau, int ny, int nx, double dx,
+                        double dy, float dt, int use_supg, void *stream) {
+    CFD_REQUIRE(u && v && u_star && v_star, "predictor2d: null pointer");
+    CFD_REQUIRE(u_star != u && v_star != v && u_star != v && v_star != u,
+                "predictor2d: outputs must not alias inputs");
+    CFD_SHAPE2D(ny, nx);
+    const PredConst k = make_pred_const(dx, dy);
+    if (use_supg)
+        hipLaunchKernelGGL(k_predictor<true>, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v,
+                           nu_eff, nu_eff_scalar, u_star, v_star, tau, ny, nx, dt, k);
+    else
+        hipLaunchKernelGGL(k_predictor<false>, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u,
+                           v, nu_eff, nu_eff_scalar, u_star, v_star, tau, ny, nx, dt, k);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_divergence2d_f32(const float *u, const float *v, float *div, int ny, int nx, double dx,
+                         double dy, float *absmax, void *stream) {
+    CFD_REQUIRE(u && v && div, "divergence2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_divergence, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v, div, ny,
+                       nx, (float)(0.5 / dx), (float)(0.5 / dy), absmax);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_gradient2d_f32(const float *phi, float *grad_x, float *grad_y, int ny, int nx, double dx,
+                       double dy, void *stream) {
+    CFD_REQUIRE(phi && grad_x && grad_y, "gradient2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_gradient, grid2d(ny, nx), dim3(256), 0, as_stream(stream), phi, grad_x,
+                       grad_y, ny, nx, (float)(0.5 / dx), (float)(0.5 / dy));
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star, float *u,
+                      float *v, int ny, int nx, double dx, double dy, float dt, float *gradmax,
+                      void *stream) {
+    CFD_REQUIRE(phi && u_star && v_star && u && v, "project2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_project, grid2d(ny, nx), dim3(256), 0, as_stream(stream), phi, u_star,
+                       v_star, u, v, ny, nx, (float)(0.5 / dx), (float)(0.5 / dy), dt, gradmax);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+size_t cfd_clean_divergence_workspace_bytes(int ny, int nx) {
+    return 2 * sizeof(float) * (size_t)(ny > 0 ? ny : 0) * (size_t)(nx > 0 ? nx : 0);
+}
+
+int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, double dy,
+                               int iterations, void *ws, void *stream) {
+    CFD_REQUIRE(u && v && ws, "clean_divergence2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipStream_t s = as_stream(stream);
+    const size_t n = (size_t)ny * nx;
+    float *phi = reinterpret_cast<float *>(ws);
+    float *div = phi + n;
+    CFD_CHECK_HIP(hipMemsetAsync(phi, 0, n * sizeof(float), s));  // np.zeros_like (v5.py:242)
+    const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy);
+    const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv));
+    const float cx = (float)(0.5 / dx), cy = (float)(0.5 / dy);
+    for (int it = 0; it < iterations; ++it) {
+        hipLaunchKernelGGL(k_divergence, grid2d(ny, nx), dim3(256), 0, s, u, v, div, ny, nx, cx, cy,
+                           (float *)nullptr);
+        if (ny > 2 && nx > 2)
+            hipLaunchKernelGGL(k_lex_gs_sweep, dim3(1), dim3(1024), 0, s, phi, div, ny, nx,
+                               (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
+        hipLaunchKernelGGL(k_sub_gradient, grid2d(ny, nx), dim3(256), 0, s, phi, u, v, ny, nx, cx,
+                           cy);
+        CFD_LAUNCH_CHECK();
+    }
+    return CFD_OK;
+}
+
+int cfd_apply_bc2d_f32(float *u, float *v, const double *y, int ny, int nx, double y_max,
+                       double v_inf, int step, void *stream) {
+    CFD_REQUIRE(u && v && y, "apply_bc2d: null pointer");
+    CFD_REQUIRE(ny >= 2 && nx >= 2, "apply_bc2d: grid must be at least 2x2");
+    const int n = ny > nx ? ny : nx;
+    hipLaunchKernelGGL(k_bc, dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), u, v, y, ny,
+                       nx, y_max, v_inf, step);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_apply_ibm2d_f32(float *u, float *v, const double *ibm_mask, int n, double force_strength,
+                        void *stream) {
+    CFD_REQUIRE(u && v && ibm_mask && n >= 0, "apply_ibm2d: bad arguments");
+    if (n == 0) return CFD_OK;
+    hipLaunchKernelGGL(k_ibm, dim3(grid1d(n)), dim3(256), 0, as_stream(stream), u, v, ibm_mask, n,
+                       force_strength);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_clip_f32(float *a, size_t n, float lo, float hi, void *stream) {
+    CFD_REQUIRE(a, "clip: null pointer");
+    if (n == 0) return CFD_OK;
+    hipLaunchKernelGGL(k_clip, dim3(grid1d(n)), dim3(256), 0, as_stream(stream), a, n, lo, hi);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_absmax_f32(const float *a, size_t n, float *out, void *stream) {
+    CFD_REQUIRE(a && out, "absmax: null pointer");
+    if (n == 0) return CFD_OK;
+    hipLaunchKernelGGL(k_absmax, dim3(grid1d(n)), dim3(256), 0, as_stream(stream), a,
+                       (const float *)nullptr, n, out);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_absmax2_f32(const float *a, const float *b, size_t n, float *out, void *stream) {
+    CFD_REQUIRE(a && b && out, "absmax2: null pointer");
+    if (n == 0) return CFD_OK;
+    hipLaunchKernelGGL(k_absmax, dim3(grid1d(n)), dim3(256), 0, as_stream(stream), a, b, n, out);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_energy_mean2d_f32(const float *u, const float *v, size_t n, double *out, void *stream) {
+    CFD_REQUIRE(u && v && out && n > 0, "energy_mean2d: bad arguments");
+    hipStream_t s = as_stream(stream);
+    CFD_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(double), s));
+    hipLaunchKernelGGL(k_energy_sum, dim3(grid1d(n)), dim3(256), 0, s, u, v, n, out);
+    hipLaunchKernelGGL(k_scale_double, dim3(1), dim3(1), 0, s, out, 1.0 / (double)n);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_vorticity_absmax2d_f32(const float *u, const float *v, const uint8_t *mask, int ny, int nx,
+                               double dx, double dy, float *out, void *stream) {
+    CFD_REQUIRE(u && v && out, "vorticity_absmax2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_vort_absmax, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v, mask,
+                       ny, nx, (float)(2.0 * dx), (float)(2.0 * dy), out);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_vorticity2d_f32(const float *u, const float *v, const uint8_t *mask, float *w, int ny,
+                        int nx, double dx, double dy, void *stream) {
+    CFD_REQUIRE(u && v && w, "vorticity2d: null pointer");
+    CFD_SHAPE2D(ny, nx);
+    hipLaunchKernelGGL(k_vorticity, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v, mask, w,
+                       ny, nx, (float)(2.0 * dx), (float)(2.0 * dy));
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_nonfinite_count_f32(const float *a, const float *b, size_t n, int *out, void *stream) {
+    CFD_REQUIRE(a && out, "nonfinite_count: null pointer");
+    hipStream_t s = as_stream(stream);
+    CFD_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(int), s));
+    if (n == 0) return CFD_OK;
+    hipLaunchKernelGGL(k_nonfinite, dim3(grid1d(n)), dim3(256), 0, s, a, b, n, out);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,377 @@
+// poisson2d.hip -- 2-D pressure-Poisson kernels for gfx950.
+//
+//  * Jacobi 5-point (f32 / f64): the reference's NumPy branch of
+//    OptimizedTurbulentSolver.solve_pressure_fast, v5.py:336-346, bit-exact.
+//  * Red-black Gauss-Seidel (f32): solve_pressure_gauss_seidel_fast,
+//    v5.py:202-226, with the serial-execution arithmetic of the reference.
+//
+// Jacobi design (HBM-bound, 12 B per f32 cell-update / 24 B per f64):
+//  one wave owns a 64*VEC-cell x-segment and marches down a chunk of rows,
+//  holding rows y-1, y, y+1 in registers (a 3-row register queue, next row
+//  prefetched one step ahead), so every phi value is fetched from HBM once per
+//  sweep.  x-neighbours come from the adjacent lane through a cross-lane
+//  shuffle; only lanes 0 and 63 load one extra scalar per row (L1/L2 hits).
+//  Loads and stores are 16 B per lane (float4 / double2).  The RHS
+//  (f32(dx^2)*div)/dt is recomputed in-register from div every sweep: the same
+//  4 B of traffic as reading a precomputed rhs array, bit-identical to NumPy,
+//  and no prologue pass or workspace.
+#include "common.hpp"
+
+namespace cfd {
+
+template <typename T, int VEC>
+struct VecOf {
+    typedef T type __attribute__((ext_vector_type(VEC)));
+};
+template <typename T>
+struct VecOf<T, 1> {
+    using type = T;
+};
+
+template <typename T, int VEC>
+__device__ inline void ld(const T *p, T (&r)[VEC]) {
+    if constexpr (VEC == 1) {
+        r[0] = p[0];
+    } else {
+        typename VecOf<T, VEC>::type v = *reinterpret_cast<const typename VecOf<T, VEC>::type *>(p);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) r[k] = v[k];
+    }
+}
+template <typename T, int VEC>
+__device__ inline void st(T *p, const T (&r)[VEC]) {
+    if constexpr (VEC == 1) {
+        p[0] = r[0];
+    } else {
+        typename VecOf<T, VEC>::type v;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) v[k] = r[k];
+        *reinterpret_cast<typename VecOf<T, VEC>::type *>(p) = v;
+    }
+}
+
+// One Jacobi sweep over rows [1, ny-1).  Grid: waves = nseg * nchunk.
+template <typename T, int VEC, bool RESID>
+__global__ __launch_bounds__(256) void jacobi2d_march(const T *__restrict__ in, T *__restrict__ out,
+                                                      const T *__restrict__ div,
+                                                      const uint8_t *__restrict__ mask, int ny,
+                                                      int nx, int nseg, int rows_per_chunk,
+                                                      T dx2, T dtv, T *__restrict__ resid) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wpb = blockDim.x / kWave;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const long wave = (long)bid * wpb + threadIdx.x / kWave;
+    const int seg = (int)(wave % nseg);
+    const int chunk = (int)(wave / nseg);
+    const int y0 = 1 + chunk * rows_per_chunk;
+    if (y0 >= ny - 1) return;  // wave-uniform
+    const int y1 = min(y0 + rows_per_chunk, ny - 1);
+    const int x0 = (seg * kWave + lane) * VEC;
+    const bool valid = x0 < nx;
+    const bool has_left = valid && lane == 0 && x0 > 0;
+    const bool has_right = lane == kWave - 1 && x0 + VEC < nx;
+
+    T prv[VEC], cur[VEC], nxt[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) prv[k] = cur[k] = nxt[k] = T(0);
+    T cl = T(0), cr = T(0), nl = T(0), nr = T(0);
+    if (valid) {
+        ld<T, VEC>(in + (size_t)(y0 - 1) * nx + x0, prv);
+        ld<T, VEC>(in + (size_t)y0 * nx + x0, cur);
+    }
+    if (has_left) cl = in[(size_t)y0 * nx + x0 - 1];
+    if (has_right) cr = in[(size_t)y0 * nx + x0 + VEC];
+    T rmax = T(0);
+
+    for (int y = y0; y < y1; ++y) {
+        const size_t row = (size_t)y * nx;
+        // prefetch row y+1 (always inside the grid: y <= ny-2)
+        if (valid) ld<T, VEC>(in + row + nx + x0, nxt);
+        if (has_left) nl = in[row + nx + x0 - 1];
+        if (has_right) nr = in[row + nx + x0 + VEC];
+        T d[VEC];
+        uint8_t m[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) { d[k] = T(0); m[k] = 0; }
+        if (valid) {
+            ld<T, VEC>(div + row + x0, d);
+            if (mask) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) m[k] = mask[row + x0 + k];
+            }
+        }
+        // x-neighbours across lanes: W of element 0 from lane-1, E of the last from lane+1
+        T wl = __shfl_up(cur[VEC - 1], 1, kWave);
+        T er = __shfl_down(cur[0], 1, kWave);
+        if (lane == 0) wl = cl;
+        if (lane == kWave - 1) er = cr;
+        T o[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const T E = (k + 1 < VEC) ? cur[k + 1] : er;
+            const T W = (k > 0) ? cur[k - 1] : wl;
+            const int x = x0 + k;
+            T val;
+            if (x == 0 || x >= nx - 1) {
+                val = cur[k];  // Dirichlet edge: copied (phi_new = phi.copy())
+            } else {
+                // ((((E + W) + N) + S) - (dx2*div)/dt) * 0.25 -- NumPy's order
+                T s = E + W;
+                s = s + nxt[k];
+                s = s + prv[k];
+                const T rhs = (dx2 * d[k]) / dtv;
+                val = T(0.25) * (s - rhs);
+            }
+            if (m[k]) val = T(0);
+            o[k] = val;
+            if constexpr (RESID) {
+                T c = val - cur[k];
+                c = c < T(0) ? -c : c;
+                if (c > rmax) rmax = c;
+            }
+        }
+        if (valid) st<T, VEC>(out + row + x0, o);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) { prv[k] = cur[k]; cur[k] = nxt[k]; }
+        cl = nl;
+        cr = nr;
+    }
+    if constexpr (RESID) wave_reduce_max_store(rmax, resid);
+}
+
+// Boundary rows/planes of a ping-pong pair: v = mask ? 0 : a[k]; a[k] = b[k] = v.
+// (phi_new[mask] = 0 also hits masked edge cells, v5.py:345.)
+template <typename T>
+__global__ void fix_cells(T *__restrict__ a, T *__restrict__ b, const uint8_t *__restrict__ mask,
+                          size_t start, size_t count) {
+    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < count;
+         k += (size_t)gridDim.x * blockDim.x) {
+        const size_t c = start + k;
+        T v = a[c];
+        if (mask && mask[c]) v = T(0);
+        a[c] = v;
+        b[c] = v;
+    }
+}
+template __global__ void fix_cells<float>(float *, float *, const uint8_t *, size_t, size_t);
+template __global__ void fix_cells<double>(double *, double *, const uint8_t *, size_t, size_t);
+
+template <typename T>
+int launch_fix_cells(T *a, T *b, const uint8_t *mask, size_t start, size_t count, hipStream_t s) {
+    if (count == 0) return CFD_OK;
+    int blocks = ceil_div((long)count, 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(fix_cells<T>, dim3(blocks), dim3(256), 0, s, a, b, mask, start, count);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+template int launch_fix_cells<float>(float *, float *, const uint8_t *, size_t, size_t, hipStream_t);
+template int launch_fix_cells<double>(double *, double *, const uint8_t *, size_t, size_t,
+                                      hipStream_t);
+
+template <typename T, int VEC>
+static int jacobi2d_sweep(const T *in, T *out, const T *div, const uint8_t *mask, int ny, int nx,
+                          T dx2, T dtv, T *resid, hipStream_t s) {
+    const int nseg = ceil_div(nx, kWave * VEC);
+    const int rows = ny - 2;
+    if (rows <= 0) return CFD_OK;
+    // ~8192 waves (32 per CU) when the grid allows; >= 4 rows per chunk.
+    long target = 8192;
+    int rpc = ceil_div((long)rows * nseg, target);
+    if (rpc < 4) rpc = 4;
+    if (rpc > 64) rpc = 64;
+    const int nchunk = ceil_div(rows, rpc);
+    const long waves = (long)nseg * nchunk;
+    const int wpb = 4;
+    const int blocks = ceil_div(waves, wpb);
+    if (resid)
+        hipLaunchKernelGGL((jacobi2d_march<T, VEC, true>), dim3(blocks), dim3(wpb * kWave), 0, s,
+                           in, out, div, mask, ny, nx, nseg, rpc, dx2, dtv, resid);
+    else
+        hipLaunchKernelGGL((jacobi2d_march<T, VEC, false>), dim3(blocks), dim3(wpb * kWave), 0, s,
+                           in, out, div, mask, ny, nx, nseg, rpc, dx2, dtv, resid);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+template <typename T>
+static int jacobi2d_solve(const T *div, T *phi, T *tmp, const uint8_t *mask, int ny, int nx,
+                          T dx2, T dtv, int iters, int resid_every, T *resid_out, hipStream_t s) {
+    CFD_REQUIRE(div && phi && tmp, "jacobi2d: null array pointer");
+    CFD_REQUIRE(ny >= 1 && nx >= 1, "jacobi2d: bad shape (%d, %d)", ny, nx);
+    CFD_REQUIRE(iters >= 0, "jacobi2d: iters < 0");
+    CFD_REQUIRE(resid_every <= 0 || resid_out, "jacobi2d: resid_every > 0 needs resid_out");
+    if (iters == 0) return CFD_OK;
+    const size_t plane = (size_t)nx;
+    int rc;
+    // Dirichlet rows 0 and ny-1 (masked -> 0), identical in both buffers.
+    if ((rc = launch_fix_cells<T>(phi, tmp, mask, 0, plane, s))) return rc;
+    if (ny > 1 && (rc = launch_fix_cells<T>(phi, tmp, mask, (size_t)(ny - 1) * plane, plane, s)))
+        return rc;
+    const int nres = resid_every > 0 ? iters / resid_every : 0;
+    if (nres > 0) CFD_CHECK_HIP(hipMemsetAsync(resid_out, 0, sizeof(T) * nres, s));
+    constexpr int V = 16 / sizeof(T);
+    const bool vec_ok = (nx % V == 0) && aligned16(div) && aligned16(phi) && aligned16(tmp);
+    T *a = phi, *b = tmp;
+    const int tk = timing_begin(s);
+    for (int it = 0; it < iters; ++it) {
+        T *r = (resid_every > 0 && (it + 1) % resid_every == 0) ? resid_out + ((it + 1) / resid_every - 1)
+                                                                 : nullptr;
+        rc = vec_ok ? jacobi2d_sweep<T, V>(a, b, div, mask, ny, nx, dx2, dtv, r, s)
+                    : jacobi2d_sweep<T, 1>(a, b, div, mask, ny, nx, dx2, dtv, r, s);
+        if (rc) return rc;
+        T *t = a; a = b; b = t;
+    }
+    timing_end(tk, s, iters);
+    if (a != phi) CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(T) * (size_t)ny * nx, hipMemcpyDeviceToDevice, s));
+    return CFD_OK;
+}
+
+// ----------------------------------------------------------- red-black GS
+// Workspace layout: [0] int stop flag (unused by kernels, kept for ABI room),
+// [1] int iters_done scratch, then float maxc[iterations] at byte 16.
+struct RbgsWs {
+    int flags[4];
+    float maxc[1];
+};
+
+// Colour pass, in place.  Each thread owns a 4-cell x-vector of one row and
+// rewrites it whole (cells of the other colour unchanged; nobody else writes
+// them in this pass).  Stop rule (v5.py:224-225) is evaluated on device: the
+// pass of iteration `it` runs only if no earlier iteration ended with
+// max_change < tol; the first pass to see that records `it` in iters_done.
+__device__ inline bool rbgs_stopped(const RbgsWs *ws, int it, float tol) {
+    return it > 0 && ws->maxc[it - 1] < tol;
+}
+
+__global__ void rbgs_init(RbgsWs *ws, int iterations, int *iters_done) {
+    for (int k = threadIdx.x; k < iterations; k += blockDim.x) ws->maxc[k] = 0.0f;
+    if (threadIdx.x < 4) ws->flags[threadIdx.x] = 0;
+    if (threadIdx.x == 0 && iters_done) *iters_done = iterations;
+}
+
+int launch_rbgs_init(RbgsWs *ws, int iterations, int *iters_done, hipStream_t s) {
+    hipLaunchKernelGGL(rbgs_init, dim3(1), dim3(1024), 0, s, ws, iterations, iters_done);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+template <int C, int VEC>
+__global__ __launch_bounds__(256) void rbgs2d_color(float *__restrict__ phi,
+                                                    const float *__restrict__ div,
+                                                    const uint8_t *__restrict__ mask, int ny,
+                                                    int nx, float cx, float cy, float cd,
+                                                    float dt_inv, float tol, RbgsWs *ws, int it,
+                                                    int *iters_done) {
+    // maxc[it-1] is final once iteration it-1's two passes completed in-stream.
+    // After a stop, later iterations never write maxc, so it stays 0 < tol and
+    // the stop persists (tol <= 0 never stops, like the reference).
+    if (rbgs_stopped(ws, it, tol)) {
+        if (C == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && iters_done)
+            atomicMin(iters_done, it);
+        return;
+    }
+    const int i = blockIdx.y + 1;  // rows 1..ny-2
+    const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * VEC;
+    float mx = 0.0f;
+    if (x0 < nx) {
+        const size_t row = (size_t)i * nx;
+        float c[VEC], n[VEC], sv[VEC], d[VEC];
+        ld<float, VEC>(phi + row + x0, c);
+        ld<float, VEC>(phi + row + nx + x0, n);
+        ld<float, VEC>(phi + row - nx + x0, sv);
+        ld<float, VEC>(div + row + x0, d);
+        const float wl = x0 > 0 ? phi[row + x0 - 1] : 0.0f;
+        const float er = x0 + VEC < nx ? phi[row + x0 + VEC] : 0.0f;
+        float o[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            o[k] = c[k];
+            const int j = x0 + k;
+            // colour c visits j = 1 + (i + c) % 2 step 2  <=>  (i + j + 1 + c) even
+            if (j >= 1 && j < nx - 1 && ((i + j + 1 + C) & 1) == 0 && !(mask && mask[row + j])) {
+                const float E = (k + 1 < VEC) ? c[k + 1] : er;
+                const float W = (k > 0) ? c[k - 1] : wl;
+                const float rhs = -d[k] * dt_inv;
+                const float a = cx * (E + W);
+                const float b = cy * (n[k] + sv[k]);
+                const float pn = ((a + b) - rhs) * cd;
+                float ch = fabsf(pn - c[k]);
+                if (ch > mx) mx = ch;
+                o[k] = pn;
+            }
+        }
+        st<float, VEC>(phi + row + x0, o);
+    }
+    wave_reduce_max_store(mx, &ws->maxc[it]);
+}
+
+template <int VEC>
+static int rbgs2d_iter(float *phi, const float *div, const uint8_t *mask, int ny, int nx, float cx,
+                       float cy, float cd, float dt_inv, float tol, RbgsWs *ws, int it,
+                       int *iters_done, hipStream_t s) {
+    const int threads = 256;
+    dim3 grid(ceil_div(ceil_div(nx, VEC), threads), ny - 2);
+    hipLaunchKernelGGL((rbgs2d_color<0, VEC>), grid, dim3(threads), 0, s, phi, div, mask, ny, nx,
+                       cx, cy, cd, dt_inv, tol, ws, it, iters_done);
+    hipLaunchKernelGGL((rbgs2d_color<1, VEC>), grid, dim3(threads), 0, s, phi, div, mask, ny, nx,
+                       cx, cy, cd, dt_inv, tol, ws, it, iters_done);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+}  // namespace cfd
+
+using namespace cfd;
+
+extern "C" {
+
+int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t *mask, int ny,
+                     int nx, double dx, float dt, int iters, int resid_every, float *resid_out,
+                     void *stream) {
+    // `cfg.dx**2` is a Python float; NEP 50 rounds it to float32 against the
+    // float32 array (v5.py:343).
+    return jacobi2d_solve<float>(div, phi, phi_tmp, mask, ny, nx, (float)(dx * dx), dt, iters,
+                                 resid_every, resid_out, as_stream(stream));
+}
+
+int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, const uint8_t *mask, int ny,
+                     int nx, double dx, float dt, int iters, int resid_every, double *resid_out,
+                     void *stream) {
+    return jacobi2d_solve<double>(div, phi, phi_tmp, mask, ny, nx, dx * dx, (double)dt, iters,
+                                  resid_every, resid_out, as_stream(stream));
+}
+
+size_t cfd_rbgs_workspace_bytes(int iterations) {
+    return 16 + sizeof(float) * (size_t)(iterations > 0 ? iterations : 1);
+}
+
+int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
+                   double dy, float dt, int iterations, double tolerance, float *phi_tmp, void *ws,
+                   int *iters_done, void *stream) {
+    (void)phi_tmp;  // the in-place colour passes need no second buffer
+    CFD_REQUIRE(phi && div && ws, "rbgs2d: null pointer");
+    CFD_REQUIRE(ny >= 1 && nx >= 1 && iterations >= 0, "rbgs2d: bad arguments");
+    hipStream_t s = as_stream(stream);
+    // v5.py:205-210: Python-float constants, rounded to f32 where they meet f32
+    const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy);
+    const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv));
+    const float cx = (float)dx2_inv, cy = (float)dy2_inv, cd = (float)denom_inv;
+    const float dt_inv = 1.0f / dt;  // 1.0 / np.float32 -> float32
+    const float tol = (float)tolerance;
+    RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
+    int rc = launch_rbgs_init(w, iterations, iters_done, s);
+    if (rc) return rc;
+    if (ny < 3 || nx < 3 || iterations == 0) return CFD_OK;
+    const bool vec_ok = (nx % 4 == 0) && aligned16(phi) && aligned16(div);
+    const int tk = timing_begin(s);
+    for (int it = 0; it < iterations; ++it) {
+        rc = vec_ok ? rbgs2d_iter<4>(phi, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, iters_done, s)
+                        : rbgs2d_iter<1>(phi, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, iters_done, s);
+        if (rc) return rc;
+    }
+    timing_end(tk, s, 2LL * iterations);
+    return CFD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,450 @@
+// poisson3d.hip -- 3-D 7-point pressure-Poisson kernels for gfx950.
+//
+// The reference is 2-D only; the 3-D path generalises its Jacobi template
+// (v5.py:336-346) to 7 points:
+//     phi_new = f32(1/6) * (((((E+W)+N)+S)+U)+D - f32(h*h)*div/dt)
+// and its red-black Gauss-Seidel (v5.py:202-226) to (z+i+j) parity colours.
+//
+// Jacobi sweep design ("2.5-D z-march"; HBM-bound, 12 B per cell-update):
+//  * a workgroup owns an x-segment of 256 cells (64 lanes x float4) by W rows
+//    (one wave per row) and marches a chunk of z-planes;
+//  * z-neighbours live in a 3-plane register queue (the plane after next is
+//    prefetched one step ahead), so each phi value is read from HBM once;
+//  * y-neighbours: variant LDS stages the current plane's W rows plus two halo
+//    rows in a double-buffered LDS tile (one barrier per plane); variant CACHE
+//    loads them straight from global (they are the rows the neighbouring
+//    waves just fetched: L1/L2 hits);
+//  * x-neighbours come from the adjacent lane by cross-lane shuffle; lanes 0
+//    and 63 fetch one scalar each per row;
+//  * the RHS (h^2*div)/dt is recomputed in-register from div (4 B either way);
+//  * the workgroup -> tile map is XCD-aware: each XCD gets a contiguous run of
+//    y-tiles so the halo rows two tiles share stay in that XCD's L2.
+#include "common.hpp"
+
+namespace cfd {
+
+// Dirichlet faces of a ping-pong pair, planes [za, zb) of an (nz, ny, nx)
+// array: every cell of a plane in `full` planes, else rows y = 0 and ny-1
+// (x faces are copied through by the sweep itself):
+//     v = mask ? 0 : a;  a = b = v      (phi_new[mask] = 0 hits faces too)
+__global__ void fix_faces3d(float *__restrict__ a, float *__restrict__ b,
+                            const uint8_t *__restrict__ mask, int ny, int nx, int za, int zb,
+                            int full_lo, int full_hi) {
+    const size_t plane = (size_t)ny * nx;
+    for (int z = za + blockIdx.y; z < zb; z += gridDim.y) {
+        const bool full = z == full_lo || z == full_hi;
+        const size_t n = full ? plane : 2 * (size_t)nx;
+        for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
+             k += (size_t)gridDim.x * blockDim.x) {
+            size_t c;
+            if (full) c = (size_t)z * plane + k;
+            else c = (size_t)z * plane + (k < (size_t)nx ? k : (size_t)(ny - 1) * nx + (k - nx));
+            float v = a[c];
+            if (mask && mask[c]) v = 0.f;
+            a[c] = v;
+            b[c] = v;
+        }
+    }
+}
+
+int launch_fix_faces3d(float *a, float *b, const uint8_t *mask, int ny, int nx, int za, int zb,
+                       int full_lo, int full_hi, hipStream_t s) {
+    if (zb <= za) return CFD_OK;
+    int gy = zb - za;
+    if (gy > 1024) gy = 1024;
+    hipLaunchKernelGGL(fix_faces3d, dim3(16, gy), dim3(256), 0, s, a, b, mask, ny, nx, za, zb,
+                       full_lo, full_hi);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+struct J3Config {
+    int variant = 0;  // 0 auto, 1 LDS, 2 cache
+    int waves = 0;    // rows per workgroup (0 = auto)
+    int zchunk = 0;   // planes per workgroup (0 = auto)
+};
+static J3Config g_j3;
+
+__device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ inline void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+
+template <int W, bool USE_LDS, bool RESID, bool MASK>
+__global__ __launch_bounds__(W * 64) void jacobi3d_march(
+    const float *__restrict__ in, float *__restrict__ out, const float *__restrict__ div,
+    const uint8_t *__restrict__ mask, int ny, int nx, int nseg, int ntile_y, int zb, int ze,
+    int zchunk, float h2, float dt, float *__restrict__ resid) {
+    __shared__ float4 lds[USE_LDS ? 2 : 1][USE_LDS ? W + 2 : 1][64];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    // logical tile: seg fastest, then y-tile, then z-chunk; XCD-contiguous runs
+    const int t = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int seg = t % nseg;
+    const int ty = (t / nseg) % ntile_y;
+    const int zc = t / (nseg * ntile_y);
+    const int z0 = zb + zc * zchunk;
+    if (z0 >= ze) return;  // workgroup-uniform
+    const int z1 = min(z0 + zchunk, ze);
+    const int y = 1 + ty * W + w;
+    const int x0 = (seg * 64 + lane) * 4;
+    const bool xin = x0 < nx;
+    const bool ok = y < ny - 1 && xin;      // this lane updates cells
+    const bool live = y <= ny - 1 && xin;   // this lane's row is read by a neighbour (LDS)
+    const bool has_left = ok && lane == 0 && x0 > 0;
+    const bool has_right = ok && lane == 63 && x0 + 4 < nx;
+    const size_t plane = (size_t)ny * nx;
+    const size_t rofs = (size_t)y * nx + x0;
+    // LDS halo rows: row y-1 for wave 0, row y+1 for the last wave
+    const bool lo_ok = USE_LDS && w == 0 && xin && y <= ny - 1;
+    const bool hi_ok = USE_LDS && w == W - 1 && xin && y + 1 <= ny - 1;
+
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 dn = zero4, cur = zero4, up = zero4, up2 = zero4;
+    float4 nn = zero4, ss = zero4, nn_next = zero4, ss_next = zero4;  // CACHE variant
+    float4 hlo = zero4, hhi = zero4, hlo_next = zero4, hhi_next = zero4;  // LDS variant
+    float cl = 0.f, cr = 0.f, nl = 0.f, nr = 0.f;
+
+    const float *pz = in + (size_t)z0 * plane;
+    if (ok) {
+        dn = ld4(pz - plane + rofs);
+        if (!USE_LDS) {
+            nn = ld4(pz + rofs + nx);
+            ss = ld4(pz + rofs - nx);
+        }
+    }
+    if (ok || (USE_LDS && live)) {
+        cur = ld4(pz + rofs);
+        up = ld4(pz + plane + rofs);
+    }
+    if (lo_ok) hlo = ld4(pz + rofs - nx);
+    if (hi_ok) hhi = ld4(pz + rofs + nx);
+    if (has_left) cl = pz[rofs - 1];
+    if (has_right) cr = pz[rofs + 4];
+    float rmax = 0.f;
+    const float sixth = 1.0f / 6.0f;
+
+    for (int z = z0; z < z1; ++z) {
+        const float *p = in + (size_t)z * plane;
+        const bool more = z + 1 < z1;
+        // prefetch for plane z+1: its upper neighbour (z+2), y-rows, x-edges
+        if (more) {
+            if (ok) {
+                up2 = ld4(p + 2 * plane + rofs);
+                if (!USE_LDS) {
+                    nn_next = ld4(p + plane + rofs + nx);
+                    ss_next = ld4(p + plane + rofs - nx);
+                }
+            } else if (USE_LDS && live) {
+                up2 = ld4(p + 2 * plane + rofs);  // boundary row: feeds a neighbour only
+            }
+            if (lo_ok) hlo_next = ld4(p + plane + rofs - nx);
+            if (hi_ok) hhi_next = ld4(p + plane + rofs + nx);
+            if (has_left) nl = p[plane + rofs - 1];
+            if (has_right) nr = p[plane + rofs + 4];
+        }
+        float4 d = zero4;
+        uchar4 m = make_uchar4(0, 0, 0, 0);
+        if (ok) {
+            d = ld4(div + (size_t)z * plane + rofs);
+            if (MASK) m = *reinterpret_cast<const uchar4 *>(mask + (size_t)z * plane + rofs);
+        }
+        if (USE_LDS) {
+            const int buf = z & 1;
+            lds[buf][w + 1][lane] = cur;
+            if (w == 0) lds[buf][0][lane] = hlo;
+            if (w == W - 1) lds[buf][W + 1][lane] = hhi;
+            __syncthreads();
+            nn = lds[buf][w + 2][lane];
+            ss = lds[buf][w][lane];
+        }
+        float wl = __shfl_up(cur.w, 1, 64);
+        float er = __shfl_down(cur.x, 1, 64);
+        if (lane == 0) wl = cl;
+        if (lane == 63) er = cr;
+        const float c[4] = {cur.x, cur.y, cur.z, cur.w};
+        const float N[4] = {nn.x, nn.y, nn.z, nn.w};
+        const float S[4] = {ss.x, ss.y, ss.z, ss.w};
+        const float U[4] = {up.x, up.y, up.z, up.w};
+        const float D[4] = {dn.x, dn.y, dn.z, dn.w};
+        const float dv[4] = {d.x, d.y, d.z, d.w};
+        const unsigned char mk[4] = {m.x, m.y, m.z, m.w};
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float E = k < 3 ? c[k + 1] : er;
+            const float Wv = k > 0 ? c[k - 1] : wl;
+            const int x = x0 + k;
+            float val;
+            if (x == 0 || x >= nx - 1) {
+                val = c[k];
+            } else {
+                float s = E + Wv;
+                s = s + N[k];
+                s = s + S[k];
+                s = s + U[k];
+                s = s + D[k];
+                val = sixth * (s - (h2 * dv[k]) / dt);
+            }
+            if (MASK && mk[k]) val = 0.f;
+            o[k] = val;
+            if (RESID) {
+                const float ch = fabsf(val - c[k]);
+                if (ch > rmax) rmax = ch;
+            }
+        }
+        if (ok) st4(out + (size_t)z * plane + rofs, make_float4(o[0], o[1], o[2], o[3]));
+        dn = cur;
+        cur = up;
+        up = up2;
+        if (!USE_LDS) {
+            nn = nn_next;
+            ss = ss_next;
+        }
+        hlo = hlo_next;
+        hhi = hhi_next;
+        cl = nl;
+        cr = nr;
+    }
+    if (RESID) wave_reduce_max_store(rmax, resid);
+}
+
+// Scalar fallback for nx % 4 != 0 or unaligned arrays (small parity cases):
+// one thread per cell, all 7 neighbours from global.
+template <bool MASK>
+__global__ __launch_bounds__(256) void jacobi3d_scalar(const float *__restrict__ in,
+                                                       float *__restrict__ out,
+                                                       const float *__restrict__ div,
+                                                       const uint8_t *__restrict__ mask, int ny,
+                                                       int nx, int zb, float h2, float dt,
+                                                       float *__restrict__ resid) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y + 1;
+    const int z = blockIdx.z + zb;
+    float ch = 0.f;
+    if (x < nx) {
+        const size_t plane = (size_t)ny * nx;
+        const size_t c = (size_t)z * plane + (size_t)y * nx + x;
+        float val;
+        if (x == 0 || x == nx - 1) {
+            val = in[c];
+        } else {
+            float s = in[c + 1] + in[c - 1];
+            s = s + in[c + nx];
+            s = s + in[c - nx];
+            s = s + in[c + plane];
+            s = s + in[c - plane];
+            val = (1.0f / 6.0f) * (s - (h2 * div[c]) / dt);
+        }
+        if (MASK && mask[c]) val = 0.f;
+        out[c] = val;
+        ch = fabsf(val - in[c]);
+        if (!(ch > 0.f)) ch = 0.f;
+    }
+    if (resid) wave_reduce_max_store(ch, resid);
+}
+
+template <int W, bool USE_LDS>
+static void launch_march(const float *in, float *out, const float *div, const uint8_t *mask,
+                         int ny, int nx, int zb, int ze, int zchunk, float h2, float dt,
+                         float *resid, hipStream_t s) {
+    const int nseg = ceil_div(nx, 256);
+    const int ntile_y = ceil_div(ny - 2, W);
+    const int nzc = ceil_div(ze - zb, zchunk);
+    const int blocks = nseg * ntile_y * nzc;
+#define CFD_J3_LAUNCH(R, M)                                                                    \
+    hipLaunchKernelGGL((jacobi3d_march<W, USE_LDS, R, M>), dim3(blocks), dim3(W * 64), 0, s, in, \
+                       out, div, mask, ny, nx, nseg, ntile_y, zb, ze, zchunk, h2, dt, resid)
+    if (resid) {
+        if (mask) CFD_J3_LAUNCH(true, true); else CFD_J3_LAUNCH(true, false);
+    } else {
+        if (mask) CFD_J3_LAUNCH(false, true); else CFD_J3_LAUNCH(false, false);
+    }
+#undef CFD_J3_LAUNCH
+}
+
+// Sweep planes [zb, ze) of in -> out (local array of nz planes).
+static int jacobi3d_sweep(const float *in, float *out, const float *div, const uint8_t *mask,
+                          int nz, int ny, int nx, int zb, int ze, float h2, float dt,
+                          float *resid, hipStream_t s) {
+    if (ze <= zb || ny < 3) return CFD_OK;
+    CFD_REQUIRE(zb >= 1 && ze <= nz - 1, "jacobi3d sweep: z range [%d,%d) outside 1..%d", zb, ze,
+                nz - 1);
+    const bool vec_ok = nx % 4 == 0 && aligned16(in) && aligned16(out) && aligned16(div) &&
+                        (!mask || (reinterpret_cast<uintptr_t>(mask) & 3u) == 0);
+    if (!vec_ok) {
+        dim3 grid(ceil_div(nx, 256), ny - 2, ze - zb);
+        if (mask)
+            hipLaunchKernelGGL(jacobi3d_scalar<true>, grid, dim3(256), 0, s, in, out, div, mask, ny,
+                               nx, zb, h2, dt, resid);
+        else
+            hipLaunchKernelGGL(jacobi3d_scalar<false>, grid, dim3(256), 0, s, in, out, div, mask,
+                               ny, nx, zb, h2, dt, resid);
+        CFD_LAUNCH_CHECK();
+        return CFD_OK;
+    }
+    int variant = g_j3.variant ? g_j3.variant : 1;
+    int W = g_j3.waves ? g_j3.waves : 4;
+    const int nseg = ceil_div(nx, 256);
+    const int L = ze - zb;
+    int zchunk = g_j3.zchunk;
+    if (zchunk <= 0) {
+        // aim for ~2048 workgroups (8 per CU) but keep >= 16 planes per march
+        const long tiles = (long)nseg * ceil_div(ny - 2, W);
+        int nzc = (int)((2048 + tiles - 1) / tiles);
+        if (nzc < 1) nzc = 1;
+        zchunk = ceil_div(L, nzc);
+        if (zchunk < 16) zchunk = 16;
+    }
+    if (zchunk > L) zchunk = L;
+#define CFD_J3_W(WV)                                                                           \
+    case WV:                                                                                   \
+        if (variant == 2)                                                                      \
+            launch_march<WV, false>(in, out, div, mask, ny, nx, zb, ze, zchunk, h2, dt, resid, s); \
+        else                                                                                   \
+            launch_march<WV, true>(in, out, div, mask, ny, nx, zb, ze, zchunk, h2, dt, resid, s);  \
+        break;
+    switch (W) {
+        CFD_J3_W(1)
+        CFD_J3_W(2)
+        CFD_J3_W(4)
+        CFD_J3_W(8)
+        CFD_J3_W(16)
+        default:
+            set_error("jacobi3d: unsupported waves-per-workgroup %d", W);
+            return CFD_E_INVALID;
+    }
+#undef CFD_J3_W
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// ----------------------------------------------------------- red-black GS 3-D
+struct RbgsWs {
+    int flags[4];
+    float maxc[1];
+};
+int launch_rbgs_init(RbgsWs *ws, int iterations, int *iters_done, hipStream_t s);
+
+template <int C>
+__global__ __launch_bounds__(256) void rbgs3d_color(float *__restrict__ phi,
+                                                    const float *__restrict__ div,
+                                                    const uint8_t *__restrict__ mask, int ny,
+                                                    int nx, float cx, float cy, float cz, float cd,
+                                                    float dt_inv, float tol, RbgsWs *ws, int it,
+                                                    int *iters_done) {
+    if (it > 0 && ws->maxc[it - 1] < tol) {
+        if (C == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0 &&
+            iters_done)
+            atomicMin(iters_done, it);
+        return;
+    }
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y + 1;
+    const int z = blockIdx.z + 1;
+    float mx = 0.f;
+    // colour c: (z + i + j + 1 + c) even; j from the first cell of that colour
+    if (x < nx - 1 && x >= 1 && ((z + i + x + 1 + C) & 1) == 0) {
+        const size_t plane = (size_t)ny * nx;
+        const size_t c = (size_t)z * plane + (size_t)i * nx + x;
+        if (!(mask && mask[c])) {
+            const float rhs = -div[c] * dt_inv;
+            const float a = cx * (phi[c + 1] + phi[c - 1]);
+            const float b = cy * (phi[c + nx] + phi[c - nx]);
+            const float e = cz * (phi[c + plane] + phi[c - plane]);
+            const float pn = (((a + b) + e) - rhs) * cd;
+            const float ch = fabsf(pn - phi[c]);
+            if (ch > mx) mx = ch;
+            phi[c] = pn;
+        }
+    }
+    wave_reduce_max_store(mx, &ws->maxc[it]);
+}
+
+}  // namespace cfd
+
+using namespace cfd;
+
+extern "C" {
+
+int cfd_set_jacobi3d_config(int variant, int waves, int zchunk) {
+    CFD_REQUIRE(variant >= 0 && variant <= 2, "variant must be 0..2");
+    CFD_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8 || waves == 16,
+                "waves must be 0,1,2,4,8,16");
+    CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
+    g_j3.variant = variant;
+    g_j3.waves = waves;
+    g_j3.zchunk = zchunk;
+    return CFD_OK;
+}
+
+int cfd_jacobi3d_sweep_f32(const float *in, float *out, const float *div, const uint8_t *mask,
+                           int nz, int ny, int nx, int z_begin, int z_end, double h, float dt,
+                           float *resid, void *stream) {
+    CFD_REQUIRE(in && out && div, "jacobi3d_sweep: null pointer");
+    CFD_REQUIRE(nz >= 1 && ny >= 1 && nx >= 1, "jacobi3d_sweep: bad shape");
+    return jacobi3d_sweep(in, out, div, mask, nz, ny, nx, z_begin, z_end, (float)(h * h), dt,
+                          resid, as_stream(stream));
+}
+
+int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t *mask, int nz,
+                     int ny, int nx, double h, float dt, int iters, int resid_every,
+                     float *resid_out, void *stream) {
+    CFD_REQUIRE(div && phi && phi_tmp, "jacobi3d: null array pointer");
+    CFD_REQUIRE(nz >= 1 && ny >= 1 && nx >= 1 && iters >= 0, "jacobi3d: bad arguments");
+    CFD_REQUIRE(resid_every <= 0 || resid_out, "jacobi3d: resid_every > 0 needs resid_out");
+    if (iters == 0) return CFD_OK;
+    hipStream_t s = as_stream(stream);
+    const size_t plane = (size_t)ny * nx;
+    int rc;
+    // Dirichlet faces the sweep never writes (planes 0, nz-1; rows 0, ny-1),
+    // identical in both buffers, masked -> 0
+    if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, 0, nz, 0, nz - 1, s))) return rc;
+    const int nres = resid_every > 0 ? iters / resid_every : 0;
+    if (nres > 0) CFD_CHECK_HIP(hipMemsetAsync(resid_out, 0, sizeof(float) * nres, s));
+    const float h2 = (float)(h * h);
+    float *a = phi, *b = phi_tmp;
+    const int tk = timing_begin(s);
+    for (int it = 0; it < iters; ++it) {
+        float *r = (resid_every > 0 && (it + 1) % resid_every == 0)
+                       ? resid_out + ((it + 1) / resid_every - 1)
+                       : nullptr;
+        if ((rc = jacobi3d_sweep(a, b, div, mask, nz, ny, nx, 1, nz - 1, h2, dt, r, s))) return rc;
+        float *t = a;
+        a = b;
+        b = t;
+    }
+    timing_end(tk, s, iters);
+    if (a != phi)
+        CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(float) * plane * nz, hipMemcpyDeviceToDevice, s));
+    return CFD_OK;
+}
+
+int cfd_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask, int nz, int ny, int nx,
+                   double dx, double dy, double dz, float dt, int iterations, double tolerance,
+                   float *phi_tmp, void *ws, int *iters_done, void *stream) {
+    (void)phi_tmp;
+    CFD_REQUIRE(phi && div && ws, "rbgs3d: null pointer");
+    CFD_REQUIRE(nz >= 1 && ny >= 1 && nx >= 1 && iterations >= 0, "rbgs3d: bad arguments");
+    hipStream_t s = as_stream(stream);
+    const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy), dz2_inv = 1.0 / (dz * dz);
+    const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv + dz2_inv));
+    const float cx = (float)dx2_inv, cy = (float)dy2_inv, cz = (float)dz2_inv, cd = (float)denom_inv;
+    const float dt_inv = 1.0f / dt;
+    const float tol = (float)tolerance;
+    RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
+    int rc = launch_rbgs_init(w, iterations, iters_done, s);
+    if (rc) return rc;
+    if (nz < 3 || ny < 3 || nx < 3) return CFD_OK;
+    dim3 grid(ceil_div(nx, 256), ny - 2, nz - 2);
+    const int tk = timing_begin(s);
+    for (int it = 0; it < iterations; ++it) {
+        hipLaunchKernelGGL(rbgs3d_color<0>, grid, dim3(256), 0, s, phi, div, mask, ny, nx, cx, cy,
+                           cz, cd, dt_inv, tol, w, it, iters_done);
+        hipLaunchKernelGGL(rbgs3d_color<1>, grid, dim3(256), 0, s, phi, div, mask, ny, nx, cx, cy,
+                           cz, cd, dt_inv, tol, w, it, iters_done);
+        CFD_LAUNCH_CHECK();
+    }
+    timing_end(tk, s, 2LL * iterations);
+    return CFD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,218 @@
+"""Reference-named device kernels: drop-ins for the @njit functions of v5.py.
+
+Each function keeps the name, argument order and meaning, and the ownership
+rules of its reference counterpart in
+``python/flow_over_cylinder (Fischer)/v5.py``.  Allocating kernels return fresh
+arrays with a zero boundary ring (``np.zeros_like``).  GS, IBM and
+divergence cleaning mutate their inputs in place and return them.  The arrays
+are torch tensors on the HIP device.  The work runs in the hand-written gfx950
+kernels of libcfdsim.so, on the current torch stream.  Nothing here falls back
+to the CPU: CPU tensors raise ``TypeError``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._lib import call, ptr, stream_handle, lib
+
+__all__ = [
+    "compute_convection_fast", "compute_convection_supg_fast", "compute_supg_stabilization_fast",
+    "compute_laplacian_fast", "compute_divergence_fast", "compute_gradient_fast",
+    "solve_pressure_gauss_seidel_fast", "solve_pressure_jacobi", "apply_ibm_fast",
+    "clean_divergence_fast", "predictor_fused", "project_velocity", "solve_pressure_jacobi3d",
+    "solve_pressure_gauss_seidel3d",
+]
+
+
+def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (memory_efficient fields), got {t.dtype}")
+    return t
+
+
+def _shape2d(t: torch.Tensor):
+    if t.dim() != 2:
+        raise ValueError(f"expected a 2-D (ny, nx) array, got shape {tuple(t.shape)}")
+    return int(t.shape[0]), int(t.shape[1])
+
+
+def _mask_u8(mask, shape):
+    if mask is None:
+        return None
+    if tuple(mask.shape) != tuple(shape):
+        raise ValueError(f"mask shape {tuple(mask.shape)} != field shape {tuple(shape)}")
+    m = mask if mask.dtype == torch.uint8 else mask.to(torch.uint8)
+    return m.contiguous()
+
+
+def _nu(nu_eff):
+    """nu_eff as (array_or_None, scalar): an array is passed through, a scalar
+    (LES off: nu + 0 + art_visc, v5.py:388) is broadcast by the kernel."""
+    if isinstance(nu_eff, torch.Tensor) and nu_eff.dim() > 0:
+        return _f32(nu_eff, "nu_eff").contiguous(), 0.0
+    return None, float(np.float32(nu_eff))
+
+
+def compute_supg_stabilization_fast(u, v, dx, dy, dt, nu_eff):
+    """v5.py:149-162."""
+    ny, nx = _shape2d(u)
+    tau = torch.empty_like(u)
+    nu_a, nu_s = _nu(nu_eff)
+    call("cfd_supg_tau2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(nu_a), nu_s, ptr(tau), ny, nx,
+         float(dx), float(dy), float(np.float32(dt)), stream_handle())
+    return tau
+
+
+def compute_convection_supg_fast(u, v, phi, dx, dy, tau_supg):
+    """v5.py:127-147 (derivative factors 1/(4dx), 1/(4dx^2): the reference's quirk)."""
+    ny, nx = _shape2d(phi)
+    conv = torch.empty_like(phi)
+    call("cfd_convection_supg2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(_f32(phi, "phi")),
+         ptr(_f32(tau_supg, "tau_supg")), ptr(conv), ny, nx, float(dx), float(dy), stream_handle())
+    return conv
+
+
+def compute_convection_fast(u, v, phi, dx, dy):
+    """First-order upwind convection, v5.py:112-125."""
+    ny, nx = _shape2d(phi)
+    conv = torch.empty_like(phi)
+    call("cfd_convection_upwind2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(_f32(phi, "phi")),
+         ptr(conv), ny, nx, float(dx), float(dy), stream_handle())
+    return conv
+
+
+def compute_laplacian_fast(phi, dx, dy, nu_eff):
+    """v5.py:164-176."""
+    ny, nx = _shape2d(phi)
+    lap = torch.empty_like(phi)
+    nu_a, nu_s = _nu(nu_eff)
+    call("cfd_laplacian2d_f32", ptr(_f32(phi, "phi")), ptr(nu_a), nu_s, ptr(lap), ny, nx, float(dx),
+         float(dy), stream_handle())
+    return lap
+
+
+def compute_divergence_fast(u, v, dx, dy, absmax=None):
+    """v5.py:178-187.  ``absmax``: optional zeroed device float32 scalar that
+    receives max|div| (the v5.py:410 diagnostic) without a host sync."""
+    ny, nx = _shape2d(u)
+    div = torch.empty_like(u)
+    call("cfd_divergence2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(div), ny, nx, float(dx),
+         float(dy), ptr(absmax), stream_handle())
+    return div
+
+
+def compute_gradient_fast(phi, dx, dy):
+    """v5.py:189-200."""
+    ny, nx = _shape2d(phi)
+    gx, gy = torch.empty_like(phi), torch.empty_like(phi)
+    call("cfd_gradient2d_f32", ptr(_f32(phi, "phi")), ptr(gx), ptr(gy), ny, nx, float(dx), float(dy),
+         stream_handle())
+    return gx, gy
+
+
+def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iterations, tolerance,
+                                     workspace=None, iters_done=None):
+    """v5.py:202-226: red-black GS, in place on ``phi``; returns ``phi``.
+    ``iters_done`` (optional int32 device scalar) receives the iteration count."""
+    ny, nx = _shape2d(phi)
+    m = _mask_u8(mask, phi.shape)
+    ws = workspace
+    need = int(lib().cfd_rbgs_workspace_bytes(int(iterations)))
+    if ws is None or ws.numel() * ws.element_size() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
+    call("cfd_rbgs2d_f32", ptr(_f32(phi, "phi")), ptr(_f32(div_u_star, "div_u_star")), ptr(m), ny, nx,
+         float(dx), float(dy), float(np.float32(dt)), int(iterations), float(tolerance), None,
+         ptr(ws), ptr(iters_done), stream_handle())
+    return phi
+
+
+def solve_pressure_jacobi(phi, div_u_star, dx, dt, mask, iterations, phi_tmp=None,
+                          resid_every=0, resid_out=None):
+    """Jacobi branch of solve_pressure_fast, v5.py:336-346, bit-exact; in place
+    on ``phi`` (float32 or float64 fields); returns ``phi``."""
+    ny, nx = _shape2d(phi)
+    if div_u_star.dtype != phi.dtype:
+        raise TypeError("phi and div_u_star must share a dtype")
+    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
+    m = _mask_u8(mask, phi.shape)
+    fn = {torch.float32: "cfd_jacobi2d_f32", torch.float64: "cfd_jacobi2d_f64"}.get(phi.dtype)
+    if fn is None:
+        raise TypeError(f"unsupported dtype {phi.dtype}")
+    call(fn, ptr(div_u_star), ptr(phi), ptr(tmp), ptr(m), ny, nx, float(dx), float(np.float32(dt)),
+         int(iterations), int(resid_every), ptr(resid_out), stream_handle())
+    return phi
+
+
+def solve_pressure_jacobi3d(phi, div, h, dt, mask, iterations, phi_tmp=None, resid_every=0,
+                            resid_out=None):
+    """7-point generalisation of the Jacobi branch on an (nz, ny, nx) float32 grid."""
+    if phi.dim() != 3:
+        raise ValueError("expected (nz, ny, nx)")
+    nz, ny, nx = (int(s) for s in phi.shape)
+    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
+    m = _mask_u8(mask, phi.shape)
+    call("cfd_jacobi3d_f32", ptr(_f32(div, "div")), ptr(_f32(phi, "phi")), ptr(tmp), ptr(m), nz, ny, nx,
+         float(h), float(np.float32(dt)), int(iterations), int(resid_every), ptr(resid_out),
+         stream_handle())
+    return phi
+
+
+def solve_pressure_gauss_seidel3d(phi, div, dx, dy, dz, dt, mask, iterations, tolerance,
+                                  workspace=None, iters_done=None):
+    """3-D red-black generalisation of v5.py:202-226, in place on ``phi``."""
+    nz, ny, nx = (int(s) for s in phi.shape)
+    m = _mask_u8(mask, phi.shape)
+    need = int(lib().cfd_rbgs_workspace_bytes(int(iterations)))
+    ws = workspace
+    if ws is None or ws.numel() * ws.element_size() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
+    call("cfd_rbgs3d_f32", ptr(_f32(phi, "phi")), ptr(_f32(div, "div")), ptr(m), nz, ny, nx, float(dx),
+         float(dy), float(dz), float(np.float32(dt)), int(iterations), float(tolerance), None, ptr(ws),
+         ptr(iters_done), stream_handle())
+    return phi
+
+
+def apply_ibm_fast(u, v, ibm_mask, force_strength):
+    """v5.py:228-237, in place; ``ibm_mask`` is the float64 mask. Returns (u, v)."""
+    if ibm_mask.dtype != torch.float64:
+        raise TypeError("ibm_mask is float64 in the reference (v5.py:281-283)")
+    call("cfd_apply_ibm2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(ibm_mask), int(u.numel()),
+         float(force_strength), stream_handle())
+    return u, v
+
+
+def clean_divergence_fast(u, v, dx, dy, iterations=2, workspace=None):
+    """v5.py:239-257, in place; serial (lexicographic) order of the phi sweep."""
+    ny, nx = _shape2d(u)
+    need = int(lib().cfd_clean_divergence_workspace_bytes(ny, nx))
+    ws = workspace
+    if ws is None or ws.numel() * ws.element_size() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=u.device)
+    call("cfd_clean_divergence2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ny, nx, float(dx), float(dy),
+         int(iterations), ptr(ws), stream_handle())
+    return u, v
+
+
+def predictor_fused(u, v, dx, dy, dt, nu_eff, use_supg=True, u_star=None, v_star=None, tau=None):
+    """v5.py:388-403 in one pass: returns (u_star, v_star, tau)."""
+    ny, nx = _shape2d(u)
+    us = torch.empty_like(u) if u_star is None else u_star
+    vs = torch.empty_like(v) if v_star is None else v_star
+    if tau is None and use_supg:
+        tau = torch.empty_like(u)
+    nu_a, nu_s = _nu(nu_eff)
+    call("cfd_predictor2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(nu_a), nu_s, ptr(us), ptr(vs),
+         ptr(tau) if use_supg else None, ny, nx, float(dx), float(dy), float(np.float32(dt)),
+         int(bool(use_supg)), stream_handle())
+    return us, vs, tau
+
+
+def project_velocity(phi, u_star, v_star, dx, dy, dt, u=None, v=None, gradmax=None):
+    """v5.py:413-417: u = u* - dt*dphi/dx, v = v* - dt*dphi/dy.  Returns (u, v)."""
+    ny, nx = _shape2d(phi)
+    u = torch.empty_like(u_star) if u is None else u
+    v = torch.empty_like(v_star) if v is None else v
+    call("cfd_project2d_f32", ptr(phi), ptr(u_star), ptr(v_star), ptr(u), ptr(v), ny, nx, float(dx),
+         float(dy), float(np.float32(dt)), ptr(gradmax), stream_handle())
+    return u, v

@@ -1,0 +1,182 @@
+"""Slab decomposition of the 3-D Poisson grid across GPUs (one process per GPU).
+
+The reference runs on one node's CPU threads (SURVEY.md section 2,
+"Parallelism").  Here the (nz, ny, nx) grid is cut on the slowest axis.  Each
+rank holds its owned planes plus one ghost plane per side.  After every sweep
+the ranks swap boundary planes with their z-neighbours over RCCL send/recv
+(xGMI), and that swap overlaps the interior sweep on a second HIP stream.
+Jacobi updates reassociate nothing across planes, so the decomposed result is
+bit-identical to the single-GPU one for every rank count.
+
+``SlabPlan`` is pure host logic: ownership, peers, update range and the
+exchange list.  The C driver ``cfd_slab_jacobi3d_f32`` executes the same
+exchange list: it sends plane 1 to ``lo_peer`` into that rank's ghost plane
+``nz_local+1``, and plane ``nz_local`` to ``hi_peer`` into its ghost plane 0.
+The CPU tests run the plan on gloo with world_size 2.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ._lib import call, lib, ptr, stream_handle
+
+UNIQUE_ID_BYTES = 128
+
+
+@dataclass(frozen=True)
+class SlabPlan:
+    nz: int        # global planes
+    nranks: int
+    rank: int
+
+    def __post_init__(self):
+        if not (0 <= self.rank < self.nranks):
+            raise ValueError("rank out of range")
+        if self.nz < self.nranks:
+            raise ValueError(f"cannot split {self.nz} planes over {self.nranks} ranks")
+
+    @property
+    def z_lo(self) -> int:
+        """First owned global plane (near-equal split, remainder to low ranks)."""
+        q, r = divmod(self.nz, self.nranks)
+        return self.rank * q + min(self.rank, r)
+
+    @property
+    def z_hi(self) -> int:
+        q, r = divmod(self.nz, self.nranks)
+        return self.z_lo + q + (1 if self.rank < r else 0)
+
+    @property
+    def nz_local(self) -> int:
+        return self.z_hi - self.z_lo
+
+    @property
+    def lo_peer(self) -> int:
+        return self.rank - 1 if self.rank > 0 else -1
+
+    @property
+    def hi_peer(self) -> int:
+        return self.rank + 1 if self.rank < self.nranks - 1 else -1
+
+    @property
+    def z_update_begin(self) -> int:
+        """Local index of the first updated plane (global plane 0 is Dirichlet)."""
+        return 2 if self.z_lo == 0 else 1
+
+    @property
+    def z_update_end(self) -> int:
+        """Local index one past the last updated plane (global nz-1 is Dirichlet)."""
+        return self.nz_local if self.z_hi == self.nz else self.nz_local + 1
+
+    def exchanges(self):
+        """[(send_local_plane, peer, peer_recv_local_plane_on_that_rank)]: the
+        list the C driver executes after each sweep."""
+        out = []
+        if self.lo_peer >= 0:
+            lo = SlabPlan(self.nz, self.nranks, self.lo_peer)
+            out.append((1, self.lo_peer, lo.nz_local + 1))
+        if self.hi_peer >= 0:
+            out.append((self.nz_local, self.hi_peer, 0))
+        return out
+
+    def local_slice(self):
+        """Global planes held locally, ghosts included (clipped at the faces)."""
+        return slice(max(self.z_lo - 1, 0), min(self.z_hi + 1, self.nz))
+
+    def scatter(self, glob: np.ndarray) -> np.ndarray:
+        """Local (nz_local+2, ny, nx) view-copy of a global array; ghost planes
+        outside the domain are zero."""
+        loc = np.zeros((self.nz_local + 2,) + glob.shape[1:], glob.dtype)
+        lo = self.z_lo - 1
+        for k in range(self.nz_local + 2):
+            g = lo + k
+            if 0 <= g < self.nz:
+                loc[k] = glob[g]
+        return loc
+
+
+def comm_unique_id() -> bytes:
+    import ctypes
+    cbuf = (ctypes.c_char * UNIQUE_ID_BYTES)()
+    call("cfd_comm_unique_id", ctypes.addressof(cbuf), UNIQUE_ID_BYTES)
+    return bytes(cbuf.raw)
+
+
+class RcclComm:
+    """An RCCL communicator owned by libcfdsim (ncclCommInitRank on the current
+    device).  The unique id travels over the torch.distributed process group."""
+
+    def __init__(self, rank: int, nranks: int, group=None):
+        import ctypes
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and nranks > 1:
+            dev = torch.device("cuda", torch.cuda.current_device()) \
+                if dist.get_backend(group) == "nccl" else torch.device("cpu")
+            t = torch.zeros(UNIQUE_ID_BYTES, dtype=torch.uint8, device=dev)
+            if rank == 0:
+                t.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
+            dist.broadcast(t, src=0, group=group)
+            uid = bytes(t.cpu().numpy().tobytes())
+        else:
+            uid = comm_unique_id()
+        cbuf = (ctypes.c_char * UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        handle = ctypes.c_void_p()
+        call("cfd_comm_init", ctypes.addressof(cbuf), int(nranks), int(rank), ctypes.byref(handle))
+        self.handle = handle
+        self.rank, self.nranks = rank, nranks
+
+    def close(self):
+        if self.handle:
+            call("cfd_comm_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SlabJacobi3D:
+    """Distributed 7-point Jacobi on this rank's slab (device tensors)."""
+
+    def __init__(self, plan: SlabPlan, ny: int, nx: int, h: float, dt, comm: RcclComm | None,
+                 device=None, mask=None):
+        self.plan, self.ny, self.nx = plan, ny, nx
+        self.h, self.dt = float(h), np.float32(dt)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        shape = (plan.nz_local + 2, ny, nx)
+        self.div = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        self.phi = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        self.tmp = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        self.mask = None if mask is None else mask.to(torch.uint8).contiguous()
+        self.comm = comm
+        self.comm_stream = torch.cuda.Stream(device=self.device)
+
+    def solve(self, iters: int, overlap: bool = True, zero_phi: bool = True):
+        if zero_phi:
+            self.phi.zero_()
+        p = self.plan
+        call("cfd_slab_jacobi3d_f32", self.comm.handle, ptr(self.div), ptr(self.phi), ptr(self.tmp),
+             ptr(self.mask), p.nz_local, self.ny, self.nx, p.lo_peer, p.hi_peer, p.z_update_begin,
+             p.z_update_end, self.h, float(self.dt), int(iters), int(bool(overlap)), stream_handle(),
+             self.comm_stream.cuda_stream)
+        return self.phi
+
+    def owned(self) -> torch.Tensor:
+        return self.phi[1:self.plan.nz_local + 1]
+
+
+def sweep_range(phi_in, phi_out, div, mask, z_begin, z_end, h, dt, resid=None):
+    """One Jacobi sweep of planes [z_begin, z_end) of a local (nz, ny, nx) array
+    (cfd_jacobi3d_sweep_f32, the slab driver's building block)."""
+    nz, ny, nx = (int(s) for s in phi_in.shape)
+    call("cfd_jacobi3d_sweep_f32", ptr(phi_in), ptr(phi_out), ptr(div),
+         ptr(None if mask is None else mask), nz, ny, nx, int(z_begin), int(z_end), float(h),
+         float(np.float32(dt)), ptr(resid), stream_handle())
+
+
+__all__ = ["SlabPlan", "RcclComm", "SlabJacobi3D", "sweep_range", "comm_unique_id", "lib"]

@@ -1,0 +1,207 @@
+/*
+ * cfdsim.h -- C ABI of the MI355X-native pressure-Poisson / predictor hot path.
+ *
+ * This is the drop-in boundary for the numba-compiled kernels and the two solver
+ * methods of the reference cylinder solver
+ *   python/flow_over_cylinder (Fischer)/v5.py            (cited as "v5.py:<line>")
+ * The reference has no FFI of its own: its boundary is numba's @njit dispatcher
+ * (module-level functions, v5.py:96-257) and OptimizedTurbulentSolver's
+ * solve_pressure_fast / time_step (v5.py:328, :375).  Each entry point below
+ * states the reference symbol it replaces.  INTEGRATION.md shows the ctypes
+ * binding a maintainer adds on the reference side.
+ *
+ * Conventions (all entry points):
+ *  - Arrays are caller-owned DEVICE pointers (hipMalloc'd or from any allocator
+ *    on the current HIP device), C order, x fastest: 2-D (ny, nx), 3-D
+ *    (nz, ny, nx).  Sizes are plain ints.  Nothing is allocated on the hot path.
+ *    Workspaces are passed in by the caller, sized by the *_workspace_* helpers.
+ *  - `stream` is a hipStream_t passed as void* (NULL = the default stream).
+ *    Every call is asynchronous on that stream, with no host synchronisation,
+ *    so it can be captured into a hipGraph.
+ *  - Return 0 on success, or a negative CFD_E_* code; cfd_last_error() then
+ *    gives a thread-local message.  NaN/Inf propagate like the reference
+ *    (no numerical error codes, v5.py:599-613 detects them at the driver).
+ *  - mask: optional uint8 (ny,nx)/(nz,ny,nx), nonzero = solid cell
+ *    (cylinder_mask, v5.py:279); NULL = no solid cells.
+ *  - Scalars keep the reference's meaning and type: dx/dy are Python floats
+ *    (double here), dt is np.float32 (float here).  The library rounds derived
+ *    constants exactly as NumPy's NEP-50 promotion does in the reference.
+ */
+#ifndef CFDSIM_H
+#define CFDSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFD_ABI_VERSION 1
+
+#define CFD_OK 0
+#define CFD_E_INVALID (-1)   /* bad argument (shape, pointer, alignment) */
+#define CFD_E_HIP (-2)       /* a HIP runtime call failed */
+#define CFD_E_COMM (-3)      /* an RCCL call failed */
+#define CFD_E_UNSUPPORTED (-4)
+
+int cfd_abi_version(void);
+const char *cfd_last_error(void);
+/* Name of the gfx target the library's device code was built for ("gfx950"). */
+const char *cfd_device_arch(void);
+
+/* ------------------------------------------------------------------ Poisson */
+
+/* Replaces the Jacobi branch of OptimizedTurbulentSolver.solve_pressure_fast,
+ * v5.py:336-346 (use_fast_pressure=False):
+ *   repeat iters: phi_new = phi; phi_new[1:-1,1:-1] =
+ *       0.25*(E + W + N + S - f32(dx**2)*div/dt);  phi_new[mask] = 0
+ * Bit-exact with the reference (same op order, no FMA contraction).
+ * phi (in/out) holds the initial guess; the reference zero-fills it first
+ * (v5.py:337); the caller does that.  phi_tmp is a same-size scratch array.
+ * Edges keep their values (Dirichlet), except masked edge cells -> 0.
+ * resid_every > 0: after every resid_every-th iteration k, max|phi_new - phi|
+ * over updated cells is written to resid_out[k/resid_every - 1] (device array
+ * of floor(iters/resid_every) elements; an extension, the reference has none). */
+int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t *mask,
+                     int ny, int nx, double dx, float dt, int iters,
+                     int resid_every, float *resid_out, void *stream);
+/* fp64 fields (memory_efficient=False, v5.py:287); dt promotes exactly. */
+int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, const uint8_t *mask,
+                     int ny, int nx, double dx, float dt, int iters,
+                     int resid_every, double *resid_out, void *stream);
+
+/* 3-D 7-point generalisation of the same Jacobi template (the reference is
+ * 2-D only): phi_new = f32(1/6) * (((((E+W)+N)+S)+U)+D - f32(h*h)*div/dt),
+ * six Dirichlet faces held, mask -> 0.  Layout (nz, ny, nx). */
+int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t *mask,
+                     int nz, int ny, int nx, double h, float dt, int iters,
+                     int resid_every, float *resid_out, void *stream);
+
+/* Replaces solve_pressure_gauss_seidel_fast, v5.py:202-226 (the
+ * use_fast_pressure=True branch, v5.py:330-335): red-black Gauss-Seidel in
+ * place on phi; colour 0 = cells with (i+j) odd first; masked cells skipped;
+ * stop after the first iteration whose max|change| < tolerance.
+ * phi_tmp: same-size scratch.  ws: cfd_rbgs_workspace_bytes(iterations) bytes.
+ * iters_done (device int*, optional) receives the iteration count executed. */
+size_t cfd_rbgs_workspace_bytes(int iterations);
+int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, int nx,
+                   double dx, double dy, float dt, int iterations, double tolerance,
+                   float *phi_tmp, void *ws, int *iters_done, void *stream);
+/* 3-D red-black generalisation: colour c updates (z+i+j) parity == (1+c)%2. */
+int cfd_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask, int nz, int ny, int nx,
+                   double dx, double dy, double dz, float dt, int iterations, double tolerance,
+                   float *phi_tmp, void *ws, int *iters_done, void *stream);
+
+/* ---------------------------------------------------------------- predictor */
+
+/* compute_supg_stabilization_fast, v5.py:149-162.  nu_eff: (ny,nx) array or
+ * NULL to use nu_eff_scalar everywhere (LES off: nu_t == 0, v5.py:386-388). */
+int cfd_supg_tau2d_f32(const float *u, const float *v, const float *nu_eff, float nu_eff_scalar,
+                       float *tau, int ny, int nx, double dx, double dy, float dt, void *stream);
+/* compute_convection_supg_fast, v5.py:127-147 (phi is u or v). */
+int cfd_convection_supg2d_f32(const float *u, const float *v, const float *phi, const float *tau,
+                              float *conv, int ny, int nx, double dx, double dy, void *stream);
+/* compute_convection_fast (first-order upwind), v5.py:112-125. */
+int cfd_convection_upwind2d_f32(const float *u, const float *v, const float *phi, float *conv,
+                                int ny, int nx, double dx, double dy, void *stream);
+/* compute_laplacian_fast, v5.py:164-176. */
+int cfd_laplacian2d_f32(const float *phi, const float *nu_eff, float nu_eff_scalar, float *lap,
+                        int ny, int nx, double dx, double dy, void *stream);
+/* Fused predictor, v5.py:388-403: tau (SUPG), conv_u/v, lap_u/v and
+ *   u_star = u + dt*(-conv_u + lap_u),  v_star = v + dt*(-conv_v + lap_v)
+ * in one pass over u, v.  tau may be NULL (not stored). */
+int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, float nu_eff_scalar,
+                        float *u_star, float *v_star, float *tau, int ny, int nx,
+                        double dx, double dy, float dt, int use_supg, void *stream);
+
+/* compute_divergence_fast, v5.py:178-187.  absmax (device float*, optional):
+ * receives max|div| (the v5.py:410 diagnostic); must be zeroed by the caller. */
+int cfd_divergence2d_f32(const float *u, const float *v, float *div, int ny, int nx,
+                         double dx, double dy, float *absmax, void *stream);
+/* compute_gradient_fast, v5.py:189-200. */
+int cfd_gradient2d_f32(const float *phi, float *grad_x, float *grad_y, int ny, int nx,
+                       double dx, double dy, void *stream);
+/* Gradient + projection, v5.py:413-417: u = u_star - dt*dphi/dx, v likewise.
+ * gradmax (optional, zeroed by caller): max sqrt(gx^2+gy^2) (v5.py:414-415). */
+int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star,
+                      float *u, float *v, int ny, int nx, double dx, double dy, float dt,
+                      float *gradmax, void *stream);
+
+/* ----------------------------------------------------------- step epilogue */
+
+/* clean_divergence_fast, v5.py:239-257, with the serial (lexicographic)
+ * Gauss-Seidel order of its phi sweep as the defined semantics (under numba's
+ * prange that sweep races).  ws: cfd_clean_divergence_workspace_bytes(ny,nx). */
+size_t cfd_clean_divergence_workspace_bytes(int ny, int nx);
+int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, double dy,
+                               int iterations, void *ws, void *stream);
+/* OptimizedTurbulentSolver.apply_boundary_conditions, v5.py:349-360.
+ * y: device float64 (ny) grid coordinates (np.linspace, v5.py:272). */
+int cfd_apply_bc2d_f32(float *u, float *v, const double *y, int ny, int nx, double y_max,
+                       double v_inf, int step, void *stream);
+/* apply_ibm_fast, v5.py:228-237: f *= (1 - ibm_mask*force_strength) where ibm_mask > 0,
+ * evaluated in float64 like the reference's float64 mask. */
+int cfd_apply_ibm2d_f32(float *u, float *v, const double *ibm_mask, int n, double force_strength,
+                        void *stream);
+/* np.clip(a, lo, hi, out=a), v5.py:437-438. */
+int cfd_clip_f32(float *a, size_t n, float lo, float hi, void *stream);
+
+/* ------------------------------------------------------------- reductions */
+/* Each writes one value to a device scalar; the caller zeroes `out` for the
+ * max reductions.  Used by the diagnostics (v5.py:410-435), adaptive dt
+ * (v5.py:322) and the health monitor (v5.py:599-613). */
+int cfd_absmax_f32(const float *a, size_t n, float *out, void *stream);            /* max|a| */
+int cfd_absmax2_f32(const float *a, const float *b, size_t n, float *out, void *stream);
+int cfd_energy_mean2d_f32(const float *u, const float *v, size_t n, double *out, void *stream);
+int cfd_vorticity_absmax2d_f32(const float *u, const float *v, const uint8_t *mask, int ny, int nx,
+                               double dx, double dy, float *out, void *stream);
+/* compute_vorticity, v5.py:365-373 (masked cells NaN, boundary ring 0). */
+int cfd_vorticity2d_f32(const float *u, const float *v, const uint8_t *mask, float *w, int ny,
+                        int nx, double dx, double dy, void *stream);
+/* count of non-finite values in a and b (v5.py:601), into a device int. */
+int cfd_nonfinite_count_f32(const float *a, const float *b, size_t n, int *out, void *stream);
+
+/* ------------------------------------------------- multi-GPU slab Jacobi */
+/* One process per GPU.  The global (nz, ny, nx) grid is split on z; rank r
+ * holds nz_local owned planes plus one ghost plane on each side: local array
+ * (nz_local + 2, ny, nx), owned planes 1..nz_local.  Ghost planes are filled
+ * by RCCL send/recv over xGMI after each sweep. */
+int cfd_comm_unique_id(void *out, size_t bytes); /* bytes >= 128 */
+int cfd_comm_init(const void *unique_id, int nranks, int rank, void **comm);
+int cfd_comm_destroy(void *comm);
+/* Exchange plan, computed and tested on the host (SlabPlan in the package):
+ * lo_peer / hi_peer: neighbour ranks or -1.  z_update_begin/end: owned planes
+ * that are updated (global Dirichlet planes are excluded).  overlap != 0:
+ * the two boundary planes are swept first, their halo exchange runs on a
+ * second stream (comm_stream) while the interior sweeps on `stream`. */
+int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
+                          const uint8_t *mask, int nz_local, int ny, int nx, int lo_peer,
+                          int hi_peer, int z_update_begin, int z_update_end, double h, float dt,
+                          int iters, int overlap, void *stream, void *comm_stream);
+/* Single-sweep building block (also used by the slab tests on one GPU):
+ * update planes [z_begin, z_end) of in -> out (local array of nz planes);
+ * x/y faces copied through, masked cells -> 0.  resid (optional, device float,
+ * zeroed by caller) receives max|out - in|. */
+int cfd_jacobi3d_sweep_f32(const float *in, float *out, const float *div, const uint8_t *mask,
+                           int nz, int ny, int nx, int z_begin, int z_end, double h, float dt,
+                           float *resid, void *stream);
+
+/* ------------------------------------------------------------- tuning */
+/* Select the 3-D Jacobi kernel variant (bench / tile sweep):
+ * variant 0 = auto, 1 = LDS plane tile, 2 = cache (no LDS); waves = rows per
+ * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */
+int cfd_set_jacobi3d_config(int variant, int waves, int zchunk);
+
+/* Sweep timing (bench harness): while enabled, every solve records a HIP
+ * event pair on its stream around its sweep launches.  cfd_timing_read
+ * synchronises on those events and returns the summed elapsed milliseconds
+ * and the number of sweeps (Jacobi iterations, or GS colour passes) they
+ * cover.  Not for use under graph capture. */
+int cfd_timing_enable(int enable);
+int cfd_timing_read(double *ms, long long *sweeps, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFDSIM_H */

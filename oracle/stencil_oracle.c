@@ -187,7 +187,9 @@ int oracle_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask,
 
 /* ---- a6: compute_supg_stabilization_fast, v5.py:149-162 --------------- */
 static float supg_tau(float u, float v, float nu, double h, float dt) {
-    float vm = powf(u * u + v * v, 0.5f); /* NumPy float32 scalar `** 0.5` */
+    /* NumPy float32 scalar `u**2` and `** 0.5` both go through libm powf,
+     * which is not always the correctly rounded u*u or sqrt: keep powf. */
+    float vm = powf(powf(u, 2.0f) + powf(v, 2.0f), 0.5f);
     if (vm > (float)1e-10) {
         float pe = (vm * (float)h) / (nu + (float)1e-10);
         float half = pe / 2.0f;

@@ -1,0 +1,37 @@
+#!/usr/bin/env bash
+# Runs a sequence of GPU steps on the gpurun box, each under its own time
+# limit.  Stops at the first step that faults, aborts or times out (exit codes
+# other than 0 = pass and 1 = test failures); logs go to gpurun_out/.
+# usage: scripts/gpu_session.sh STEP...   (steps: smoke tests bench prof pmc tiles bench512 bench2d)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+export NCCL_SOCKET_IFNAME=${NCCL_SOCKET_IFNAME:-lo}
+step() {
+  local name=$1 limit=$2; shift 2
+  echo "=== $name (limit ${limit}s): $*"
+  local t0=$(date +%s)
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)"
+  tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -x ;;
+    testsq) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    bench) step bench 600 python bench.py ;;
+    bench512) step bench512 600 python bench.py --workload jacobi3d_512 --no-cpu-baseline ;;
+    bench2d) step bench2d 600 python bench.py --workload jacobi2d_8192_f64 ;;
+    tiles) step tiles 900 python bench.py --steps 2 --warmup 1 --sweep-tiles --no-cpu-baseline ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    pmc_write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "=== all steps done"

@@ -1,0 +1,58 @@
+"""The C-ABI library loads and exports every symbol include/cfdsim.h declares
+(CPU only: no compute calls without a GPU)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+from cfd_simulations_amd import _lib
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "cfdsim.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(cfd_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    assert "cfd_jacobi3d_f32" in names and "cfd_slab_jacobi3d_f32" in names
+    assert len(names) >= 30
+
+
+def test_bindings_cover_header_exactly():
+    assert sorted(_lib.PROTOTYPES) == declared_functions()
+
+
+def test_library_exports_every_symbol():
+    if not _lib.LIB_PATH.exists():
+        pytest.fail(f"{_lib.LIB_PATH} not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(str(_lib.LIB_PATH))
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_library_identifies_itself():
+    L = _lib.lib()
+    assert L.cfd_abi_version() == _lib.ABI_VERSION
+    assert L.cfd_device_arch() == b"gfx950"
+    assert L.cfd_rbgs_workspace_bytes(1500) >= 4 * 1500
+    assert L.cfd_clean_divergence_workspace_bytes(180, 600) == 2 * 4 * 180 * 600
+
+
+def test_invalid_arguments_report_errors_without_gpu():
+    """Argument validation runs before any device work."""
+    with pytest.raises(_lib.CfdError, match="null"):
+        _lib.call("cfd_jacobi2d_f32", None, None, None, None, 8, 8, 0.1, 1.0, 1, 0, None, None)
+    with pytest.raises(_lib.CfdError, match="waves"):
+        _lib.call("cfd_set_jacobi3d_config", 1, 3, 0)
+
+
+def test_device_arch_of_code_object():
+    """The fat binary carries a gfx950 code object."""
+    data = _lib.LIB_PATH.read_bytes()
+    assert b"gfx950" in data

@@ -1,0 +1,333 @@
+"""GPU parity: the HIP kernels (called through the C ABI) against the pinned
+CPU oracle and the reference-generated fixtures.
+
+Bars (stated per test):
+  * Jacobi 2-D/3-D, red-black GS, divergence, gradient, projection,
+    clean_divergence, BC/IBM/clip: BIT-EXACT (same op order, no FMA).
+  * SUPG predictor and everything downstream of it (full time_step): relative
+    L-inf <= 1e-6 per call / 1e-5 over three steps.  The one intended
+    difference is |V| = sqrtf(u*u + v*v) on the GPU where NumPy's float32
+    scalar `**` goes through libm powf (1 ulp apart on ~0.07% of inputs).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from cfd_simulations_amd import kernels as K
+from cfd_simulations_amd import slab as S
+from cfd_simulations_amd._lib import call, lib, ptr, stream_handle
+from cfd_simulations_amd.solver import OptimizedTurbulentConfig, OptimizedTurbulentSolver
+
+from conftest import rel_linf
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+@pytest.fixture(autouse=True)
+def _reset_j3():
+    call("cfd_set_jacobi3d_config", 0, 0, 0)
+    yield
+    call("cfd_set_jacobi3d_config", 0, 0, 0)
+
+
+# ------------------------------------------------------------- Jacobi 2-D
+@pytest.mark.parametrize("name", ["jacobi2d_f32_128x128_it500_seed1234",
+                                  "jacobi2d_f32_128x128_it500_seed1234_mask",
+                                  "jacobi2d_f64_128x128_it500_seed1234",
+                                  "jacobi2d_f64_128x128_it500_seed1234_mask",
+                                  "jacobi2d_f32_40x72_it60_cyl"])
+def test_jacobi2d_golden_bitexact(golden, name):
+    d = golden(name + ".npz")
+    phi = torch.zeros_like(dev(d["div"]))
+    K.solve_pressure_jacobi(phi, dev(d["div"]), float(d["dx"]), d["dt"], dev(d["mask"]), int(d["iters"]))
+    out = host(phi)
+    assert out.dtype == d["phi"].dtype
+    assert np.array_equal(out, d["phi"])
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("shape,iters", [((37, 53), 17), ((3, 3), 4), ((130, 260), 31),
+                                         ((66, 516), 8), ((2, 9), 3)])
+def test_jacobi2d_random_bitexact(dtype, shape, iters):
+    rng = np.random.default_rng(11)
+    div = rng.standard_normal(shape).astype(dtype)
+    phi0 = rng.standard_normal(shape).astype(dtype)  # nonzero edges + initial guess
+    mask = rng.random(shape) < 0.1
+    ref = oracle.jacobi2d(div, phi0, dx=0.013, dt=np.float32(3e-4), iters=iters, mask=mask)
+    phi = dev(phi0)
+    K.solve_pressure_jacobi(phi, dev(div), 0.013, np.float32(3e-4), dev(mask), iters)
+    assert np.array_equal(host(phi), ref)
+
+
+def test_jacobi2d_residual():
+    rng = np.random.default_rng(3)
+    div = rng.standard_normal((64, 96)).astype(np.float32)
+    k_every, iters = 5, 20
+    res = torch.zeros(iters // k_every, dtype=torch.float32, device=DEV)
+    phi = torch.zeros((64, 96), dtype=torch.float32, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(div), 0.02, np.float32(1e-3), None, iters, resid_every=k_every,
+                            resid_out=res)
+    got = host(res)
+    for k in range(1, iters // k_every + 1):
+        a = oracle.jacobi2d(div, dx=0.02, dt=np.float32(1e-3), iters=k * k_every)
+        b = oracle.jacobi2d(div, dx=0.02, dt=np.float32(1e-3), iters=k * k_every - 1)
+        assert got[k - 1] == np.abs(a - b).max()
+
+
+def test_jacobi2d_8192_f64_full_size():
+    """Config 2 at full size (8192^2 fp64): a few sweeps, bit-exact."""
+    n, iters = 8192, 3
+    rng = np.random.default_rng(1234)
+    div = rng.standard_normal((n, n))
+    ref = oracle.jacobi2d(div, dx=1.0 / (n - 1), dt=np.float32(5e-5), iters=iters)
+    phi = torch.zeros((n, n), dtype=torch.float64, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(div), 1.0 / (n - 1), np.float32(5e-5), None, iters)
+    assert np.array_equal(host(phi), ref)
+
+
+# ------------------------------------------------------------- Jacobi 3-D
+J3_CASES = [((10, 12, 16), None), ((9, 11, 13), None), ((34, 40, 260), None),
+            ((6, 7, 520), None), ((20, 19, 8), "mask")]
+
+
+@pytest.mark.parametrize("variant,waves,zchunk", [(0, 0, 0), (1, 1, 0), (1, 2, 3), (1, 4, 5),
+                                                  (1, 8, 0), (1, 16, 2), (2, 1, 0), (2, 4, 7),
+                                                  (2, 16, 1)])
+@pytest.mark.parametrize("shape,masked", J3_CASES)
+def test_jacobi3d_bitexact(shape, masked, variant, waves, zchunk):
+    call("cfd_set_jacobi3d_config", variant, waves, zchunk)
+    rng = np.random.default_rng(sum(shape))
+    div = rng.standard_normal(shape).astype(np.float32)
+    phi0 = rng.standard_normal(shape).astype(np.float32)
+    mask = (rng.random(shape) < 0.15) if masked else None
+    ref = oracle.jacobi3d(div, phi0, h=0.05, dt=np.float32(2e-3), iters=5, mask=mask)
+    phi = dev(phi0)
+    K.solve_pressure_jacobi3d(phi, dev(div), 0.05, np.float32(2e-3), None if mask is None else dev(mask), 5)
+    assert np.array_equal(host(phi), ref)
+
+
+def test_jacobi3d_residual_matches_oracle():
+    rng = np.random.default_rng(8)
+    div = rng.standard_normal((18, 20, 64)).astype(np.float32)
+    res = torch.zeros(2, dtype=torch.float32, device=DEV)
+    phi = torch.zeros_like(dev(div))
+    K.solve_pressure_jacobi3d(phi, dev(div), 0.1, np.float32(1e-2), None, 6, resid_every=3, resid_out=res)
+    got = host(res)
+    for k in (1, 2):
+        a = oracle.jacobi3d(div, h=0.1, dt=np.float32(1e-2), iters=3 * k)
+        b = oracle.jacobi3d(div, h=0.1, dt=np.float32(1e-2), iters=3 * k - 1)
+        assert got[k - 1] == np.abs(a - b).max()
+
+
+@pytest.mark.parametrize("n", [512, 1024])
+def test_jacobi3d_full_size_bitexact(n):
+    """Configs 3 and 5 at full size (512^3, 1024^3 fp32): two sweeps vs the oracle."""
+    iters = 2
+    rng = np.random.default_rng(1234)
+    div = rng.standard_normal((n, n, n), dtype=np.float32)
+    ref = oracle.jacobi3d(div, h=1.0 / (n - 1), dt=np.float32(5e-5), iters=iters)
+    phi = torch.zeros((n, n, n), dtype=torch.float32, device=DEV)
+    d = dev(div)
+    del div
+    K.solve_pressure_jacobi3d(phi, d, 1.0 / (n - 1), np.float32(5e-5), None, iters)
+    assert np.array_equal(host(phi), ref)
+
+
+def test_jacobi3d_variants_agree_at_1024():
+    """Every kernel variant and tile gives the same bits (30 sweeps, 1024^3)."""
+    n = 1024
+    g = torch.Generator(device=DEV).manual_seed(7)
+    div = torch.randn((n, n, n), generator=g, device=DEV, dtype=torch.float32)
+    outs = []
+    for cfgv in [(1, 4, 0), (2, 4, 0), (1, 8, 64), (2, 16, 0)]:
+        call("cfd_set_jacobi3d_config", *cfgv)
+        phi = torch.zeros_like(div)
+        K.solve_pressure_jacobi3d(phi, div, 1.0 / (n - 1), np.float32(5e-5), None, 30)
+        outs.append(phi)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+
+
+# ------------------------------------------------------------- red-black GS
+@pytest.mark.parametrize("name", ["rbgs2d_f32_64x64_it20_seed7", "rbgs2d_f32_64x64_it20_seed7_mask",
+                                  "rbgs2d_f32_48x80_it15_aniso", "rbgs2d_f32_24x24_earlyexit"])
+def test_rbgs2d_golden_bitexact(golden, name):
+    d = golden(name + ".npz")
+    phi = torch.zeros_like(dev(d["div"]))
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = K.solve_pressure_gauss_seidel_fast(phi, dev(d["div"]), float(d["dx"]), float(d["dy"]), d["dt"],
+                                             dev(d["mask"]), int(d["iters"]), float(d["tol"]),
+                                             iters_done=done)
+    assert out is phi  # in place, same object (v5.py:223,226)
+    assert np.array_equal(host(phi), d["phi"])
+    n = int(host(done)[0])
+    assert n == int(d["iters_done"]) if "iters_done" in d else n == int(d["iters"])
+
+
+@pytest.mark.parametrize("shape", [(31, 45), (64, 128), (5, 4)])
+def test_rbgs2d_random_bitexact(shape):
+    rng = np.random.default_rng(4)
+    div = rng.standard_normal(shape).astype(np.float32)
+    phi0 = rng.standard_normal(shape).astype(np.float32)
+    mask = rng.random(shape) < 0.1
+    ref, n_ref = oracle.rbgs2d(div, phi0, dx=0.03, dy=0.05, dt=np.float32(1e-3), iters=25, tol=1e-8,
+                               mask=mask)
+    phi = dev(phi0)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.solve_pressure_gauss_seidel_fast(phi, dev(div), 0.03, 0.05, np.float32(1e-3), dev(mask), 25, 1e-8,
+                                       iters_done=done)
+    assert np.array_equal(host(phi), ref)
+    assert int(host(done)[0]) == n_ref
+
+
+@pytest.mark.parametrize("shape", [(9, 10, 12), (14, 17, 33)])
+def test_rbgs3d_random_bitexact(shape):
+    rng = np.random.default_rng(6)
+    div = rng.standard_normal(shape).astype(np.float32)
+    mask = rng.random(shape) < 0.1
+    ref, n_ref = oracle.rbgs3d(div, dx=0.1, dy=0.12, dz=0.09, dt=np.float32(1e-2), iters=9, tol=1e-8,
+                               mask=mask)
+    phi = torch.zeros_like(dev(div))
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.solve_pressure_gauss_seidel3d(phi, dev(div), 0.1, 0.12, 0.09, np.float32(1e-2), dev(mask), 9, 1e-8,
+                                    iters_done=done)
+    assert np.array_equal(host(phi), ref)
+    assert int(host(done)[0]) == n_ref
+
+
+# ------------------------------------------------------------- predictor & co
+def test_predictor_components_vs_reference(golden):
+    d = golden("predictor2d_f32_40x56_seed3.npz")
+    dx, dy, dt = float(d["dx"]), float(d["dy"]), d["dt"]
+    u, v, nu = dev(d["u"]), dev(d["v"]), dev(d["nu_eff"])
+    tau = K.compute_supg_stabilization_fast(u, v, dx, dy, dt, nu)
+    assert rel_linf(host(tau), d["tau"]) <= 1e-6
+    # with the reference's own tau the convection is bit-exact
+    tref = dev(d["tau"])
+    assert np.array_equal(host(K.compute_convection_supg_fast(u, v, u, dx, dy, tref)), d["conv_u"])
+    assert np.array_equal(host(K.compute_convection_supg_fast(u, v, v, dx, dy, tref)), d["conv_v"])
+    assert np.array_equal(host(K.compute_convection_fast(u, v, u, dx, dy)), d["conv_u_upwind"])
+    assert np.array_equal(host(K.compute_convection_fast(u, v, v, dx, dy)), d["conv_v_upwind"])
+    assert np.array_equal(host(K.compute_laplacian_fast(u, dx, dy, nu)), d["lap_u"])
+    assert np.array_equal(host(K.compute_laplacian_fast(v, dx, dy, float(d["nu_eff"][0, 0]))), d["lap_v"])
+    us, vs, t2 = K.predictor_fused(u, v, dx, dy, dt, nu, use_supg=True)
+    assert rel_linf(host(us), d["u_star"]) <= 1e-6 and rel_linf(host(vs), d["v_star"]) <= 1e-6
+    us, vs, _ = K.predictor_fused(u, v, dx, dy, dt, float(d["nu_eff"][0, 0]), use_supg=False)
+    assert np.array_equal(host(us), d["u_star_upwind"]) and np.array_equal(host(vs), d["v_star_upwind"])
+    div = K.compute_divergence_fast(dev(d["u_star"]), dev(d["v_star"]), dx, dy)
+    assert np.array_equal(host(div), d["div"])
+    gx, gy = K.compute_gradient_fast(dev(d["u_star"]), dx, dy)
+    assert np.array_equal(host(gx), d["grad_x"]) and np.array_equal(host(gy), d["grad_y"])
+
+
+def test_project_and_clean_divergence_bitexact(golden):
+    d = golden("step_v5_120x36_n3_gs.npz")
+    c = OptimizedTurbulentConfig(nx=120, ny=36)
+    phi, us, vs = d["phi1"], d["u_star1"], d["v_star1"]
+    dt = d["dt0"]
+    gx, gy = oracle.gradient2d(phi, dx=c.dx, dy=c.dy)
+    u_ref, v_ref = us - dt * gx, vs - dt * gy
+    u, v = K.project_velocity(dev(phi), dev(us), dev(vs), c.dx, c.dy, dt)
+    assert np.array_equal(host(u), u_ref) and np.array_equal(host(v), v_ref)
+    cu, cv = oracle.clean_divergence2d(u_ref, v_ref, dx=c.dx, dy=c.dy, iterations=2)
+    K.clean_divergence_fast(u, v, c.dx, c.dy, iterations=2)
+    assert np.array_equal(host(u), cu) and np.array_equal(host(v), cv)
+
+
+def test_bc_ibm_clip_bitexact(golden):
+    d = golden("step_v5_120x36_n3_gs.npz")
+    c = OptimizedTurbulentConfig(nx=120, ny=36)
+    y = np.linspace(c.y_min, c.y_max, c.ny)
+    o = oracle.OracleSolver(c, d["u1"], d["v1"], d["cylinder_mask"], d["ibm_mask"], y)
+    for step in (0, 7, 1500):
+        o.step = step
+        uu, vv = d["u2"].copy(), d["v2"].copy()
+        o.apply_boundary_conditions(uu, vv)
+        u, v = dev(d["u2"]), dev(d["v2"])
+        call("cfd_apply_bc2d_f32", ptr(u), ptr(v), ptr(dev(y)), c.ny, c.nx, float(c.y_max), float(c.V_inf),
+             step, stream_handle())
+        assert rel_linf(host(u), uu) <= 1e-7 and np.array_equal(host(v), vv)
+        fs = min(1.0, step / c.initial_steps)
+        o.apply_ibm(uu, vv, fs)
+        u, v = dev(uu), dev(vv)
+        uu2, vv2 = uu.copy(), vv.copy()
+        o.apply_ibm(uu2, vv2, fs)
+        K.apply_ibm_fast(u, v, dev(d["ibm_mask"]), fs)
+        assert np.array_equal(host(u), uu2) and np.array_equal(host(v), vv2)
+    a = np.array([-9, -5, -1, 0, 2, 5, 7, np.nan], np.float32)
+    t = dev(a)
+    call("cfd_clip_f32", ptr(t), t.numel(), -5.0, 5.0, stream_handle())
+    assert np.array_equal(host(t), np.clip(a, -5, 5), equal_nan=True)
+
+
+@pytest.mark.parametrize("branch", ["gs", "jacobi"])
+def test_time_step_vs_reference(golden, branch):
+    """Three OptimizedTurbulentSolver.time_step() calls vs the reference's."""
+    d = golden(f"step_v5_120x36_n3_{branch}.npz")
+    c = OptimizedTurbulentConfig(nx=120, ny=36, pressure_iterations=200,
+                                 use_fast_pressure=(branch == "gs"), log_diagnostics=True)
+    s = OptimizedTurbulentSolver(c)
+    assert np.array_equal(host(s.u), d["u0"]) and np.array_equal(host(s.v), d["v0"])
+    for k in range(3):
+        dt = s.time_step()
+        assert np.float32(dt) == d[f"dt{k}"]
+        for f, t in (("u", s.u), ("v", s.v), ("phi", s.phi), ("u_star", s.u_star), ("div", s.div_u_star)):
+            assert rel_linf(host(t), d[f"{f}{k + 1}"]) <= 1e-5, (f, k)
+    e = np.array([v for _, v in s.energy_history])
+    assert np.allclose(e, d["energy"], rtol=1e-6, atol=0)
+    diag = s.diagnostics
+    assert all(np.isfinite(v) for v in diag.values())
+
+
+# ------------------------------------------------------------- slabs
+def test_slab_sweeps_emulated_on_one_gpu():
+    """The slab driver's building blocks (cfd_jacobi3d_sweep_f32 on local
+    arrays with ghost planes) with the SlabPlan exchange list, emulated on
+    one GPU for 3 slabs: bit-identical to the single-domain solve."""
+    nz, ny, nx, iters, R = 23, 18, 36, 6, 3
+    rng = np.random.default_rng(9)
+    div = rng.standard_normal((nz, ny, nx)).astype(np.float32)
+    ref = oracle.jacobi3d(div, h=0.07, dt=np.float32(4e-3), iters=iters)
+    plans = [S.SlabPlan(nz, R, r) for r in range(R)]
+    A = [dev(p.scatter(np.zeros_like(div))) for p in plans]
+    B = [a.clone() for a in A]
+    D = [dev(p.scatter(div)) for p in plans]
+    for _ in range(iters):
+        for p, a, b, d_ in zip(plans, A, B, D):
+            S.sweep_range(a, b, d_, None, p.z_update_begin, p.z_update_end, 0.07, np.float32(4e-3))
+        for p, b in zip(plans, B):
+            for send, peer, recv in p.exchanges():
+                B[peer][recv].copy_(b[send])
+        A, B = B, A
+    got = np.concatenate([host(a)[1:p.nz_local + 1] for p, a in zip(plans, A)])
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_slab_rccl_single_rank(overlap):
+    """The RCCL slab driver with a one-rank communicator equals the plain solve."""
+    n, iters = 40, 7
+    rng = np.random.default_rng(10)
+    div = rng.standard_normal((n, n, n + 8)).astype(np.float32)
+    ref = oracle.jacobi3d(div, h=0.05, dt=np.float32(1e-3), iters=iters)
+    plan = S.SlabPlan(n, 1, 0)
+    comm = S.RcclComm(0, 1)
+    try:
+        sj = S.SlabJacobi3D(plan, n, n + 8, 0.05, np.float32(1e-3), comm)
+        sj.div.copy_(dev(plan.scatter(div)))
+        sj.solve(iters, overlap=overlap)
+        assert np.array_equal(host(sj.owned()), ref)
+    finally:
+        comm.close()
