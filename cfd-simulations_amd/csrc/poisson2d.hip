@@ -139,35 +139,40 @@ __global__ __launch_bounds__(256) void jacobi2d_march(const T *__restrict__ in, 
     if constexpr (RESID) wave_reduce_max_store(rmax, resid);
 }
 
-// Boundary rows/planes of a ping-pong pair: v = mask ? 0 : a[k]; a[k] = b[k] = v.
-// (phi_new[mask] = 0 also hits masked edge cells, v5.py:345.)
+// Edge rows the sweep never writes: dst = mask ? 0 : src over [start, start+count).
+// Before sweep 1 this builds the output buffer's edges from the input's
+// (phi_new = phi.copy(); phi_new[mask] = 0, v5.py:339,345 -- sweep 1 itself
+// still reads the unmasked input edges); after sweep 1 it copies them back
+// so both ping-pong buffers hold the final edges.
 template <typename T>
-__global__ void fix_cells(T *__restrict__ a, T *__restrict__ b, const uint8_t *__restrict__ mask,
-                          size_t start, size_t count) {
+__global__ void fix_cells(const T *__restrict__ src, T *__restrict__ dst,
+                          const uint8_t *__restrict__ mask, size_t start, size_t count) {
     for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < count;
          k += (size_t)gridDim.x * blockDim.x) {
         const size_t c = start + k;
-        T v = a[c];
+        T v = src[c];
         if (mask && mask[c]) v = T(0);
-        a[c] = v;
-        b[c] = v;
+        dst[c] = v;
     }
 }
-template __global__ void fix_cells<float>(float *, float *, const uint8_t *, size_t, size_t);
-template __global__ void fix_cells<double>(double *, double *, const uint8_t *, size_t, size_t);
-
 template <typename T>
-int launch_fix_cells(T *a, T *b, const uint8_t *mask, size_t start, size_t count, hipStream_t s) {
+static int launch_fix_cells(const T *src, T *dst, const uint8_t *mask, size_t start, size_t count,
+                            hipStream_t s) {
     if (count == 0) return CFD_OK;
     int blocks = ceil_div((long)count, 256);
     if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(fix_cells<T>, dim3(blocks), dim3(256), 0, s, a, b, mask, start, count);
+    hipLaunchKernelGGL(fix_cells<T>, dim3(blocks), dim3(256), 0, s, src, dst, mask, start, count);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }
-template int launch_fix_cells<float>(float *, float *, const uint8_t *, size_t, size_t, hipStream_t);
-template int launch_fix_cells<double>(double *, double *, const uint8_t *, size_t, size_t,
-                                      hipStream_t);
+
+// rows 0 and ny-1: dst = mask ? 0 : src
+template <typename T>
+static int fix_edge_rows(const T *src, T *dst, const uint8_t *mask, int ny, int nx, hipStream_t s) {
+    int rc = launch_fix_cells<T>(src, dst, mask, 0, (size_t)nx, s);
+    if (!rc && ny > 1) rc = launch_fix_cells<T>(src, dst, mask, (size_t)(ny - 1) * nx, (size_t)nx, s);
+    return rc;
+}
 
 template <typename T, int VEC>
 static int jacobi2d_sweep(const T *in, T *out, const T *div, const uint8_t *mask, int ny, int nx,
@@ -202,12 +207,9 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, const uint8_t *mask, int
     CFD_REQUIRE(iters >= 0, "jacobi2d: iters < 0");
     CFD_REQUIRE(resid_every <= 0 || resid_out, "jacobi2d: resid_every > 0 needs resid_out");
     if (iters == 0) return CFD_OK;
-    const size_t plane = (size_t)nx;
     int rc;
-    // Dirichlet rows 0 and ny-1 (masked -> 0), identical in both buffers.
-    if ((rc = launch_fix_cells<T>(phi, tmp, mask, 0, plane, s))) return rc;
-    if (ny > 1 && (rc = launch_fix_cells<T>(phi, tmp, mask, (size_t)(ny - 1) * plane, plane, s)))
-        return rc;
+    // Dirichlet rows 0 and ny-1 of the first output buffer (masked -> 0)
+    if ((rc = fix_edge_rows<T>(phi, tmp, mask, ny, nx, s))) return rc;
     const int nres = resid_every > 0 ? iters / resid_every : 0;
     if (nres > 0) CFD_CHECK_HIP(hipMemsetAsync(resid_out, 0, sizeof(T) * nres, s));
     constexpr int V = 16 / sizeof(T);
@@ -220,6 +222,8 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, const uint8_t *mask, int
         rc = vec_ok ? jacobi2d_sweep<T, V>(a, b, div, mask, ny, nx, dx2, dtv, r, s)
                     : jacobi2d_sweep<T, 1>(a, b, div, mask, ny, nx, dx2, dtv, r, s);
         if (rc) return rc;
+        // after sweep 1, give the other buffer the final edge rows too
+        if (it == 0 && iters > 1 && (rc = fix_edge_rows<T>(tmp, phi, nullptr, ny, nx, s))) return rc;
         T *t = a; a = b; b = t;
     }
     timing_end(tk, s, iters);

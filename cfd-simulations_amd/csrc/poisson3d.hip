@@ -23,11 +23,14 @@
 
 namespace cfd {
 
-// Dirichlet faces of a ping-pong pair, planes [za, zb) of an (nz, ny, nx)
-// array: every cell of a plane in `full` planes, else rows y = 0 and ny-1
-// (x faces are copied through by the sweep itself):
-//     v = mask ? 0 : a;  a = b = v      (phi_new[mask] = 0 hits faces too)
-__global__ void fix_faces3d(float *__restrict__ a, float *__restrict__ b,
+// Dirichlet faces the sweep never writes, planes [za, zb) of an (nz, ny, nx)
+// array: every cell of the planes full_lo / full_hi, rows y = 0 and ny-1 of
+// the others (x faces are copied through by the sweep itself):
+//     dst = mask ? 0 : src        (phi_new[mask] = 0 hits faces too)
+// Before sweep 1 this builds the output buffer's faces (sweep 1 still reads
+// the unmasked input faces, like the reference); after sweep 1 it copies them
+// back so both ping-pong buffers hold the final faces.
+__global__ void fix_faces3d(const float *__restrict__ src, float *__restrict__ dst,
                             const uint8_t *__restrict__ mask, int ny, int nx, int za, int zb,
                             int full_lo, int full_hi) {
     const size_t plane = (size_t)ny * nx;
@@ -39,20 +42,19 @@ __global__ void fix_faces3d(float *__restrict__ a, float *__restrict__ b,
             size_t c;
             if (full) c = (size_t)z * plane + k;
             else c = (size_t)z * plane + (k < (size_t)nx ? k : (size_t)(ny - 1) * nx + (k - nx));
-            float v = a[c];
+            float v = src[c];
             if (mask && mask[c]) v = 0.f;
-            a[c] = v;
-            b[c] = v;
+            dst[c] = v;
         }
     }
 }
 
-int launch_fix_faces3d(float *a, float *b, const uint8_t *mask, int ny, int nx, int za, int zb,
-                       int full_lo, int full_hi, hipStream_t s) {
+int launch_fix_faces3d(const float *src, float *dst, const uint8_t *mask, int ny, int nx, int za,
+                       int zb, int full_lo, int full_hi, hipStream_t s) {
     if (zb <= za) return CFD_OK;
     int gy = zb - za;
     if (gy > 1024) gy = 1024;
-    hipLaunchKernelGGL(fix_faces3d, dim3(16, gy), dim3(256), 0, s, a, b, mask, ny, nx, za, zb,
+    hipLaunchKernelGGL(fix_faces3d, dim3(16, gy), dim3(256), 0, s, src, dst, mask, ny, nx, za, zb,
                        full_lo, full_hi);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(W * 64) void jacobi3d_march(
             }
             if (MASK && mk[k]) val = 0.f;
             o[k] = val;
-            if (RESID) {
+            if (RESID && ok) {  // only cells this lane owns
                 const float ch = fabsf(val - c[k]);
                 if (ch > rmax) rmax = ch;
             }
@@ -395,8 +397,7 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t
     hipStream_t s = as_stream(stream);
     const size_t plane = (size_t)ny * nx;
     int rc;
-    // Dirichlet faces the sweep never writes (planes 0, nz-1; rows 0, ny-1),
-    // identical in both buffers, masked -> 0
+    // Dirichlet faces the sweep never writes (planes 0, nz-1; rows 0, ny-1)
     if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, 0, nz, 0, nz - 1, s))) return rc;
     const int nres = resid_every > 0 ? iters / resid_every : 0;
     if (nres > 0) CFD_CHECK_HIP(hipMemsetAsync(resid_out, 0, sizeof(float) * nres, s));
@@ -408,6 +409,9 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t
                        ? resid_out + ((it + 1) / resid_every - 1)
                        : nullptr;
         if ((rc = jacobi3d_sweep(a, b, div, mask, nz, ny, nx, 1, nz - 1, h2, dt, r, s))) return rc;
+        if (it == 0 && iters > 1 &&
+            (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, 0, nz, 0, nz - 1, s)))
+            return rc;
         float *t = a;
         a = b;
         b = t;

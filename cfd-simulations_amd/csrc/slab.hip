@@ -17,8 +17,8 @@
 #include "common.hpp"
 
 namespace cfd {
-int launch_fix_faces3d(float *a, float *b, const uint8_t *mask, int ny, int nx, int za, int zb,
-                       int full_lo, int full_hi, hipStream_t s);
+int launch_fix_faces3d(const float *src, float *dst, const uint8_t *mask, int ny, int nx, int za,
+                       int zb, int full_lo, int full_hi, hipStream_t s);
 
 struct SlabComm {
     ncclComm_t comm = nullptr;
@@ -128,11 +128,13 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
     const int nzt = nz_local + 2;
     const size_t plane = (size_t)ny * nx;
     int rc;
-    // Dirichlet faces: rows y=0, ny-1 of every plane, and the global boundary
-    // planes (owned planes outside the update range) in full.
+    // Dirichlet faces of the owned planes: rows y=0, ny-1, and the global
+    // boundary planes (owned planes outside the update range) in full.  Ghost
+    // planes arrive whole from the neighbours (their face rows are never read).
     const int full_lo = z_update_begin > 1 ? 1 : -1;
     const int full_hi = z_update_end < nz_local + 1 ? nz_local : -1;
-    if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, 0, nzt, full_lo, full_hi, s))) return rc;
+    if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, 1, nz_local + 1, full_lo, full_hi, s)))
+        return rc;
     // ghosts of the initial guess
     if ((rc = exchange(c, phi, nz_local, plane, lo_peer, hi_peer, s))) return rc;
     const float h2f = (float)(h * h);
@@ -170,6 +172,10 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
                 return rc;
             CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
         }
+        // after sweep 1, the other buffer gets the final owned faces too
+        if (it == 0 && iters > 1 &&
+            (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, 1, nz_local + 1, full_lo, full_hi, s)))
+            return rc;
         float *t = a;
         a = b;
         b = t;
