@@ -82,6 +82,15 @@ class SlabPlan:
             out.append((self.nz_local, self.hi_peer, 0))
         return out
 
+    def receives(self):
+        """[(local_ghost_plane, peer)]: where this rank's ghosts come from."""
+        out = []
+        if self.lo_peer >= 0:
+            out.append((0, self.lo_peer))
+        if self.hi_peer >= 0:
+            out.append((self.nz_local + 1, self.hi_peer))
+        return out
+
     def local_slice(self):
         """Global planes held locally, ghosts included (clipped at the faces)."""
         return slice(max(self.z_lo - 1, 0), min(self.z_hi + 1, self.nz))
