@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="3-D kernel: 0 auto, 1 LDS, 2 cache")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--zchunk", type=int, default=0)
+    ap.add_argument("--tb", type=int, default=0, help="3-D sweeps fused per pass: 0 auto (2), 1 off, 2 on")
+    ap.add_argument("--tb-rows", type=int, default=0)
+    ap.add_argument("--tb-zchunk", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-planes", type=int, default=256)
@@ -132,6 +135,7 @@ def main():
     shape, dt_name, iters_default, bpc = WORKLOADS[ARGS.workload]
     iters = ARGS.iters or iters_default
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
+    call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
     dt = np.float32(5e-5)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
@@ -209,9 +213,14 @@ def main():
         sweep_ms_max = sweep_ms
 
     value = cells_all * ARGS.steps / elapsed / 1e9
-    # roofline of the dominant kernel: this rank's sweep (per launch)
-    alg_bytes = cells_rank * bpc
-    achieved = alg_bytes / (sweep_ms * 1e-3) / 1e9
+    # roofline of the dominant kernel, per launch.  A temporally blocked launch
+    # (jacobi3d_tb2) performs 2 sweeps in one HBM pass: 12 B of algorithmic
+    # traffic per cell per launch = 6 B per cell-update.
+    blocked = len(shape) == 3 and world == 1 and ARGS.tb != 1 and iters >= 2
+    spl = 2 if blocked else 1
+    launch_ms = sweep_ms * spl
+    alg_bytes = cells_rank * 12 if blocked else cells_rank * bpc
+    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
     traffic = load_traffic(ARGS.workload, world)
     out = {
         "metric": METRIC,
@@ -230,13 +239,17 @@ def main():
                    "decomposition": "z-slab" if len(shape) == 3 else "none",
                    "halo": ("rccl send/recv, overlapped" if not ARGS.no_overlap else "rccl send/recv")
                    if world > 1 else "none",
-                   "kernel_variant": ARGS.variant, "waves": ARGS.waves, "zchunk": ARGS.zchunk},
+                   "kernel_variant": ARGS.variant, "waves": ARGS.waves, "zchunk": ARGS.zchunk,
+                   "temporal_blocking": ARGS.tb, "tb_rows": ARGS.tb_rows},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "jacobi3d_march" if len(shape) == 3 else "jacobi2d_march",
-                     "bytes_per_cell_update": bpc, "cell_updates_per_launch": cells_rank,
-                     "avg_launch_ms": round(sweep_ms, 4), "max_rank_avg_launch_ms": round(sweep_ms_max, 4)},
+                     "kernel": ("jacobi3d_tb2" if blocked else "jacobi3d_march") if len(shape) == 3
+                     else "jacobi2d_march",
+                     "sweeps_per_launch": spl, "bytes_per_cell_update": bpc / spl,
+                     "cells_per_launch": cells_rank, "algorithmic_bytes_per_launch": alg_bytes,
+                     "avg_launch_ms": round(launch_ms, 4),
+                     "max_rank_avg_launch_ms": round(sweep_ms_max * spl, 4)},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not ARGS.no_cpu_baseline:
@@ -252,6 +265,7 @@ def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells):
     """Config 3: time every (variant, waves, zchunk) tile on this grid."""
     import torch
     res = []
+    call("cfd_set_jacobi3d_blocking", 1, 0, 0)
     for variant in (1, 2):
         for waves in (1, 2, 4, 8, 16):
             for zchunk in (0, 64, 128):
@@ -270,6 +284,24 @@ def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells):
                             "GBps": round(cells * bpc / per / 1e6, 1)})
                 print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
+    for rows in (2, 6, 14):
+        for zchunk in (0, 32, 64, 128, 256):
+            call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
+            phi.zero_()
+            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 4, phi_tmp=tmp)
+            torch.cuda.synchronize()
+            call("cfd_timing_enable", 1)
+            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 20, phi_tmp=tmp)
+            ms = ctypes.c_double()
+            n = ctypes.c_longlong()
+            call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(n), 1)
+            call("cfd_timing_enable", 0)
+            per = ms.value / n.value
+            res.append({"tb_rows": rows, "zchunk": zchunk, "ms_per_sweep": round(per, 4),
+                        "GBps_pass": round(cells * 12 / (2 * per) / 1e6, 1),
+                        "Gcell_per_s": round(cells / per / 1e6, 1)})
+            print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
+    call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
     return res
 
 

@@ -62,6 +62,7 @@ PROTOTYPES = {
     "cfd_jacobi3d_sweep_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_double,
                                        c_float, P, P]),
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),
+    "cfd_set_jacobi3d_blocking": (c_int, [c_int, c_int, c_int]),
     "cfd_timing_enable": (c_int, [c_int]),
     "cfd_timing_read": (c_int, [ctypes.POINTER(c_double), ctypes.POINTER(ctypes.c_longlong), c_int]),
 }

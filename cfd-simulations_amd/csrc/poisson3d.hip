@@ -64,8 +64,15 @@ struct J3Config {
     int variant = 0;  // 0 auto, 1 LDS, 2 cache
     int waves = 0;    // rows per workgroup (0 = auto)
     int zchunk = 0;   // planes per workgroup (0 = auto)
+    int tb_steps = 0; // sweeps fused per pass: 0 auto (2), 1 off, 2 on
+    int tb_rows = 0;  // output rows per temporally blocked tile (0 = auto)
+    int tb_zchunk = 0;
 };
 static J3Config g_j3;
+
+int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
+                      int ze, int fixed_lo, int fixed_hi, float h2, float dt, int W, int zchunk,
+                      hipStream_t s);
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
@@ -367,6 +374,16 @@ using namespace cfd;
 
 extern "C" {
 
+int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
+    CFD_REQUIRE(steps >= 0 && steps <= 2, "blocking steps must be 0 (auto), 1 or 2");
+    CFD_REQUIRE(rows == 0 || rows == 2 || rows == 6 || rows == 14, "blocking rows must be 0, 2, 6, 14");
+    CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
+    g_j3.tb_steps = steps;
+    g_j3.tb_rows = rows;
+    g_j3.tb_zchunk = zchunk;
+    return CFD_OK;
+}
+
 int cfd_set_jacobi3d_config(int variant, int waves, int zchunk) {
     CFD_REQUIRE(variant >= 0 && variant <= 2, "variant must be 0..2");
     CFD_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8 || waves == 16,
@@ -404,6 +421,29 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t
     const float h2 = (float)(h * h);
     float *a = phi, *b = phi_tmp;
     const int tk = timing_begin(s);
+    const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(div);
+    if (g_j3.tb_steps != 1 && !mask && resid_every <= 0 && vec_ok && nz >= 3 && ny >= 3 && iters >= 2) {
+        // temporally blocked: one single sweep if iters is odd, then fused pairs
+        const int W = g_j3.tb_rows ? g_j3.tb_rows : 6;
+        int done = 0;
+        while (done < iters) {
+            if ((iters - done) & 1)
+                rc = jacobi3d_sweep(a, b, div, mask, nz, ny, nx, 1, nz - 1, h2, dt, nullptr, s);
+            else
+                rc = jacobi3d_tb2_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt, W, g_j3.tb_zchunk, s);
+            if (rc) return rc;
+            if (done == 0 && (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, 0, nz, 0, nz - 1, s)))
+                return rc;
+            done += ((iters - done) & 1) ? 1 : 2;
+            float *t = a;
+            a = b;
+            b = t;
+        }
+        timing_end(tk, s, iters);
+        if (a != phi)
+            CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(float) * plane * nz, hipMemcpyDeviceToDevice, s));
+        return CFD_OK;
+    }
     for (int it = 0; it < iters; ++it) {
         float *r = (resid_every > 0 && (it + 1) % resid_every == 0)
                        ? resid_out + ((it + 1) / resid_every - 1)

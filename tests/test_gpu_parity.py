@@ -38,8 +38,10 @@ def host(t):
 @pytest.fixture(autouse=True)
 def _reset_j3():
     call("cfd_set_jacobi3d_config", 0, 0, 0)
+    call("cfd_set_jacobi3d_blocking", 0, 0, 0)
     yield
     call("cfd_set_jacobi3d_config", 0, 0, 0)
+    call("cfd_set_jacobi3d_blocking", 0, 0, 0)
 
 
 # ------------------------------------------------------------- Jacobi 2-D
@@ -118,6 +120,22 @@ def test_jacobi3d_bitexact(shape, masked, variant, waves, zchunk):
     assert np.array_equal(host(phi), ref)
 
 
+@pytest.mark.parametrize("rows,zchunk", [(2, 0), (6, 0), (14, 0), (6, 3), (2, 1), (14, 5)])
+@pytest.mark.parametrize("shape,iters", [((10, 12, 16), 6), ((9, 11, 20), 7), ((34, 40, 260), 4),
+                                         ((6, 7, 520), 5), ((20, 19, 8), 2), ((5, 33, 768), 9),
+                                         ((3, 3, 4), 4)])
+def test_jacobi3d_temporal_blocking_bitexact(shape, iters, rows, zchunk):
+    """Two sweeps fused per pass (jacobi3d_tb2) == two single sweeps, bitwise."""
+    call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
+    rng = np.random.default_rng(sum(shape) + iters)
+    div = rng.standard_normal(shape).astype(np.float32)
+    phi0 = rng.standard_normal(shape).astype(np.float32)
+    ref = oracle.jacobi3d(div, phi0, h=0.05, dt=np.float32(2e-3), iters=iters)
+    phi = dev(phi0)
+    K.solve_pressure_jacobi3d(phi, dev(div), 0.05, np.float32(2e-3), None, iters)
+    assert np.array_equal(host(phi), ref)
+
+
 def test_jacobi3d_residual_matches_oracle():
     rng = np.random.default_rng(8)
     div = rng.standard_normal((18, 20, 64)).astype(np.float32)
@@ -151,8 +169,10 @@ def test_jacobi3d_variants_agree_at_1024():
     g = torch.Generator(device=DEV).manual_seed(7)
     div = torch.randn((n, n, n), generator=g, device=DEV, dtype=torch.float32)
     outs = []
-    for cfgv in [(1, 4, 0), (2, 4, 0), (1, 8, 64), (2, 16, 0)]:
+    for cfgv, tb in [((1, 4, 0), 1), ((2, 4, 0), 1), ((1, 8, 64), 1), ((2, 16, 0), 1), ((0, 0, 0), 2),
+                     ((0, 0, 0), (2, 14, 0)), ((0, 0, 0), (2, 2, 40))]:
         call("cfd_set_jacobi3d_config", *cfgv)
+        call("cfd_set_jacobi3d_blocking", *(tb if isinstance(tb, tuple) else (tb, 0, 0)))
         phi = torch.zeros_like(div)
         K.solve_pressure_jacobi3d(phi, div, 1.0 / (n - 1), np.float32(5e-5), None, 30)
         outs.append(phi)
