@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--tb-rows", type=int, default=0)
     ap.add_argument("--tb-zchunk", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-rhs-ws", action="store_true", help="form the RHS in-register every sweep")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-planes", type=int, default=256)
     ap.add_argument("--sweep-tiles", action="store_true", help="print a tile-size sweep (N=1, 3-D)")
@@ -142,18 +143,19 @@ def main():
     if len(shape) == 3:
         nz, ny, nx = shape
         h = 1.0 / (nx - 1)
-        plan = S.SlabPlan(nz, world, rank)
+        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else 2)
         if world == 1:
             div = torch.randn(shape, generator=g, device=dev, dtype=torch.float32)
             phi = torch.zeros_like(div)
             tmp = torch.zeros_like(div)
+            rhs = None if ARGS.no_rhs_ws else torch.empty_like(div)
 
             def step():
                 phi.zero_()
-                K.solve_pressure_jacobi3d(phi, div, h, dt, None, iters, phi_tmp=tmp)
+                K.solve_pressure_jacobi3d(phi, div, h, dt, None, iters, phi_tmp=tmp, rhs_ws=rhs)
         else:
             comm = S.RcclComm(rank, world)
-            sj = S.SlabJacobi3D(plan, ny, nx, h, dt, comm, device=dev)
+            sj = S.SlabJacobi3D(plan, ny, nx, h, dt, comm, device=dev, rhs_workspace=not ARGS.no_rhs_ws)
             sj.div.copy_(torch.randn(sj.div.shape, generator=g, device=dev, dtype=torch.float32))
 
             def step():
@@ -169,11 +171,12 @@ def main():
         div = torch.randn(shape, generator=g, device=dev, dtype=torch.float64)
         phi = torch.zeros_like(div)
         tmp = torch.zeros_like(div)
+        rhs = None if ARGS.no_rhs_ws else torch.empty_like(div)
         h = 1.0 / (nx - 1)
 
         def step():
             phi.zero_()
-            K.solve_pressure_jacobi(phi, div, h, dt, None, iters, phi_tmp=tmp)
+            K.solve_pressure_jacobi(phi, div, h, dt, None, iters, phi_tmp=tmp, rhs_ws=rhs)
         cells_all = (ny - 2) * (nx - 2) * iters
         cells_rank = (ny - 2) * (nx - 2)
         workload = f"jacobi2d_5pt_{ny}x{nx}_f64"
@@ -184,7 +187,7 @@ def main():
             dist.barrier()
 
     if ARGS.sweep_tiles and world == 1 and len(shape) == 3:
-        tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells_rank)
+        tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells_rank, rhs)
 
     for _ in range(ARGS.warmup):
         step()
@@ -216,7 +219,7 @@ def main():
     # roofline of the dominant kernel, per launch.  A temporally blocked launch
     # (jacobi3d_tb2) performs 2 sweeps in one HBM pass: 12 B of algorithmic
     # traffic per cell per launch = 6 B per cell-update.
-    blocked = len(shape) == 3 and world == 1 and ARGS.tb != 1 and iters >= 2
+    blocked = len(shape) == 3 and ARGS.tb != 1 and iters >= 2
     spl = 2 if blocked else 1
     launch_ms = sweep_ms * spl
     alg_bytes = cells_rank * 12 if blocked else cells_rank * bpc
@@ -240,7 +243,8 @@ def main():
                    "halo": ("rccl send/recv, overlapped" if not ARGS.no_overlap else "rccl send/recv")
                    if world > 1 else "none",
                    "kernel_variant": ARGS.variant, "waves": ARGS.waves, "zchunk": ARGS.zchunk,
-                   "temporal_blocking": ARGS.tb, "tb_rows": ARGS.tb_rows},
+                   "temporal_blocking": ARGS.tb, "tb_rows": ARGS.tb_rows,
+                   "rhs_workspace": not ARGS.no_rhs_ws},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
@@ -261,7 +265,7 @@ def main():
         dist.destroy_process_group()
 
 
-def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells):
+def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):
     """Config 3: time every (variant, waves, zchunk) tile on this grid."""
     import torch
     res = []
@@ -271,10 +275,10 @@ def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells):
             for zchunk in (0, 64, 128):
                 call("cfd_set_jacobi3d_config", variant, waves, zchunk)
                 phi.zero_()
-                K.solve_pressure_jacobi3d(phi, div, h, dt, None, 4, phi_tmp=tmp)
+                K.solve_pressure_jacobi3d(phi, div, h, dt, None, 4, phi_tmp=tmp, rhs_ws=rhs)
                 torch.cuda.synchronize()
                 call("cfd_timing_enable", 1)
-                K.solve_pressure_jacobi3d(phi, div, h, dt, None, 20, phi_tmp=tmp)
+                K.solve_pressure_jacobi3d(phi, div, h, dt, None, 20, phi_tmp=tmp, rhs_ws=rhs)
                 ms = ctypes.c_double()
                 n = ctypes.c_longlong()
                 call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(n), 1)
@@ -288,10 +292,10 @@ def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells):
         for zchunk in (0, 32, 64, 128, 256):
             call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
             phi.zero_()
-            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 4, phi_tmp=tmp)
+            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 4, phi_tmp=tmp, rhs_ws=rhs)
             torch.cuda.synchronize()
             call("cfd_timing_enable", 1)
-            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 20, phi_tmp=tmp)
+            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 20, phi_tmp=tmp, rhs_ws=rhs)
             ms = ctypes.c_double()
             n = ctypes.c_longlong()
             call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(n), 1)

@@ -26,9 +26,10 @@ PROTOTYPES = {
     "cfd_abi_version": (c_int, []),
     "cfd_last_error": (c_char_p, []),
     "cfd_device_arch": (c_char_p, []),
-    "cfd_jacobi2d_f32": (c_int, [P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
-    "cfd_jacobi2d_f64": (c_int, [P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
-    "cfd_jacobi3d_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
+    "cfd_jacobi2d_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
+    "cfd_jacobi2d_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
+    "cfd_jacobi3d_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_double, c_float, c_int, c_int, P,
+                                 P]),
     "cfd_rbgs_workspace_bytes": (c_size_t, [c_int]),
     "cfd_rbgs2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_float, c_int, c_double,
                                P, P, P, P]),
@@ -57,8 +58,8 @@ PROTOTYPES = {
     "cfd_comm_unique_id": (c_int, [P, c_size_t]),
     "cfd_comm_init": (c_int, [P, c_int, c_int, ctypes.POINTER(c_void_p)]),
     "cfd_comm_destroy": (c_int, [P]),
-    "cfd_slab_jacobi3d_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                      c_double, c_float, c_int, c_int, P, P]),
+    "cfd_slab_jacobi3d_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_int, c_double, c_float, c_int, c_int, P, P]),
     "cfd_jacobi3d_sweep_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_double,
                                        c_float, P, P]),
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),

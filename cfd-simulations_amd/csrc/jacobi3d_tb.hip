@@ -21,7 +21,7 @@
 //
 // Scope: no mask, no residual (the solver falls back to single sweeps for
 // those), nx % 4 == 0, 16-byte aligned arrays.
-#include "common.hpp"
+#include "internal.hpp"
 
 namespace cfd {
 
@@ -30,6 +30,8 @@ __device__ inline void stg4(float *p, float4 v) { *reinterpret_cast<float4 *>(p)
 __device__ inline float4 lds4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
+// d is div (PRE = false: rhs = (h2*div)/dt here) or the precomputed rhs
+template <bool PRE>
 __device__ inline float jac7(float E, float W, float N, float S, float U, float D, float d, float h2,
                              float dt) {
     float s = E + W;
@@ -37,10 +39,11 @@ __device__ inline float jac7(float E, float W, float N, float S, float U, float 
     s = s + S;
     s = s + U;
     s = s + D;
-    return (1.0f / 6.0f) * (s - (h2 * d) / dt);
+    const float rhs = PRE ? d : (h2 * d) / dt;
+    return (1.0f / 6.0f) * (s - rhs);
 }
 
-template <int W>
+template <int W, bool PRE>
 __global__ __launch_bounds__((W + 2) * 64) void jacobi3d_tb2(
     const float *__restrict__ in, float *__restrict__ out, const float *__restrict__ div, int nz,
     int ny, int nx, int nseg, int ntile_y, int zb, int ze, int zchunk, int fixed_lo, int fixed_hi,
@@ -154,7 +157,7 @@ __global__ __launch_bounds__((W + 2) * 64) void jacobi3d_tb2(
                 const int xk = x + k;
                 const float E = k < 3 ? c[k + 1] : er;
                 const float Wv = k > 0 ? c[k - 1] : wl;
-                o[k] = (xk == 0 || xk == nx - 1) ? c[k] : jac7(E, Wv, n[k], sv[k], u[k], dd[k], dv[k], h2, dt);
+                o[k] = (xk == 0 || xk == nx - 1) ? c[k] : jac7<PRE>(E, Wv, n[k], sv[k], u[k], dd[k], dv[k], h2, dt);
             }
             l1 = make_float4(o[0], o[1], o[2], o[3]);
         }
@@ -165,12 +168,12 @@ __global__ __launch_bounds__((W + 2) * 64) void jacobi3d_tb2(
             if (lane == 0) {
                 v = hc.w;  // x = xs-1
                 if (int_row && !fixed)
-                    v = jac7(cc.x, hc.z, A[b][g + 2][3], A[b][g][3], hp.w, hm.w, dh, h2, dt);
+                    v = jac7<PRE>(cc.x, hc.z, A[b][g + 2][3], A[b][g][3], hp.w, hm.w, dh, h2, dt);
                 B[b][g][3] = v;
             } else {
                 v = hc.x;  // x = xs+256
                 if (int_row && !fixed && xs + 256 != nx - 1)
-                    v = jac7(hc.y, cc.w, A[b][g + 2][260], A[b][g][260], hp.x, hm.x, dh, h2, dt);
+                    v = jac7<PRE>(hc.y, cc.w, A[b][g + 2][260], A[b][g][260], hp.x, hm.x, dh, h2, dt);
                 B[b][g][260] = v;
             }
         }
@@ -196,7 +199,7 @@ __global__ __launch_bounds__((W + 2) * 64) void jacobi3d_tb2(
                 const int xk = x + k;
                 const float E = k < 3 ? c[k + 1] : er1;
                 const float Wv = k > 0 ? c[k - 1] : wl1;
-                o[k] = (xk == 0 || xk == nx - 1) ? c[k] : jac7(E, Wv, n[k], sv[k], u[k], dd[k], dv[k], h2, dt);
+                o[k] = (xk == 0 || xk == nx - 1) ? c[k] : jac7<PRE>(E, Wv, n[k], sv[k], u[k], dd[k], dv[k], h2, dt);
             }
             stg4(out + (size_t)(z - 1) * plane + rofs, make_float4(o[0], o[1], o[2], o[3]));
         }
@@ -215,7 +218,7 @@ __global__ __launch_bounds__((W + 2) * 64) void jacobi3d_tb2(
 // otherwise they are updated too (2-deep ghost planes, slab mode).
 int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, float h2, float dt, int W, int zchunk,
-                      hipStream_t s) {
+                      bool pre, hipStream_t s) {
     if (ze <= zb || ny < 3) return CFD_OK;
     const int nseg = ceil_div(nx, 256);
     const int ntile_y = ceil_div(ny - 2, W);
@@ -231,8 +234,14 @@ int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int
     const int blocks = nseg * ntile_y * ceil_div(L, zchunk);
 #define CFD_TB2(WV)                                                                             \
     case WV:                                                                                    \
-        hipLaunchKernelGGL(jacobi3d_tb2<WV>, dim3(blocks), dim3((WV + 2) * 64), 0, s, in, out, div, \
-                           nz, ny, nx, nseg, ntile_y, zb, ze, zchunk, fixed_lo, fixed_hi, h2, dt);  \
+        if (pre)                                                                                \
+            hipLaunchKernelGGL((jacobi3d_tb2<WV, true>), dim3(blocks), dim3((WV + 2) * 64), 0, s, in, \
+                               out, div, nz, ny, nx, nseg, ntile_y, zb, ze, zchunk, fixed_lo,      \
+                               fixed_hi, h2, dt);                                               \
+        else                                                                                    \
+            hipLaunchKernelGGL((jacobi3d_tb2<WV, false>), dim3(blocks), dim3((WV + 2) * 64), 0, s, in, \
+                               out, div, nz, ny, nx, nseg, ntile_y, zb, ze, zchunk, fixed_lo,      \
+                               fixed_hi, h2, dt);                                               \
         break;
     switch (W) {
         CFD_TB2(2)

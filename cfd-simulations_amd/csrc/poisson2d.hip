@@ -51,7 +51,8 @@ __device__ inline void st(T *p, const T (&r)[VEC]) {
 }
 
 // One Jacobi sweep over rows [1, ny-1).  Grid: waves = nseg * nchunk.
-template <typename T, int VEC, bool RESID>
+// PRE: `div` holds the precomputed rhs = (dx2*div)/dt (same bits as in-register)
+template <typename T, int VEC, bool RESID, bool PRE>
 __global__ __launch_bounds__(256) void jacobi2d_march(const T *__restrict__ in, T *__restrict__ out,
                                                       const T *__restrict__ div,
                                                       const uint8_t *__restrict__ mask, int ny,
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(256) void jacobi2d_march(const T *__restrict__ in, 
                 T s = E + W;
                 s = s + nxt[k];
                 s = s + prv[k];
-                const T rhs = (dx2 * d[k]) / dtv;
+                const T rhs = PRE ? d[k] : (dx2 * d[k]) / dtv;
                 val = T(0.25) * (s - rhs);
             }
             if (m[k]) val = T(0);
@@ -176,7 +177,7 @@ static int fix_edge_rows(const T *src, T *dst, const uint8_t *mask, int ny, int 
 
 template <typename T, int VEC>
 static int jacobi2d_sweep(const T *in, T *out, const T *div, const uint8_t *mask, int ny, int nx,
-                          T dx2, T dtv, T *resid, hipStream_t s) {
+                          T dx2, T dtv, bool pre, T *resid, hipStream_t s) {
     const int nseg = ceil_div(nx, kWave * VEC);
     const int rows = ny - 2;
     if (rows <= 0) return CFD_OK;
@@ -189,19 +190,30 @@ static int jacobi2d_sweep(const T *in, T *out, const T *div, const uint8_t *mask
     const long waves = (long)nseg * nchunk;
     const int wpb = 4;
     const int blocks = ceil_div(waves, wpb);
-    if (resid)
-        hipLaunchKernelGGL((jacobi2d_march<T, VEC, true>), dim3(blocks), dim3(wpb * kWave), 0, s,
-                           in, out, div, mask, ny, nx, nseg, rpc, dx2, dtv, resid);
-    else
-        hipLaunchKernelGGL((jacobi2d_march<T, VEC, false>), dim3(blocks), dim3(wpb * kWave), 0, s,
-                           in, out, div, mask, ny, nx, nseg, rpc, dx2, dtv, resid);
+#define CFD_J2(R, PR)                                                                             \
+    hipLaunchKernelGGL((jacobi2d_march<T, VEC, R, PR>), dim3(blocks), dim3(wpb * kWave), 0, s, in, \
+                       out, div, mask, ny, nx, nseg, rpc, dx2, dtv, resid)
+    if (resid) {
+        if (pre) CFD_J2(true, true); else CFD_J2(true, false);
+    } else {
+        if (pre) CFD_J2(false, true); else CFD_J2(false, false);
+    }
+#undef CFD_J2
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }
 
 template <typename T>
-static int jacobi2d_solve(const T *div, T *phi, T *tmp, const uint8_t *mask, int ny, int nx,
-                          T dx2, T dtv, int iters, int resid_every, T *resid_out, hipStream_t s) {
+__global__ void k_rhs2d(const T *__restrict__ div, T *__restrict__ rhs, size_t n, T dx2, T dtv) {
+    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
+         k += (size_t)gridDim.x * blockDim.x)
+        rhs[k] = (dx2 * div[k]) / dtv;
+}
+
+template <typename T>
+static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t *mask, int ny,
+                          int nx, T dx2, T dtv, int iters, int resid_every, T *resid_out,
+                          hipStream_t s) {
     CFD_REQUIRE(div && phi && tmp, "jacobi2d: null array pointer");
     CFD_REQUIRE(ny >= 1 && nx >= 1, "jacobi2d: bad shape (%d, %d)", ny, nx);
     CFD_REQUIRE(iters >= 0, "jacobi2d: iters < 0");
@@ -212,15 +224,26 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, const uint8_t *mask, int
     if ((rc = fix_edge_rows<T>(phi, tmp, mask, ny, nx, s))) return rc;
     const int nres = resid_every > 0 ? iters / resid_every : 0;
     if (nres > 0) CFD_CHECK_HIP(hipMemsetAsync(resid_out, 0, sizeof(T) * nres, s));
+    // RHS prologue: with a workspace the sweeps read rhs instead of dividing
+    const bool pre = rhs_ws != nullptr;
+    const T *src = div;
+    if (pre) {
+        const size_t n = (size_t)ny * nx;
+        long blocks = (long)((n + 255) / 256);
+        if (blocks > 4096) blocks = 4096;
+        hipLaunchKernelGGL(k_rhs2d<T>, dim3(blocks), dim3(256), 0, s, div, rhs_ws, n, dx2, dtv);
+        CFD_LAUNCH_CHECK();
+        src = rhs_ws;
+    }
     constexpr int V = 16 / sizeof(T);
-    const bool vec_ok = (nx % V == 0) && aligned16(div) && aligned16(phi) && aligned16(tmp);
+    const bool vec_ok = (nx % V == 0) && aligned16(src) && aligned16(phi) && aligned16(tmp);
     T *a = phi, *b = tmp;
     const int tk = timing_begin(s);
     for (int it = 0; it < iters; ++it) {
         T *r = (resid_every > 0 && (it + 1) % resid_every == 0) ? resid_out + ((it + 1) / resid_every - 1)
                                                                  : nullptr;
-        rc = vec_ok ? jacobi2d_sweep<T, V>(a, b, div, mask, ny, nx, dx2, dtv, r, s)
-                    : jacobi2d_sweep<T, 1>(a, b, div, mask, ny, nx, dx2, dtv, r, s);
+        rc = vec_ok ? jacobi2d_sweep<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, r, s)
+                    : jacobi2d_sweep<T, 1>(a, b, src, mask, ny, nx, dx2, dtv, pre, r, s);
         if (rc) return rc;
         // after sweep 1, give the other buffer the final edge rows too
         if (it == 0 && iters > 1 && (rc = fix_edge_rows<T>(tmp, phi, nullptr, ny, nx, s))) return rc;
@@ -330,20 +353,20 @@ using namespace cfd;
 
 extern "C" {
 
-int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t *mask, int ny,
-                     int nx, double dx, float dt, int iters, int resid_every, float *resid_out,
-                     void *stream) {
+int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws,
+                     const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
+                     int resid_every, float *resid_out, void *stream) {
     // `cfg.dx**2` is a Python float; NEP 50 rounds it to float32 against the
     // float32 array (v5.py:343).
-    return jacobi2d_solve<float>(div, phi, phi_tmp, mask, ny, nx, (float)(dx * dx), dt, iters,
-                                 resid_every, resid_out, as_stream(stream));
+    return jacobi2d_solve<float>(div, phi, phi_tmp, rhs_ws, mask, ny, nx, (float)(dx * dx), dt,
+                                 iters, resid_every, resid_out, as_stream(stream));
 }
 
-int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, const uint8_t *mask, int ny,
-                     int nx, double dx, float dt, int iters, int resid_every, double *resid_out,
-                     void *stream) {
-    return jacobi2d_solve<double>(div, phi, phi_tmp, mask, ny, nx, dx * dx, (double)dt, iters,
-                                  resid_every, resid_out, as_stream(stream));
+int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
+                     const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
+                     int resid_every, double *resid_out, void *stream) {
+    return jacobi2d_solve<double>(div, phi, phi_tmp, rhs_ws, mask, ny, nx, dx * dx, (double)dt,
+                                  iters, resid_every, resid_out, as_stream(stream));
 }
 
 size_t cfd_rbgs_workspace_bytes(int iterations) {

@@ -19,7 +19,7 @@
 //  * the RHS (h^2*div)/dt is recomputed in-register from div (4 B either way);
 //  * the workgroup -> tile map is XCD-aware: each XCD gets a contiguous run of
 //    y-tiles so the halo rows two tiles share stay in that XCD's L2.
-#include "common.hpp"
+#include "internal.hpp"
 
 namespace cfd {
 
@@ -70,14 +70,17 @@ struct J3Config {
 };
 static J3Config g_j3;
 
-int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
-                      int ze, int fixed_lo, int fixed_hi, float h2, float dt, int W, int zchunk,
-                      hipStream_t s);
+// defaults from the r01 tile sweep (1024^3): 14 output rows per tile, 64 planes
+int jacobi3d_tb_rows() { return g_j3.tb_rows ? g_j3.tb_rows : 14; }
+int jacobi3d_tb_zchunk() { return g_j3.tb_zchunk ? g_j3.tb_zchunk : 64; }
+bool jacobi3d_tb_enabled() { return g_j3.tb_steps != 1; }
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
-template <int W, bool USE_LDS, bool RESID, bool MASK>
+// PRE: `div` holds the precomputed rhs = (h2*div)/dt (cfd_rhs prologue);
+// otherwise the rhs is formed in-register (same bits, one fp32 division).
+template <int W, bool USE_LDS, bool RESID, bool MASK, bool PRE>
 __global__ __launch_bounds__(W * 64) void jacobi3d_march(
     const float *__restrict__ in, float *__restrict__ out, const float *__restrict__ div,
     const uint8_t *__restrict__ mask, int ny, int nx, int nseg, int ntile_y, int zb, int ze,
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(W * 64) void jacobi3d_march(
                 s = s + S[k];
                 s = s + U[k];
                 s = s + D[k];
-                val = sixth * (s - (h2 * dv[k]) / dt);
+                val = sixth * (s - (PRE ? dv[k] : (h2 * dv[k]) / dt));
             }
             if (MASK && mk[k]) val = 0.f;
             o[k] = val;
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(256) void jacobi3d_scalar(const float *__restrict__
                                                        float *__restrict__ out,
                                                        const float *__restrict__ div,
                                                        const uint8_t *__restrict__ mask, int ny,
-                                                       int nx, int zb, float h2, float dt,
+                                                       int nx, int zb, float h2, float dt, int pre,
                                                        float *__restrict__ resid) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y + 1;
@@ -241,7 +244,7 @@ __global__ __launch_bounds__(256) void jacobi3d_scalar(const float *__restrict__
             s = s + in[c - nx];
             s = s + in[c + plane];
             s = s + in[c - plane];
-            val = (1.0f / 6.0f) * (s - (h2 * div[c]) / dt);
+            val = (1.0f / 6.0f) * (s - (pre ? div[c] : (h2 * div[c]) / dt));
         }
         if (MASK && mask[c]) val = 0.f;
         out[c] = val;
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(256) void jacobi3d_scalar(const float *__restrict__
     if (resid) wave_reduce_max_store(ch, resid);
 }
 
-template <int W, bool USE_LDS>
+template <int W, bool USE_LDS, bool PRE>
 static void launch_march(const float *in, float *out, const float *div, const uint8_t *mask,
                          int ny, int nx, int zb, int ze, int zchunk, float h2, float dt,
                          float *resid, hipStream_t s) {
@@ -260,8 +263,8 @@ static void launch_march(const float *in, float *out, const float *div, const ui
     const int nzc = ceil_div(ze - zb, zchunk);
     const int blocks = nseg * ntile_y * nzc;
 #define CFD_J3_LAUNCH(R, M)                                                                    \
-    hipLaunchKernelGGL((jacobi3d_march<W, USE_LDS, R, M>), dim3(blocks), dim3(W * 64), 0, s, in, \
-                       out, div, mask, ny, nx, nseg, ntile_y, zb, ze, zchunk, h2, dt, resid)
+    hipLaunchKernelGGL((jacobi3d_march<W, USE_LDS, R, M, PRE>), dim3(blocks), dim3(W * 64), 0, s, \
+                       in, out, div, mask, ny, nx, nseg, ntile_y, zb, ze, zchunk, h2, dt, resid)
     if (resid) {
         if (mask) CFD_J3_LAUNCH(true, true); else CFD_J3_LAUNCH(true, false);
     } else {
@@ -270,10 +273,11 @@ static void launch_march(const float *in, float *out, const float *div, const ui
 #undef CFD_J3_LAUNCH
 }
 
-// Sweep planes [zb, ze) of in -> out (local array of nz planes).
-static int jacobi3d_sweep(const float *in, float *out, const float *div, const uint8_t *mask,
-                          int nz, int ny, int nx, int zb, int ze, float h2, float dt,
-                          float *resid, hipStream_t s) {
+// Sweep planes [zb, ze) of in -> out (local array of nz planes).  pre: `div`
+// is the precomputed rhs (launch_rhs), else the divergence.
+int jacobi3d_sweep(const float *in, float *out, const float *div, const uint8_t *mask, int nz,
+                   int ny, int nx, int zb, int ze, float h2, float dt, bool pre, float *resid,
+                   hipStream_t s) {
     if (ze <= zb || ny < 3) return CFD_OK;
     CFD_REQUIRE(zb >= 1 && ze <= nz - 1, "jacobi3d sweep: z range [%d,%d) outside 1..%d", zb, ze,
                 nz - 1);
@@ -283,33 +287,38 @@ static int jacobi3d_sweep(const float *in, float *out, const float *div, const u
         dim3 grid(ceil_div(nx, 256), ny - 2, ze - zb);
         if (mask)
             hipLaunchKernelGGL(jacobi3d_scalar<true>, grid, dim3(256), 0, s, in, out, div, mask, ny,
-                               nx, zb, h2, dt, resid);
+                               nx, zb, h2, dt, (int)pre, resid);
         else
             hipLaunchKernelGGL(jacobi3d_scalar<false>, grid, dim3(256), 0, s, in, out, div, mask,
-                               ny, nx, zb, h2, dt, resid);
+                               ny, nx, zb, h2, dt, (int)pre, resid);
         CFD_LAUNCH_CHECK();
         return CFD_OK;
     }
+    // defaults from the r01 tile sweep (1024^3): LDS tile, 16 rows, 64 planes
     int variant = g_j3.variant ? g_j3.variant : 1;
-    int W = g_j3.waves ? g_j3.waves : 4;
+    int W = g_j3.waves ? g_j3.waves : 16;
     const int nseg = ceil_div(nx, 256);
     const int L = ze - zb;
     int zchunk = g_j3.zchunk;
     if (zchunk <= 0) {
-        // aim for ~2048 workgroups (8 per CU) but keep >= 16 planes per march
+        // >= ~1024 workgroups when the grid allows, 64 planes per march otherwise
         const long tiles = (long)nseg * ceil_div(ny - 2, W);
-        int nzc = (int)((2048 + tiles - 1) / tiles);
+        int nzc = (int)((1024 + tiles - 1) / tiles);
         if (nzc < 1) nzc = 1;
         zchunk = ceil_div(L, nzc);
+        if (zchunk > 64) zchunk = 64;
         if (zchunk < 16) zchunk = 16;
     }
     if (zchunk > L) zchunk = L;
-#define CFD_J3_W(WV)                                                                           \
-    case WV:                                                                                   \
-        if (variant == 2)                                                                      \
-            launch_march<WV, false>(in, out, div, mask, ny, nx, zb, ze, zchunk, h2, dt, resid, s); \
-        else                                                                                   \
-            launch_march<WV, true>(in, out, div, mask, ny, nx, zb, ze, zchunk, h2, dt, resid, s);  \
+#define CFD_J3_W(WV)                                                                                 \
+    case WV:                                                                                         \
+        if (variant == 2) {                                                                          \
+            if (pre) launch_march<WV, false, true>(in, out, div, mask, ny, nx, zb, ze, zchunk, h2, dt, resid, s); \
+            else launch_march<WV, false, false>(in, out, div, mask, ny, nx, zb, ze, zchunk, h2, dt, resid, s); \
+        } else {                                                                                     \
+            if (pre) launch_march<WV, true, true>(in, out, div, mask, ny, nx, zb, ze, zchunk, h2, dt, resid, s); \
+            else launch_march<WV, true, false>(in, out, div, mask, ny, nx, zb, ze, zchunk, h2, dt, resid, s); \
+        }                                                                                            \
         break;
     switch (W) {
         CFD_J3_W(1)
@@ -322,6 +331,33 @@ static int jacobi3d_sweep(const float *in, float *out, const float *div, const u
             return CFD_E_INVALID;
     }
 #undef CFD_J3_W
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// rhs = (f32(h*h) * div) / dt over n cells (the Poisson RHS prologue; the
+// same bits the sweep kernels form in-register when no workspace is given).
+__global__ void k_rhs_f32(const float *__restrict__ div, float *__restrict__ rhs, size_t n4,
+                          size_t n, float h2, float dt) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n4; k += stride) {
+        float4 d = reinterpret_cast<const float4 *>(div)[k];
+        d.x = (h2 * d.x) / dt;
+        d.y = (h2 * d.y) / dt;
+        d.z = (h2 * d.z) / dt;
+        d.w = (h2 * d.w) / dt;
+        reinterpret_cast<float4 *>(rhs)[k] = d;
+    }
+    for (size_t k = 4 * n4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n; k += stride)
+        rhs[k] = (h2 * div[k]) / dt;
+}
+
+int launch_rhs_f32(const float *div, float *rhs, size_t n, float h2, float dt, hipStream_t s) {
+    const size_t n4 = (aligned16(div) && aligned16(rhs)) ? n / 4 : 0;
+    long blocks = (long)((n / 4 + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_rhs_f32, dim3(blocks), dim3(256), 0, s, div, rhs, n4, n, h2, dt);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }
@@ -400,13 +436,13 @@ int cfd_jacobi3d_sweep_f32(const float *in, float *out, const float *div, const 
                            float *resid, void *stream) {
     CFD_REQUIRE(in && out && div, "jacobi3d_sweep: null pointer");
     CFD_REQUIRE(nz >= 1 && ny >= 1 && nx >= 1, "jacobi3d_sweep: bad shape");
-    return jacobi3d_sweep(in, out, div, mask, nz, ny, nx, z_begin, z_end, (float)(h * h), dt,
+    return jacobi3d_sweep(in, out, div, mask, nz, ny, nx, z_begin, z_end, (float)(h * h), dt, false,
                           resid, as_stream(stream));
 }
 
-int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t *mask, int nz,
-                     int ny, int nx, double h, float dt, int iters, int resid_every,
-                     float *resid_out, void *stream) {
+int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws,
+                     const uint8_t *mask, int nz, int ny, int nx, double h, float dt, int iters,
+                     int resid_every, float *resid_out, void *stream) {
     CFD_REQUIRE(div && phi && phi_tmp, "jacobi3d: null array pointer");
     CFD_REQUIRE(nz >= 1 && ny >= 1 && nx >= 1 && iters >= 0, "jacobi3d: bad arguments");
     CFD_REQUIRE(resid_every <= 0 || resid_out, "jacobi3d: resid_every > 0 needs resid_out");
@@ -419,22 +455,31 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t
     const int nres = resid_every > 0 ? iters / resid_every : 0;
     if (nres > 0) CFD_CHECK_HIP(hipMemsetAsync(resid_out, 0, sizeof(float) * nres, s));
     const float h2 = (float)(h * h);
+    // RHS prologue: with a workspace the sweeps read rhs instead of dividing
+    const bool pre = rhs_ws != nullptr;
+    const float *src = div;
+    if (pre) {
+        if ((rc = launch_rhs_f32(div, rhs_ws, plane * nz, h2, dt, s))) return rc;
+        src = rhs_ws;
+    }
     float *a = phi, *b = phi_tmp;
     const int tk = timing_begin(s);
-    const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(div);
-    if (g_j3.tb_steps != 1 && !mask && resid_every <= 0 && vec_ok && nz >= 3 && ny >= 3 && iters >= 2) {
+    const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(src);
+    if (jacobi3d_tb_enabled() && !mask && resid_every <= 0 && vec_ok && nz >= 3 && ny >= 3 &&
+        iters >= 2) {
         // temporally blocked: one single sweep if iters is odd, then fused pairs
-        const int W = g_j3.tb_rows ? g_j3.tb_rows : 6;
         int done = 0;
         while (done < iters) {
-            if ((iters - done) & 1)
-                rc = jacobi3d_sweep(a, b, div, mask, nz, ny, nx, 1, nz - 1, h2, dt, nullptr, s);
+            const bool single = (iters - done) & 1;
+            if (single)
+                rc = jacobi3d_sweep(a, b, src, mask, nz, ny, nx, 1, nz - 1, h2, dt, pre, nullptr, s);
             else
-                rc = jacobi3d_tb2_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt, W, g_j3.tb_zchunk, s);
+                rc = jacobi3d_tb2_pass(a, b, src, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt,
+                                       jacobi3d_tb_rows(), jacobi3d_tb_zchunk(), pre, s);
             if (rc) return rc;
             if (done == 0 && (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, 0, nz, 0, nz - 1, s)))
                 return rc;
-            done += ((iters - done) & 1) ? 1 : 2;
+            done += single ? 1 : 2;
             float *t = a;
             a = b;
             b = t;
@@ -448,7 +493,7 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t
         float *r = (resid_every > 0 && (it + 1) % resid_every == 0)
                        ? resid_out + ((it + 1) / resid_every - 1)
                        : nullptr;
-        if ((rc = jacobi3d_sweep(a, b, div, mask, nz, ny, nx, 1, nz - 1, h2, dt, r, s))) return rc;
+        if ((rc = jacobi3d_sweep(a, b, src, mask, nz, ny, nx, 1, nz - 1, h2, dt, pre, r, s))) return rc;
         if (it == 0 && iters > 1 &&
             (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, 0, nz, 0, nz - 1, s)))
             return rc;

@@ -14,11 +14,9 @@
 // (SlabPlan in the Python package) and tested there on CPU with gloo.
 #include <rccl/rccl.h>
 
-#include "common.hpp"
+#include "internal.hpp"
 
 namespace cfd {
-int launch_fix_faces3d(const float *src, float *dst, const uint8_t *mask, int ny, int nx, int za,
-                       int zb, int full_lo, int full_hi, hipStream_t s);
 
 struct SlabComm {
     ncclComm_t comm = nullptr;
@@ -36,17 +34,21 @@ struct SlabComm {
         }                                                                                 \
     } while (0)
 
-// ghost exchange of array `a` (local planes 0..nzl+1)
-static int exchange(SlabComm *c, float *a, int nzl, size_t plane, int lo, int hi, hipStream_t s) {
+// Ghost exchange of array `a` (local planes 0 .. nzl+2G-1, owned G .. G+nzl-1):
+// the G owned planes next to each neighbour go into that neighbour's G ghost
+// planes; each direction is one contiguous message of G planes.
+static int exchange(SlabComm *c, float *a, int nzl, int G, size_t plane, int lo, int hi,
+                    hipStream_t s) {
     if (lo < 0 && hi < 0) return CFD_OK;
+    const size_t n = (size_t)G * plane;
     CFD_CHECK_NCCL(ncclGroupStart());
     if (lo >= 0) {
-        CFD_CHECK_NCCL(ncclSend(a + plane, plane, ncclFloat32, lo, c->comm, s));
-        CFD_CHECK_NCCL(ncclRecv(a, plane, ncclFloat32, lo, c->comm, s));
+        CFD_CHECK_NCCL(ncclSend(a + (size_t)G * plane, n, ncclFloat32, lo, c->comm, s));
+        CFD_CHECK_NCCL(ncclRecv(a, n, ncclFloat32, lo, c->comm, s));
     }
     if (hi >= 0) {
-        CFD_CHECK_NCCL(ncclSend(a + (size_t)nzl * plane, plane, ncclFloat32, hi, c->comm, s));
-        CFD_CHECK_NCCL(ncclRecv(a + (size_t)(nzl + 1) * plane, plane, ncclFloat32, hi, c->comm, s));
+        CFD_CHECK_NCCL(ncclSend(a + (size_t)nzl * plane, n, ncclFloat32, hi, c->comm, s));
+        CFD_CHECK_NCCL(ncclRecv(a + (size_t)(nzl + G) * plane, n, ncclFloat32, hi, c->comm, s));
     }
     CFD_CHECK_NCCL(ncclGroupEnd());
     return CFD_OK;
@@ -57,10 +59,6 @@ static int exchange(SlabComm *c, float *a, int nzl, size_t plane, int lo, int hi
 using namespace cfd;
 
 extern "C" {
-
-int cfd_jacobi3d_sweep_f32(const float *in, float *out, const float *div, const uint8_t *mask,
-                           int nz, int ny, int nx, int z_begin, int z_end, double h, float dt,
-                           float *resid, void *stream);
 
 int cfd_comm_unique_id(void *out, size_t bytes) {
     CFD_REQUIRE(out && bytes >= sizeof(ncclUniqueId), "comm_unique_id: need %zu bytes",
@@ -111,71 +109,90 @@ int cfd_comm_destroy(void *comm) {
 }
 
 int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
-                          const uint8_t *mask, int nz_local, int ny, int nx, int lo_peer,
-                          int hi_peer, int z_update_begin, int z_update_end, double h, float dt,
-                          int iters, int overlap, void *stream, void *comm_stream) {
+                          float *rhs_ws, const uint8_t *mask, int nz_local, int ghost, int ny,
+                          int nx, int lo_peer, int hi_peer, int z_update_begin, int z_update_end,
+                          double h, float dt, int iters, int overlap, void *stream,
+                          void *comm_stream) {
     SlabComm *c = reinterpret_cast<SlabComm *>(comm);
     CFD_REQUIRE(c && div && phi && phi_tmp, "slab_jacobi3d: null pointer");
-    CFD_REQUIRE(nz_local >= 1 && ny >= 1 && nx >= 1 && iters >= 0, "slab_jacobi3d: bad shape");
-    CFD_REQUIRE(z_update_begin >= 1 && z_update_end <= nz_local + 1 &&
+    CFD_REQUIRE(ghost == 1 || ghost == 2, "slab_jacobi3d: ghost depth must be 1 or 2");
+    CFD_REQUIRE(nz_local >= ghost && ny >= 1 && nx >= 1 && iters >= 0, "slab_jacobi3d: bad shape");
+    const int G = ghost;
+    CFD_REQUIRE(z_update_begin >= G && z_update_end <= nz_local + G &&
                     z_update_begin <= z_update_end,
-                "slab_jacobi3d: update range [%d,%d) outside owned planes 1..%d", z_update_begin,
-                z_update_end, nz_local);
+                "slab_jacobi3d: update range [%d,%d) outside owned planes %d..%d", z_update_begin,
+                z_update_end, G, nz_local + G - 1);
     CFD_REQUIRE(lo_peer < c->nranks && hi_peer < c->nranks, "slab_jacobi3d: bad peer");
     if (iters == 0) return CFD_OK;
     hipStream_t s = as_stream(stream);
     hipStream_t cs = comm_stream ? as_stream(comm_stream) : s;
-    const int nzt = nz_local + 2;
+    const int nzt = nz_local + 2 * G;
     const size_t plane = (size_t)ny * nx;
+    const float h2 = (float)(h * h);
     int rc;
     // Dirichlet faces of the owned planes: rows y=0, ny-1, and the global
-    // boundary planes (owned planes outside the update range) in full.  Ghost
-    // planes arrive whole from the neighbours (their face rows are never read).
-    const int full_lo = z_update_begin > 1 ? 1 : -1;
-    const int full_hi = z_update_end < nz_local + 1 ? nz_local : -1;
-    if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, 1, nz_local + 1, full_lo, full_hi, s)))
+    // boundary planes (owned planes outside the update range) in full.
+    // Ghost planes arrive whole from the neighbours.
+    const int full_lo = z_update_begin > G ? G : -1;
+    const int full_hi = z_update_end < nz_local + G ? nz_local + G - 1 : -1;
+    if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
         return rc;
+    const bool pre = rhs_ws != nullptr;
+    const float *src = div;
+    if (pre) {
+        if ((rc = launch_rhs_f32(div, rhs_ws, plane * nzt, h2, dt, s))) return rc;
+        src = rhs_ws;
+    }
     // ghosts of the initial guess
-    if ((rc = exchange(c, phi, nz_local, plane, lo_peer, hi_peer, s))) return rc;
-    const float h2f = (float)(h * h);
-    (void)h2f;
+    if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
     const int zb = z_update_begin, ze = z_update_end;
-    // planes whose values a neighbour needs next sweep
-    const bool lo_b = lo_peer >= 0 && zb == 1;
-    const bool hi_b = hi_peer >= 0 && ze == nz_local + 1;
+    const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(src);
+    // two sweeps per pass needs 2-deep ghosts (and no mask)
+    const bool tb = G == 2 && jacobi3d_tb_enabled() && !mask && vec_ok && ny >= 3;
+    const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
+    // owned planes a neighbour needs after each pass: the G next to it
+    const bool lo_b = lo_peer >= 0, hi_b = hi_peer >= 0;
+    const bool can_overlap = overlap && c->nranks > 1 && (ze - zb) >= 2 * G + 1;
     float *a = phi, *b = phi_tmp;
     const int tk = timing_begin(s);
-    for (int it = 0; it < iters; ++it) {
-        if (!overlap || c->nranks == 1) {
-            if ((rc = cfd_jacobi3d_sweep_f32(a, b, div, mask, nzt, ny, nx, zb, ze, h, dt, nullptr, s)))
-                return rc;
-            if ((rc = exchange(c, b, nz_local, plane, lo_peer, hi_peer, s))) return rc;
+    int done = 0;
+    while (done < iters) {
+        const bool pair = tb && (iters - done) >= 2 && !((iters - done) & 1);
+        auto run = [&](int z0, int z1) -> int {
+            if (z1 <= z0) return CFD_OK;
+            if (pair)
+                return jacobi3d_tb2_pass(a, b, src, nzt, ny, nx, z0, z1, z0 == zb && fixed_lo,
+                                         z1 == ze && fixed_hi, h2, dt, jacobi3d_tb_rows(),
+                                         jacobi3d_tb_zchunk(), pre, s);
+            return jacobi3d_sweep(a, b, src, mask, nzt, ny, nx, z0, z1, h2, dt, pre, nullptr, s);
+        };
+        if (!can_overlap) {
+            if ((rc = run(zb, ze))) return rc;
+            if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
         } else {
-            int ib = zb, ie = ze;  // interior range after peeling boundary planes
-            if (lo_b && ib < ie) {
-                if ((rc = cfd_jacobi3d_sweep_f32(a, b, div, mask, nzt, ny, nx, 1, 2, h, dt, nullptr, s)))
-                    return rc;
-                ib = 2;
+            // boundary planes first, their exchange on the comm stream, the
+            // interior meanwhile on the main stream
+            int ib = zb, ie = ze;
+            if (lo_b) {
+                if ((rc = run(zb, zb + G))) return rc;
+                ib = zb + G;
             }
-            if (hi_b && ib < ie) {
-                if ((rc = cfd_jacobi3d_sweep_f32(a, b, div, mask, nzt, ny, nx, ie - 1, ie, h, dt,
-                                                 nullptr, s)))
-                    return rc;
-                ie -= 1;
+            if (hi_b) {
+                if ((rc = run(ze - G, ze))) return rc;
+                ie = ze - G;
             }
             CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
             CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
-            if ((rc = exchange(c, b, nz_local, plane, lo_peer, hi_peer, cs))) return rc;
+            if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, cs))) return rc;
             CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
-            if (ib < ie &&
-                (rc = cfd_jacobi3d_sweep_f32(a, b, div, mask, nzt, ny, nx, ib, ie, h, dt, nullptr, s)))
-                return rc;
+            if ((rc = run(ib, ie))) return rc;
             CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
         }
-        // after sweep 1, the other buffer gets the final owned faces too
-        if (it == 0 && iters > 1 &&
-            (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, 1, nz_local + 1, full_lo, full_hi, s)))
+        // after the first pass, the other buffer gets the final owned faces too
+        if (done == 0 &&
+            (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
             return rc;
+        done += pair ? 2 : 1;
         float *t = a;
         a = b;
         b = t;

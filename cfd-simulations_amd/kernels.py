@@ -128,9 +128,10 @@ def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iteratio
 
 
 def solve_pressure_jacobi(phi, div_u_star, dx, dt, mask, iterations, phi_tmp=None,
-                          resid_every=0, resid_out=None):
+                          resid_every=0, resid_out=None, rhs_ws=None):
     """Jacobi branch of solve_pressure_fast, v5.py:336-346, bit-exact; in place
-    on ``phi`` (float32 or float64 fields); returns ``phi``."""
+    on ``phi`` (float32 or float64 fields); returns ``phi``.  ``rhs_ws``: an
+    optional same-size workspace that lets the sweeps skip the division."""
     ny, nx = _shape2d(phi)
     if div_u_star.dtype != phi.dtype:
         raise TypeError("phi and div_u_star must share a dtype")
@@ -139,21 +140,21 @@ def solve_pressure_jacobi(phi, div_u_star, dx, dt, mask, iterations, phi_tmp=Non
     fn = {torch.float32: "cfd_jacobi2d_f32", torch.float64: "cfd_jacobi2d_f64"}.get(phi.dtype)
     if fn is None:
         raise TypeError(f"unsupported dtype {phi.dtype}")
-    call(fn, ptr(div_u_star), ptr(phi), ptr(tmp), ptr(m), ny, nx, float(dx), float(np.float32(dt)),
-         int(iterations), int(resid_every), ptr(resid_out), stream_handle())
+    call(fn, ptr(div_u_star), ptr(phi), ptr(tmp), ptr(rhs_ws), ptr(m), ny, nx, float(dx),
+         float(np.float32(dt)), int(iterations), int(resid_every), ptr(resid_out), stream_handle())
     return phi
 
 
 def solve_pressure_jacobi3d(phi, div, h, dt, mask, iterations, phi_tmp=None, resid_every=0,
-                            resid_out=None):
+                            resid_out=None, rhs_ws=None):
     """7-point generalisation of the Jacobi branch on an (nz, ny, nx) float32 grid."""
     if phi.dim() != 3:
         raise ValueError("expected (nz, ny, nx)")
     nz, ny, nx = (int(s) for s in phi.shape)
     tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
     m = _mask_u8(mask, phi.shape)
-    call("cfd_jacobi3d_f32", ptr(_f32(div, "div")), ptr(_f32(phi, "phi")), ptr(tmp), ptr(m), nz, ny, nx,
-         float(h), float(np.float32(dt)), int(iterations), int(resid_every), ptr(resid_out),
+    call("cfd_jacobi3d_f32", ptr(_f32(div, "div")), ptr(_f32(phi, "phi")), ptr(tmp), ptr(rhs_ws), ptr(m),
+         nz, ny, nx, float(h), float(np.float32(dt)), int(iterations), int(resid_every), ptr(resid_out),
          stream_handle())
     return phi
 

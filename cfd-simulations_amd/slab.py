@@ -5,14 +5,16 @@ The reference runs on one node's CPU threads (SURVEY.md section 2,
 rank holds its owned planes plus one ghost plane per side.  After every sweep
 the ranks swap boundary planes with their z-neighbours over RCCL send/recv
 (xGMI), and that swap overlaps the interior sweep on a second HIP stream.
-Jacobi updates reassociate nothing across planes, so the decomposed result is
-bit-identical to the single-GPU one for every rank count.
+With 2-deep ghosts the sweeps run temporally blocked: two sweeps per pass and
+one 2-plane exchange per pass, half as many messages at the same bytes per
+sweep.  Jacobi updates reassociate nothing across planes, so the decomposed
+result is bit-identical to the single-GPU one for every rank count.
 
 ``SlabPlan`` is pure host logic: ownership, peers, update range and the
 exchange list.  The C driver ``cfd_slab_jacobi3d_f32`` executes the same
-exchange list: it sends plane 1 to ``lo_peer`` into that rank's ghost plane
-``nz_local+1``, and plane ``nz_local`` to ``hi_peer`` into its ghost plane 0.
-The CPU tests run the plan on gloo with world_size 2.
+exchange list: it sends the ``ghost`` owned planes next to each neighbour into
+that neighbour's ghost planes (``SlabPlan.exchanges()``).  The CPU tests run
+the plan on gloo with world_size 2 and 3.
 """
 from __future__ import annotations
 
@@ -28,15 +30,22 @@ UNIQUE_ID_BYTES = 128
 
 @dataclass(frozen=True)
 class SlabPlan:
+    """Ownership and halo plan of one rank.  Local arrays hold the owned
+    planes plus ``ghost`` planes per side (2 for temporally blocked passes):
+    local index k <-> global plane z_lo - ghost + k."""
     nz: int        # global planes
     nranks: int
     rank: int
+    ghost: int = 1
 
     def __post_init__(self):
         if not (0 <= self.rank < self.nranks):
             raise ValueError("rank out of range")
-        if self.nz < self.nranks:
-            raise ValueError(f"cannot split {self.nz} planes over {self.nranks} ranks")
+        if self.ghost not in (1, 2):
+            raise ValueError("ghost depth must be 1 or 2")
+        if self.nz < self.nranks * self.ghost:
+            raise ValueError(f"cannot split {self.nz} planes over {self.nranks} ranks "
+                             f"with {self.ghost}-deep ghosts")
 
     @property
     def z_lo(self) -> int:
@@ -54,6 +63,11 @@ class SlabPlan:
         return self.z_hi - self.z_lo
 
     @property
+    def nz_total(self) -> int:
+        """Planes of the local array, ghosts included."""
+        return self.nz_local + 2 * self.ghost
+
+    @property
     def lo_peer(self) -> int:
         return self.rank - 1 if self.rank > 0 else -1
 
@@ -64,46 +78,47 @@ class SlabPlan:
     @property
     def z_update_begin(self) -> int:
         """Local index of the first updated plane (global plane 0 is Dirichlet)."""
-        return 2 if self.z_lo == 0 else 1
+        return self.ghost + (1 if self.z_lo == 0 else 0)
 
     @property
     def z_update_end(self) -> int:
         """Local index one past the last updated plane (global nz-1 is Dirichlet)."""
-        return self.nz_local if self.z_hi == self.nz else self.nz_local + 1
+        return self.ghost + self.nz_local - (1 if self.z_hi == self.nz else 0)
 
     def exchanges(self):
-        """[(send_local_plane, peer, peer_recv_local_plane_on_that_rank)]: the
-        list the C driver executes after each sweep."""
+        """[(send_first_local_plane, count, peer, peer_recv_first_local_plane)]:
+        the messages the C driver sends after each pass."""
+        g = self.ghost
         out = []
         if self.lo_peer >= 0:
-            lo = SlabPlan(self.nz, self.nranks, self.lo_peer)
-            out.append((1, self.lo_peer, lo.nz_local + 1))
+            lo = SlabPlan(self.nz, self.nranks, self.lo_peer, g)
+            out.append((g, g, self.lo_peer, lo.nz_local + g))
         if self.hi_peer >= 0:
-            out.append((self.nz_local, self.hi_peer, 0))
+            out.append((self.nz_local, g, self.hi_peer, 0))
         return out
 
     def receives(self):
-        """[(local_ghost_plane, peer)]: where this rank's ghosts come from."""
+        """[(first_local_ghost_plane, count, peer)]: where the ghosts come from."""
+        g = self.ghost
         out = []
         if self.lo_peer >= 0:
-            out.append((0, self.lo_peer))
+            out.append((0, g, self.lo_peer))
         if self.hi_peer >= 0:
-            out.append((self.nz_local + 1, self.hi_peer))
+            out.append((self.nz_local + g, g, self.hi_peer))
         return out
 
-    def local_slice(self):
-        """Global planes held locally, ghosts included (clipped at the faces)."""
-        return slice(max(self.z_lo - 1, 0), min(self.z_hi + 1, self.nz))
+    def owned(self) -> slice:
+        return slice(self.ghost, self.ghost + self.nz_local)
 
     def scatter(self, glob: np.ndarray) -> np.ndarray:
-        """Local (nz_local+2, ny, nx) view-copy of a global array; ghost planes
-        outside the domain are zero."""
-        loc = np.zeros((self.nz_local + 2,) + glob.shape[1:], glob.dtype)
-        lo = self.z_lo - 1
-        for k in range(self.nz_local + 2):
-            g = lo + k
-            if 0 <= g < self.nz:
-                loc[k] = glob[g]
+        """Local (nz_total, ny, nx) copy of a global array; ghost planes outside
+        the domain are zero."""
+        loc = np.zeros((self.nz_total,) + glob.shape[1:], glob.dtype)
+        base = self.z_lo - self.ghost
+        for k in range(self.nz_total):
+            gz = base + k
+            if 0 <= gz < self.nz:
+                loc[k] = glob[gz]
         return loc
 
 
@@ -150,17 +165,20 @@ class RcclComm:
 
 
 class SlabJacobi3D:
-    """Distributed 7-point Jacobi on this rank's slab (device tensors)."""
+    """Distributed 7-point Jacobi on this rank's slab (device tensors).  With
+    ``plan.ghost == 2`` the sweeps run temporally blocked (two per pass, one
+    2-plane halo exchange per pass)."""
 
     def __init__(self, plan: SlabPlan, ny: int, nx: int, h: float, dt, comm: RcclComm | None,
-                 device=None, mask=None):
+                 device=None, mask=None, rhs_workspace: bool = True):
         self.plan, self.ny, self.nx = plan, ny, nx
         self.h, self.dt = float(h), np.float32(dt)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        shape = (plan.nz_local + 2, ny, nx)
+        shape = (plan.nz_total, ny, nx)
         self.div = torch.zeros(shape, dtype=torch.float32, device=self.device)
         self.phi = torch.zeros(shape, dtype=torch.float32, device=self.device)
         self.tmp = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        self.rhs = torch.empty(shape, dtype=torch.float32, device=self.device) if rhs_workspace else None
         self.mask = None if mask is None else mask.to(torch.uint8).contiguous()
         self.comm = comm
         self.comm_stream = torch.cuda.Stream(device=self.device)
@@ -170,13 +188,13 @@ class SlabJacobi3D:
             self.phi.zero_()
         p = self.plan
         call("cfd_slab_jacobi3d_f32", self.comm.handle, ptr(self.div), ptr(self.phi), ptr(self.tmp),
-             ptr(self.mask), p.nz_local, self.ny, self.nx, p.lo_peer, p.hi_peer, p.z_update_begin,
-             p.z_update_end, self.h, float(self.dt), int(iters), int(bool(overlap)), stream_handle(),
-             self.comm_stream.cuda_stream)
+             ptr(self.rhs), ptr(self.mask), p.nz_local, p.ghost, self.ny, self.nx, p.lo_peer, p.hi_peer,
+             p.z_update_begin, p.z_update_end, self.h, float(self.dt), int(iters), int(bool(overlap)),
+             stream_handle(), self.comm_stream.cuda_stream)
         return self.phi
 
     def owned(self) -> torch.Tensor:
-        return self.phi[1:self.plan.nz_local + 1]
+        return self.phi[self.plan.owned()]
 
 
 def sweep_range(phi_in, phi_out, div, mask, z_begin, z_end, h, dt, resid=None):

@@ -160,6 +160,7 @@ class OptimizedTurbulentSolver:
         self.u, self.v, self.p, self.nu_t, self.tau_supg = z(), z(), z(), z(), z()
         self.u_star, self.v_star, self.div_u_star, self.phi = z(), z(), z(), z()
         self._phi_tmp = z()
+        self._rhs_ws = z()
         self._gs_ws = torch.empty(int(lib().cfd_rbgs_workspace_bytes(cfg.pressure_iterations)),
                                   dtype=torch.uint8, device=self.device)
         self._gs_done = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -200,7 +201,7 @@ class OptimizedTurbulentSolver:
                                                iters_done=self._gs_done)
         else:
             K.solve_pressure_jacobi(self.phi, div_u_star, cfg.dx, cfg.dt, self._mask_u8,
-                                    cfg.pressure_iterations, phi_tmp=self._phi_tmp)
+                                    cfg.pressure_iterations, phi_tmp=self._phi_tmp, rhs_ws=self._rhs_ws)
         return self.phi
 
     def apply_boundary_conditions(self, u, v):  # v5.py:349-360

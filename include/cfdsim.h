@@ -59,23 +59,25 @@ const char *cfd_device_arch(void);
  * Bit-exact with the reference (same op order, no FMA contraction).
  * phi (in/out) holds the initial guess; the reference zero-fills it first
  * (v5.py:337); the caller does that.  phi_tmp is a same-size scratch array.
+ * rhs_ws (optional, same size): when given, the RHS f32(dx**2)*div/dt is
+ * formed once per solve (the same bits) and the sweeps skip the division.
  * Edges keep their values (Dirichlet), except masked edge cells -> 0.
  * resid_every > 0: after every resid_every-th iteration k, max|phi_new - phi|
  * over updated cells is written to resid_out[k/resid_every - 1] (device array
  * of floor(iters/resid_every) elements; an extension, the reference has none). */
-int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t *mask,
-                     int ny, int nx, double dx, float dt, int iters,
+int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws,
+                     const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, float *resid_out, void *stream);
 /* fp64 fields (memory_efficient=False, v5.py:287); dt promotes exactly. */
-int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, const uint8_t *mask,
-                     int ny, int nx, double dx, float dt, int iters,
+int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
+                     const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, double *resid_out, void *stream);
 
 /* 3-D 7-point generalisation of the same Jacobi template (the reference is
  * 2-D only): phi_new = f32(1/6) * (((((E+W)+N)+S)+U)+D - f32(h*h)*div/dt),
  * six Dirichlet faces held, mask -> 0.  Layout (nz, ny, nx). */
-int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, const uint8_t *mask,
-                     int nz, int ny, int nx, double h, float dt, int iters,
+int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws,
+                     const uint8_t *mask, int nz, int ny, int nx, double h, float dt, int iters,
                      int resid_every, float *resid_out, void *stream);
 
 /* Replaces solve_pressure_gauss_seidel_fast, v5.py:202-226 (the
@@ -171,14 +173,20 @@ int cfd_comm_unique_id(void *out, size_t bytes); /* bytes >= 128 */
 int cfd_comm_init(const void *unique_id, int nranks, int rank, void **comm);
 int cfd_comm_destroy(void *comm);
 /* Exchange plan, computed and tested on the host (SlabPlan in the package):
- * lo_peer / hi_peer: neighbour ranks or -1.  z_update_begin/end: owned planes
- * that are updated (global Dirichlet planes are excluded).  overlap != 0:
- * the two boundary planes are swept first, their halo exchange runs on a
- * second stream (comm_stream) while the interior sweeps on `stream`. */
+ * ghost = ghost planes per side (1, or 2 for temporally blocked passes):
+ * local array (nz_local + 2*ghost, ny, nx), owned planes ghost ..
+ * ghost+nz_local-1.  lo_peer / hi_peer: neighbour ranks or -1.
+ * z_update_begin/end: local indices of the owned planes that are updated
+ * (global Dirichlet planes excluded).  After each pass the `ghost` owned
+ * planes next to a neighbour go into its ghost planes.  rhs_ws: optional
+ * same-size workspace (see cfd_jacobi2d_f32).  overlap != 0: the boundary
+ * planes are computed first, their exchange runs on comm_stream while the
+ * interior computes on `stream`. */
 int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
-                          const uint8_t *mask, int nz_local, int ny, int nx, int lo_peer,
-                          int hi_peer, int z_update_begin, int z_update_end, double h, float dt,
-                          int iters, int overlap, void *stream, void *comm_stream);
+                          float *rhs_ws, const uint8_t *mask, int nz_local, int ghost, int ny,
+                          int nx, int lo_peer, int hi_peer, int z_update_begin, int z_update_end,
+                          double h, float dt, int iters, int overlap, void *stream,
+                          void *comm_stream);
 /* Single-sweep building block (also used by the slab tests on one GPU):
  * update planes [z_begin, z_end) of in -> out (local array of nz planes);
  * x/y faces copied through, masked cells -> 0.  resid (optional, device float,

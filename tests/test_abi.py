@@ -47,7 +47,7 @@ def test_library_identifies_itself():
 def test_invalid_arguments_report_errors_without_gpu():
     """Argument validation runs before any device work."""
     with pytest.raises(_lib.CfdError, match="null"):
-        _lib.call("cfd_jacobi2d_f32", None, None, None, None, 8, 8, 0.1, 1.0, 1, 0, None, None)
+        _lib.call("cfd_jacobi2d_f32", None, None, None, None, None, 8, 8, 0.1, 1.0, 1, 0, None, None)
     with pytest.raises(_lib.CfdError, match="waves"):
         _lib.call("cfd_set_jacobi3d_config", 1, 3, 0)
 

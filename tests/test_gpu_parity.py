@@ -73,6 +73,31 @@ def test_jacobi2d_random_bitexact(dtype, shape, iters):
     assert np.array_equal(host(phi), ref)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_jacobi2d_rhs_workspace_bitexact(dtype):
+    """The RHS prologue (rhs_ws) gives the same bits as the in-register RHS."""
+    rng = np.random.default_rng(12)
+    shape = (70, 132)
+    div = rng.standard_normal(shape).astype(dtype)
+    mask = rng.random(shape) < 0.05
+    ref = oracle.jacobi2d(div, dx=0.011, dt=np.float32(7e-5), iters=9, mask=mask)
+    phi = torch.zeros(shape, dtype=torch.float32 if dtype == np.float32 else torch.float64, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(div), 0.011, np.float32(7e-5), dev(mask), 9, rhs_ws=torch.empty_like(phi))
+    assert np.array_equal(host(phi), ref)
+
+
+@pytest.mark.parametrize("tb", [1, 2])
+@pytest.mark.parametrize("shape,iters", [((12, 14, 64), 6), ((9, 10, 260), 5), ((7, 9, 13), 3)])
+def test_jacobi3d_rhs_workspace_bitexact(shape, iters, tb):
+    call("cfd_set_jacobi3d_blocking", tb, 0, 0)
+    rng = np.random.default_rng(13)
+    div = rng.standard_normal(shape).astype(np.float32)
+    ref = oracle.jacobi3d(div, h=0.02, dt=np.float32(3e-4), iters=iters)
+    phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+    K.solve_pressure_jacobi3d(phi, dev(div), 0.02, np.float32(3e-4), None, iters, rhs_ws=torch.empty_like(phi))
+    assert np.array_equal(host(phi), ref)
+
+
 def test_jacobi2d_residual():
     rng = np.random.default_rng(3)
     div = rng.standard_normal((64, 96)).astype(np.float32)
@@ -313,7 +338,7 @@ def test_time_step_vs_reference(golden, branch):
 
 # ------------------------------------------------------------- slabs
 def test_slab_sweeps_emulated_on_one_gpu():
-    """The slab driver's building blocks (cfd_jacobi3d_sweep_f32 on local
+    """The slab driver's building block (cfd_jacobi3d_sweep_f32 on local
     arrays with ghost planes) with the SlabPlan exchange list, emulated on
     one GPU for 3 slabs: bit-identical to the single-domain solve."""
     nz, ny, nx, iters, R = 23, 18, 36, 6, 3
@@ -328,23 +353,24 @@ def test_slab_sweeps_emulated_on_one_gpu():
         for p, a, b, d_ in zip(plans, A, B, D):
             S.sweep_range(a, b, d_, None, p.z_update_begin, p.z_update_end, 0.07, np.float32(4e-3))
         for p, b in zip(plans, B):
-            for send, peer, recv in p.exchanges():
-                B[peer][recv].copy_(b[send])
+            for first, count, peer, recv in p.exchanges():
+                B[peer][recv:recv + count].copy_(b[first:first + count])
         A, B = B, A
-    got = np.concatenate([host(a)[1:p.nz_local + 1] for p, a in zip(plans, A)])
+    got = np.concatenate([host(a)[p.owned()] for p, a in zip(plans, A)])
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("ghost", [1, 2])
 @pytest.mark.parametrize("overlap", [False, True])
-def test_slab_rccl_single_rank(overlap):
+def test_slab_rccl_single_rank(overlap, ghost):
     """The RCCL slab driver with a one-rank communicator equals the plain solve."""
     n, iters = 40, 7
     rng = np.random.default_rng(10)
     div = rng.standard_normal((n, n, n + 8)).astype(np.float32)
     ref = oracle.jacobi3d(div, h=0.05, dt=np.float32(1e-3), iters=iters)
-    plan = S.SlabPlan(n, 1, 0)
     comm = S.RcclComm(0, 1)
     try:
+        plan = S.SlabPlan(n, 1, 0, ghost=ghost)
         sj = S.SlabJacobi3D(plan, n, n + 8, 0.05, np.float32(1e-3), comm)
         sj.div.copy_(dev(plan.scatter(div)))
         sj.solve(iters, overlap=overlap)

@@ -33,7 +33,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, nz, ny, nx, iters, out_dir):
+def _worker(rank, world, port, nz, ny, nx, iters, ghost, out_dir):
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
@@ -48,40 +48,57 @@ def _worker(rank, world, port, nz, ny, nx, iters, out_dir):
     try:
         rng = np.random.default_rng(42)
         div = rng.standard_normal((nz, ny, nx)).astype(np.float32)
-        p = Plan(nz, world, rank)
+        p = Plan(nz, world, rank, ghost)
         dloc = p.scatter(div)
         phi = np.zeros_like(dloc)
         zb, ze = p.z_update_begin, p.z_update_end
-        for _ in range(iters):
-            new = phi.copy()
-            if ze > zb:
-                # one sweep of planes [zb, ze): the oracle on the sub-block with
-                # planes zb-1 and ze as held boundaries
-                new[zb - 1:ze + 1] = oracle.jacobi3d(dloc[zb - 1:ze + 1], phi[zb - 1:ze + 1], h=0.05,
+        fixed_lo, fixed_hi = p.z_lo == 0, p.z_hi == nz
+
+        def sweep(a, lo, hi):
+            # one sweep of planes [lo, hi): the oracle on the sub-block with
+            # planes lo-1 and hi held
+            out = a.copy()
+            if hi > lo:
+                out[lo - 1:hi + 1] = oracle.jacobi3d(dloc[lo - 1:hi + 1], a[lo - 1:hi + 1], h=0.05,
                                                      dt=np.float32(2e-3), iters=1)
-            reqs = []
-            for send_plane, peer, _ in p.exchanges():
-                reqs.append(dist.isend(torch.from_numpy(new[send_plane].copy()), dst=peer))
-            bufs = []
-            for ghost, peer in p.receives():
-                t = torch.empty((ny, nx), dtype=torch.float32)
+            return out
+
+        done = 0
+        while done < iters:
+            if ghost == 2 and (iters - done) % 2 == 0:
+                # the fused pass: level 1 on [zb-1, ze+1) (inner ghosts too,
+                # unless they are global Dirichlet planes), level 2 on [zb, ze)
+                l1 = sweep(phi, zb - 1 + fixed_lo, ze + 1 - fixed_hi)
+                new = phi.copy()
+                new[zb:ze] = sweep(l1, zb, ze)[zb:ze]
+                done += 2
+            else:
+                new = sweep(phi, zb, ze)
+                done += 1
+            reqs, bufs = [], []
+            for first, count, peer, _ in p.exchanges():
+                reqs.append(dist.isend(torch.from_numpy(new[first:first + count].copy()), dst=peer))
+            for first, count, peer in p.receives():
+                t = torch.empty((count, ny, nx), dtype=torch.float32)
                 reqs.append(dist.irecv(t, src=peer))
-                bufs.append((ghost, t))
+                bufs.append((first, count, t))
             for r in reqs:
                 r.wait()
-            for ghost, t in bufs:
-                new[ghost] = t.numpy()
+            for first, count, t in bufs:
+                new[first:first + count] = t.numpy()
             phi = new
-        np.save(os.path.join(out_dir, f"rank{rank}.npy"), phi[1:p.nz_local + 1])
+        np.save(os.path.join(out_dir, f"rank{rank}.npy"), phi[p.owned()])
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nz", [(2, 17), (3, 20)])
-def test_slab_decomposition_gloo_bitexact(tmp_path, world, nz):
+@pytest.mark.parametrize("world,nz,ghost,iters", [(2, 17, 1, 5), (3, 20, 1, 5), (2, 17, 2, 6),
+                                                  (3, 21, 2, 7), (3, 8, 2, 4)])
+def test_slab_decomposition_gloo_bitexact(tmp_path, world, nz, ghost, iters):
     import oracle
-    ny, nx, iters = 9, 12, 5
-    mp.spawn(_worker, args=(world, _free_port(), nz, ny, nx, iters, str(tmp_path)), nprocs=world, join=True)
+    ny, nx = 9, 12
+    mp.spawn(_worker, args=(world, _free_port(), nz, ny, nx, iters, ghost, str(tmp_path)), nprocs=world,
+             join=True)
     got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
     rng = np.random.default_rng(42)
     div = rng.standard_normal((nz, ny, nx)).astype(np.float32)
@@ -89,12 +106,13 @@ def test_slab_decomposition_gloo_bitexact(tmp_path, world, nz):
     assert np.array_equal(got, ref)
 
 
-def test_slab_plan_partition():
+@pytest.mark.parametrize("ghost", [1, 2])
+def test_slab_plan_partition(ghost):
     for nz in (7, 64, 1024):
         for R in (1, 2, 3, 4, 8):
-            if nz < R:
+            if nz < R * ghost:
                 continue
-            plans = [SlabPlan(nz, R, r) for r in range(R)]
+            plans = [SlabPlan(nz, R, r, ghost) for r in range(R)]
             assert plans[0].z_lo == 0 and plans[-1].z_hi == nz
             for a, b in zip(plans, plans[1:]):
                 assert a.z_hi == b.z_lo
@@ -103,23 +121,32 @@ def test_slab_plan_partition():
             # update ranges cover exactly the interior planes 1..nz-2
             upd = []
             for p in plans:
-                upd += [p.z_lo - 1 + k for k in range(p.z_update_begin, p.z_update_end)]
+                upd += [p.z_lo - ghost + k for k in range(p.z_update_begin, p.z_update_end)]
             assert upd == list(range(1, nz - 1))
-            # each send lands in the peer's matching ghost
+            # each send lands in the peer's matching ghost planes
             for p in plans:
-                for send, peer, recv in p.exchanges():
+                for first, count, peer, recv in p.exchanges():
                     q = plans[peer]
-                    assert p.z_lo - 1 + send == q.z_lo - 1 + recv
-                    assert (recv, p.rank) in q.receives()
+                    assert count == ghost
+                    assert p.z_lo - ghost + first == q.z_lo - ghost + recv
+                    assert (recv, count, p.rank) in q.receives()
+                    # the sent planes are owned by p
+                    assert p.owned().start <= first and first + count <= p.owned().stop
 
 
 def test_slab_plan_1024_on_8():
     p = SlabPlan(1024, 8, 3)
     assert (p.z_lo, p.z_hi, p.nz_local) == (384, 512, 128)
-    assert p.exchanges() == [(1, 2, 129), (128, 4, 0)]
-    assert p.receives() == [(0, 2), (129, 4)]
+    assert p.exchanges() == [(1, 1, 2, 129), (128, 1, 4, 0)]
+    assert p.receives() == [(0, 1, 2), (129, 1, 4)]
     assert (p.z_update_begin, p.z_update_end) == (1, 129)
     p0 = SlabPlan(1024, 8, 0)
     assert (p0.z_update_begin, p0.z_update_end, p0.lo_peer) == (2, 129, -1)
     p7 = SlabPlan(1024, 8, 7)
     assert (p7.z_update_begin, p7.z_update_end, p7.hi_peer) == (1, 128, -1)
+    q = SlabPlan(1024, 8, 3, ghost=2)
+    assert q.nz_total == 132 and q.owned() == slice(2, 130)
+    assert q.exchanges() == [(2, 2, 2, 130), (128, 2, 4, 0)]
+    assert q.receives() == [(0, 2, 2), (130, 2, 4)]
+    q0 = SlabPlan(1024, 8, 0, ghost=2)
+    assert (q0.z_update_begin, q0.z_update_end) == (3, 130)
