@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--tb", type=int, default=0, help="3-D sweeps fused per pass: 0 auto (2), 1 off, 2 on")
     ap.add_argument("--tb-rows", type=int, default=0)
     ap.add_argument("--tb-zchunk", type=int, default=0)
+    ap.add_argument("--tb-prefetch", type=int, default=0, help="planes of prefetch in the blocked kernel")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-rhs-ws", action="store_true", help="form the RHS in-register every sweep")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -137,6 +138,7 @@ def main():
     iters = ARGS.iters or iters_default
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
     call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
+    call("cfd_set_jacobi3d_prefetch", ARGS.tb_prefetch)
     dt = np.float32(5e-5)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
@@ -288,9 +290,9 @@ def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):
                             "GBps": round(cells * bpc / per / 1e6, 1)})
                 print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
-    for rows in (2, 6, 14):
-        for zchunk in (0, 32, 64, 128, 256):
+    for rows, zchunk, pf in [(r, z, p) for p in (1, 2) for r in (5, 13) for z in (32, 64, 128)]:
             call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
+            call("cfd_set_jacobi3d_prefetch", pf)
             phi.zero_()
             K.solve_pressure_jacobi3d(phi, div, h, dt, None, 4, phi_tmp=tmp, rhs_ws=rhs)
             torch.cuda.synchronize()
@@ -301,11 +303,12 @@ def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):
             call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(n), 1)
             call("cfd_timing_enable", 0)
             per = ms.value / n.value
-            res.append({"tb_rows": rows, "zchunk": zchunk, "ms_per_sweep": round(per, 4),
+            res.append({"tb_rows": rows, "zchunk": zchunk, "prefetch": pf, "ms_per_sweep": round(per, 4),
                         "GBps_pass": round(cells * 12 / (2 * per) / 1e6, 1),
                         "Gcell_per_s": round(cells / per / 1e6, 1)})
             print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
     call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
+    call("cfd_set_jacobi3d_prefetch", ARGS.tb_prefetch)
     return res
 
 

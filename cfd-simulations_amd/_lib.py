@@ -64,6 +64,7 @@ PROTOTYPES = {
                                        c_float, P, P]),
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_blocking": (c_int, [c_int, c_int, c_int]),
+    "cfd_set_jacobi3d_prefetch": (c_int, [c_int]),
     "cfd_timing_enable": (c_int, [c_int]),
     "cfd_timing_read": (c_int, [ctypes.POINTER(c_double), ctypes.POINTER(ctypes.c_longlong), c_int]),
 }

@@ -13,6 +13,7 @@ int launch_rhs_f32(const float *div, float *rhs, size_t n, float h2, float dt, h
 int jacobi3d_tb_rows();      // configured rows per temporally blocked tile
 int jacobi3d_tb_zchunk();
 bool jacobi3d_tb_enabled();
+int jacobi3d_tb_prefetch();  // planes of prefetch in the blocked kernel (1 or 2)
 // jacobi3d_tb.hip
 int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, float h2, float dt, int W, int zchunk,

@@ -43,18 +43,28 @@ __device__ inline float jac7(float E, float W, float N, float S, float U, float 
     return (1.0f / 6.0f) * (s - rhs);
 }
 
-template <int W, bool PRE>
-__global__ __launch_bounds__((W + 2) * 64) void jacobi3d_tb2(
+// PD: prefetch distance in planes (1 or 2): how many steps ahead the next
+// planes' loads are issued.
+//
+// Roles: waves 0..G-1 ("row waves") each own one phi^(k+1) row of the tile
+// (rows y0-1 .. y0+W), 64 lanes x float4 = 256 columns.  Wave G (the "halo
+// wave") owns everything outside that 256 x (W+2) block: the two extra phi^k
+// rows (y0-2, y0+W+1), the 4-float x-halo chunks of all W+4 rows, and the
+// phi^(k+1) values of the two halo columns (x0-1, x0+256), one lane per
+// (row, side).  The row waves therefore run identical, branch-free code.
+template <int W, bool PRE, int PD>
+__global__ __launch_bounds__((W + 3) * 64) void jacobi3d_tb2(
     const float *__restrict__ in, float *__restrict__ out, const float *__restrict__ div, int nz,
     int ny, int nx, int nseg, int ntile_y, int zb, int ze, int zchunk, int fixed_lo, int fixed_hi,
     float h2, float dt) {
-    constexpr int G = W + 2;    // waves: phi^(k+1) rows y0-1 .. y0+W
-    constexpr int RS = 264;     // LDS row: 4 halo | 256 | 4 halo floats
+    constexpr int G = W + 2;  // row waves
+    constexpr int RS = 264;   // LDS row: 4 halo | 256 | 4 halo floats
+    static_assert(2 * (W + 4) <= 64, "halo wave: one lane per (row, side)");
     __shared__ __attribute__((aligned(16))) float A[2][W + 4][RS];  // phi^k rows y0-2 .. y0+W+1
     __shared__ __attribute__((aligned(16))) float B[2][G][RS];      // phi^(k+1) rows y0-1 .. y0+W
 
     const int lane = threadIdx.x & 63;
-    const int g = threadIdx.x >> 6;
+    const int wv = threadIdx.x >> 6;
     const int t = xcd_swizzle(blockIdx.x, gridDim.x);
     const int seg = t % nseg;
     const int ty = (t / nseg) % ntile_y;
@@ -63,152 +73,181 @@ __global__ __launch_bounds__((W + 2) * 64) void jacobi3d_tb2(
     if (z0 >= ze) return;  // workgroup-uniform
     const int z1 = min(z0 + zchunk, ze);
     const int y0 = 1 + ty * W;
-    const int y = y0 - 1 + g;
     const int xs = seg * 256;
     const int x = xs + 4 * lane;
     const bool xin = x < nx;
-    const bool rowin = y >= 0 && y <= ny - 1;
-    const bool ld_ok = xin && rowin;
-    const bool int_row = y >= 1 && y <= ny - 2;
-    const bool out_row = g >= 1 && g <= W && y <= ny - 2;
-    // extra phi^k rows: wave 0 -> y0-2, last wave -> y0+W+1
-    const bool has_extra = g == 0 || g == G - 1;
-    const int ye = g == 0 ? y0 - 2 : y0 + W + 1;
-    const bool extra_ok = has_extra && xin && ye >= 0 && ye <= ny - 1;
-    const int arow_extra = g == 0 ? 0 : W + 3;
-    // x-halo chunks: lane 0 -> [xs-4, xs), lane 63 -> [xs+256, xs+260)
-    const bool halo_lane = (lane == 0 && xs > 0) || (lane == 63 && xs + 256 < nx);
-    const int hx = lane == 0 ? xs - 4 : xs + 256;
-    const int hcol = lane == 0 ? 0 : 260;
-    const bool hal_ok = halo_lane && rowin;
-    const bool ehal_ok = halo_lane && has_extra && ye >= 0 && ye <= ny - 1;
-
     const size_t plane = (size_t)ny * nx;
-    const size_t rofs = (size_t)(rowin ? y : 0) * nx + (xin ? x : 0);
-    const size_t eofs = (size_t)(extra_ok ? ye : 0) * nx + (xin ? x : 0);
-    const size_t hofs = (size_t)(rowin ? y : 0) * nx + (halo_lane ? hx : 0);
-    const size_t ehofs = (size_t)(ehal_ok ? ye : 0) * nx + (halo_lane ? hx : 0);
-    const int hd = lane == 0 ? 3 : 0;  // the halo cell next to the tile
-
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 cm = z4, cc = z4, cp = z4, cpp = z4;  // phi^k centre, planes z-1 .. z+2
-    float4 hm = z4, hc = z4, hp = z4, hpp = z4;  // phi^k x-halo chunk
-    float4 ec = z4, ecn = z4, ehc = z4, ehcn = z4;
-    float4 dcur = z4, dnext = z4, dprev = z4;
-    float dh = 0.f, dhn = 0.f;
-    float4 l1m2 = z4, l1m1 = z4, l1c = z4;  // phi^(k+1) centre, planes z-2 .. z
-
     const int zs = z0 - 1;  // first front plane
     auto P = [&](int p) { return in + (size_t)p * plane; };
-    if (ld_ok) {
-        if (zs - 1 >= 0) cm = ldg4(P(zs - 1) + rofs);
-        cc = ldg4(P(zs) + rofs);
-        if (zs + 1 <= nz - 1) cp = ldg4(P(zs + 1) + rofs);
-        dcur = ldg4(div + (size_t)zs * plane + rofs);
-    }
-    if (hal_ok) {
-        if (zs - 1 >= 0) hm = ldg4(P(zs - 1) + hofs);
-        hc = ldg4(P(zs) + hofs);
-        if (zs + 1 <= nz - 1) hp = ldg4(P(zs + 1) + hofs);
-        dh = div[(size_t)zs * plane + hofs + hd];
-    }
-    if (extra_ok) ec = ldg4(P(zs) + eofs);
-    if (ehal_ok) ehc = ldg4(P(zs) + ehofs);
+    auto R = [&](int p) { return div + (size_t)p * plane; };
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
-    for (int z = zs; z <= z1; ++z) {
-        const bool more = z < z1;
-        if (more) {  // prefetch for the next step
-            if (z + 2 <= nz - 1) {
-                if (ld_ok) cpp = ldg4(P(z + 2) + rofs);
-                if (hal_ok) hpp = ldg4(P(z + 2) + hofs);
+    if (wv < G) {
+        // ------------------------------------------------------------ row wave
+        const int g = wv;
+        const int y = y0 - 1 + g;
+        const bool rowin = y >= 0 && y <= ny - 1;
+        const bool ld_ok = xin && rowin;
+        const bool int_row = y >= 1 && y <= ny - 2;
+        const bool out_row = g >= 1 && g <= W && y <= ny - 2;
+        const size_t rofs = (size_t)(rowin ? y : 0) * nx + (xin ? x : 0);
+        float4 cm = z4, cc = z4, cp = z4, cpp = z4, c3 = z4;  // phi^k centre, planes z-1 .. z+3
+        float4 dprev = z4, dcur = z4, dnext = z4, d2 = z4;    // rhs/div, planes z-1 .. z+2
+        float4 l1m2 = z4, l1m1 = z4, l1c = z4;                // phi^(k+1), planes z-2 .. z
+        if (ld_ok) {
+            if (zs - 1 >= 0) cm = ldg4(P(zs - 1) + rofs);
+            cc = ldg4(P(zs) + rofs);
+            if (zs + 1 <= nz - 1) cp = ldg4(P(zs + 1) + rofs);
+            dcur = ldg4(R(zs) + rofs);
+            if (PD == 2 && zs + 1 <= z1) {
+                if (zs + 2 <= nz - 1) cpp = ldg4(P(zs + 2) + rofs);
+                dnext = ldg4(R(zs + 1) + rofs);
             }
-            if (extra_ok) ecn = ldg4(P(z + 1) + eofs);
-            if (ehal_ok) ehcn = ldg4(P(z + 1) + ehofs);
-            if (ld_ok) dnext = ldg4(div + (size_t)(z + 1) * plane + rofs);
-            if (hal_ok) dhn = div[(size_t)(z + 1) * plane + hofs + hd];
         }
-        const int b = z & 1;
-        // 1. publish phi^k of plane z
-        if (ld_ok) sts4(&A[b][g + 1][4 + 4 * lane], cc);
-        if (hal_ok) sts4(&A[b][g + 1][hcol], hc);
-        if (extra_ok) sts4(&A[b][arow_extra][4 + 4 * lane], ec);
-        if (ehal_ok) sts4(&A[b][arow_extra][hcol], ehc);
-        __syncthreads();
-
-        // 2. phi^(k+1) of plane z
-        const bool fixed = (z == zb - 1 && fixed_lo) || (z == ze && fixed_hi);
-        float wl = __shfl_up(cc.w, 1, 64);
-        float er = __shfl_down(cc.x, 1, 64);
-        if (lane == 0) wl = hc.w;
-        if (lane == 63) er = hc.x;
-        float4 l1 = cc;
-        if (ld_ok && int_row && !fixed) {
-            const float4 N = lds4(&A[b][g + 2][4 + 4 * lane]);
-            const float4 S = lds4(&A[b][g][4 + 4 * lane]);
-            const float c[4] = {cc.x, cc.y, cc.z, cc.w};
-            const float n[4] = {N.x, N.y, N.z, N.w};
-            const float sv[4] = {S.x, S.y, S.z, S.w};
-            const float u[4] = {cp.x, cp.y, cp.z, cp.w};
-            const float dd[4] = {cm.x, cm.y, cm.z, cm.w};
-            const float dv[4] = {dcur.x, dcur.y, dcur.z, dcur.w};
-            float o[4];
+        for (int z = zs; z <= z1; ++z) {
+            const int zp = z + PD - 1;  // this step fetches what step zp+1 needs
+            if (ld_ok && zp + 1 <= z1) {
+                const float4 nc = (zp + 2 <= nz - 1) ? ldg4(P(zp + 2) + rofs) : z4;
+                const float4 nd = ldg4(R(zp + 1) + rofs);
+                if constexpr (PD == 2) { c3 = nc; d2 = nd; } else { cpp = nc; dnext = nd; }
+            }
+            const int b = z & 1;
+            if (ld_ok) sts4(&A[b][g + 1][4 + 4 * lane], cc);
+            __syncthreads();
+            // phi^(k+1) of plane z, row y
+            const bool fixed = (z == zb - 1 && fixed_lo) || (z == ze && fixed_hi);
+            float wl = __shfl_up(cc.w, 1, 64);
+            float er = __shfl_down(cc.x, 1, 64);
+            const float wl_l = A[b][g + 1][3], er_l = A[b][g + 1][260];
+            if (lane == 0) wl = wl_l;
+            if (lane == 63) er = er_l;
+            float4 l1 = cc;
+            if (ld_ok && int_row && !fixed) {
+                const float4 N = lds4(&A[b][g + 2][4 + 4 * lane]);
+                const float4 S = lds4(&A[b][g][4 + 4 * lane]);
+                const float c[4] = {cc.x, cc.y, cc.z, cc.w};
+                const float n[4] = {N.x, N.y, N.z, N.w};
+                const float sv[4] = {S.x, S.y, S.z, S.w};
+                const float u[4] = {cp.x, cp.y, cp.z, cp.w};
+                const float dd[4] = {cm.x, cm.y, cm.z, cm.w};
+                const float dv[4] = {dcur.x, dcur.y, dcur.z, dcur.w};
+                float o[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int xk = x + k;
-                const float E = k < 3 ? c[k + 1] : er;
-                const float Wv = k > 0 ? c[k - 1] : wl;
-                o[k] = (xk == 0 || xk == nx - 1) ? c[k] : jac7<PRE>(E, Wv, n[k], sv[k], u[k], dd[k], dv[k], h2, dt);
+                for (int k = 0; k < 4; ++k) {
+                    const int xk = x + k;
+                    const float E = k < 3 ? c[k + 1] : er;
+                    const float Wv = k > 0 ? c[k - 1] : wl;
+                    o[k] = (xk == 0 || xk == nx - 1) ? c[k]
+                                                     : jac7<PRE>(E, Wv, n[k], sv[k], u[k], dd[k], dv[k], h2, dt);
+                }
+                l1 = make_float4(o[0], o[1], o[2], o[3]);
             }
-            l1 = make_float4(o[0], o[1], o[2], o[3]);
-        }
-        l1c = l1;
-        if (ld_ok) sts4(&B[b][g][4 + 4 * lane], l1);
-        if (hal_ok) {  // the halo column next to the tile
-            float v;
-            if (lane == 0) {
-                v = hc.w;  // x = xs-1
-                if (int_row && !fixed)
-                    v = jac7<PRE>(cc.x, hc.z, A[b][g + 2][3], A[b][g][3], hp.w, hm.w, dh, h2, dt);
-                B[b][g][3] = v;
-            } else {
-                v = hc.x;  // x = xs+256
-                if (int_row && !fixed && xs + 256 != nx - 1)
-                    v = jac7<PRE>(hc.y, cc.w, A[b][g + 2][260], A[b][g][260], hp.x, hm.x, dh, h2, dt);
-                B[b][g][260] = v;
-            }
-        }
-
-        // 3. phi^(k+2) of plane z-1 (B[b^1] was written last step, behind this step's barrier)
-        float wl1 = __shfl_up(l1m1.w, 1, 64);
-        float er1 = __shfl_down(l1m1.x, 1, 64);
-        if (z >= z0 + 1 && out_row && xin) {
-            const int pb = b ^ 1;
-            if (lane == 0) wl1 = B[pb][g][3];
-            if (lane == 63) er1 = B[pb][g][260];
-            const float4 N = lds4(&B[pb][g + 1][4 + 4 * lane]);
-            const float4 S = lds4(&B[pb][g - 1][4 + 4 * lane]);
-            const float c[4] = {l1m1.x, l1m1.y, l1m1.z, l1m1.w};
-            const float n[4] = {N.x, N.y, N.z, N.w};
-            const float sv[4] = {S.x, S.y, S.z, S.w};
-            const float u[4] = {l1c.x, l1c.y, l1c.z, l1c.w};
-            const float dd[4] = {l1m2.x, l1m2.y, l1m2.z, l1m2.w};
-            const float dv[4] = {dprev.x, dprev.y, dprev.z, dprev.w};
-            float o[4];
+            l1c = l1;
+            if (ld_ok) sts4(&B[b][g][4 + 4 * lane], l1);
+            // phi^(k+2) of plane z-1 (B[b^1]: last step's, behind this step's barrier)
+            float wl1 = __shfl_up(l1m1.w, 1, 64);
+            float er1 = __shfl_down(l1m1.x, 1, 64);
+            if (z >= z0 + 1 && out_row && xin) {
+                const int pb = b ^ 1;
+                if (lane == 0) wl1 = B[pb][g][3];
+                if (lane == 63) er1 = B[pb][g][260];
+                const float4 N = lds4(&B[pb][g + 1][4 + 4 * lane]);
+                const float4 S = lds4(&B[pb][g - 1][4 + 4 * lane]);
+                const float c[4] = {l1m1.x, l1m1.y, l1m1.z, l1m1.w};
+                const float n[4] = {N.x, N.y, N.z, N.w};
+                const float sv[4] = {S.x, S.y, S.z, S.w};
+                const float u[4] = {l1c.x, l1c.y, l1c.z, l1c.w};
+                const float dd[4] = {l1m2.x, l1m2.y, l1m2.z, l1m2.w};
+                const float dv[4] = {dprev.x, dprev.y, dprev.z, dprev.w};
+                float o[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int xk = x + k;
-                const float E = k < 3 ? c[k + 1] : er1;
-                const float Wv = k > 0 ? c[k - 1] : wl1;
-                o[k] = (xk == 0 || xk == nx - 1) ? c[k] : jac7<PRE>(E, Wv, n[k], sv[k], u[k], dd[k], dv[k], h2, dt);
+                for (int k = 0; k < 4; ++k) {
+                    const int xk = x + k;
+                    const float E = k < 3 ? c[k + 1] : er1;
+                    const float Wv = k > 0 ? c[k - 1] : wl1;
+                    o[k] = (xk == 0 || xk == nx - 1) ? c[k]
+                                                     : jac7<PRE>(E, Wv, n[k], sv[k], u[k], dd[k], dv[k], h2, dt);
+                }
+                stg4(out + (size_t)(z - 1) * plane + rofs, make_float4(o[0], o[1], o[2], o[3]));
             }
-            stg4(out + (size_t)(z - 1) * plane + rofs, make_float4(o[0], o[1], o[2], o[3]));
+            cm = cc; cc = cp; cp = cpp;
+            dprev = dcur; dcur = dnext;
+            if constexpr (PD == 2) { cpp = c3; dnext = d2; }
+            l1m2 = l1m1; l1m1 = l1c;
         }
-        // rotate the queues
-        cm = cc; cc = cp; cp = cpp;
-        hm = hc; hc = hp; hp = hpp;
-        ec = ecn; ehc = ehcn;
-        dprev = dcur; dcur = dnext; dh = dhn;
-        l1m2 = l1m1; l1m1 = l1c;
+    } else {
+        // ------------------------------------------------------------ halo wave
+        // extra phi^k rows (all lanes): tile row 0 = y0-2, tile row W+3 = y0+W+1
+        const int ylo = y0 - 2, yhi = y0 + W + 1;
+        const bool elo = xin && ylo >= 0 && ylo <= ny - 1;
+        const bool ehi = xin && yhi >= 0 && yhi <= ny - 1;
+        const size_t olo = (size_t)(elo ? ylo : 0) * nx + (xin ? x : 0);
+        const size_t ohi = (size_t)(ehi ? yhi : 0) * nx + (xin ? x : 0);
+        // halo chunks: lane -> tile row r (y0-2+r), side (0: x0-4..x0-1, 1: x0+256..x0+259)
+        const int r = lane >> 1, side = lane & 1;
+        const int yr = y0 - 2 + r;
+        const bool hon = lane < 2 * (W + 4) && yr >= 0 && yr <= ny - 1 &&
+                         (side ? xs + 256 < nx : xs > 0);
+        const int hx = side ? xs + 256 : xs - 4;
+        const size_t hofs = (size_t)(hon ? yr : 0) * nx + (hon ? hx : 0);
+        const size_t rhofs = hofs + (side ? 0 : 3);  // the cell next to the tile
+        const bool l1row = r >= 1 && r <= W + 2;     // phi^(k+1) rows y0-1 .. y0+W
+        const bool hint = hon && l1row && yr >= 1 && yr <= ny - 2;
+        const int col = side ? 260 : 0;               // chunk position in an LDS row
+        float4 lo = z4, lon = z4, lo2 = z4, hi = z4, hin = z4, hi2 = z4;
+        float4 hm = z4, hc = z4, hp = z4, hpp = z4, h3 = z4;
+        float rh = 0.f, rhn = 0.f, rh2 = 0.f;
+        if (elo) lo = ldg4(P(zs) + olo);
+        if (ehi) hi = ldg4(P(zs) + ohi);
+        if (hon) {
+            if (zs - 1 >= 0) hm = ldg4(P(zs - 1) + hofs);
+            hc = ldg4(P(zs) + hofs);
+            if (zs + 1 <= nz - 1) hp = ldg4(P(zs + 1) + hofs);
+            if (l1row) rh = R(zs)[rhofs];
+        }
+        if (PD == 2 && zs + 1 <= z1) {
+            if (elo) lon = ldg4(P(zs + 1) + olo);
+            if (ehi) hin = ldg4(P(zs + 1) + ohi);
+            if (hon) {
+                if (zs + 2 <= nz - 1) hpp = ldg4(P(zs + 2) + hofs);
+                if (l1row) rhn = R(zs + 1)[rhofs];
+            }
+        }
+        for (int z = zs; z <= z1; ++z) {
+            const int zp = z + PD - 1;
+            if (zp + 1 <= z1) {
+                const float4 nlo = elo ? ldg4(P(zp + 1) + olo) : z4;
+                const float4 nhi = ehi ? ldg4(P(zp + 1) + ohi) : z4;
+                const float4 nh = (hon && zp + 2 <= nz - 1) ? ldg4(P(zp + 2) + hofs) : z4;
+                const float nr = (hon && l1row) ? R(zp + 1)[rhofs] : 0.f;
+                if constexpr (PD == 2) { lo2 = nlo; hi2 = nhi; h3 = nh; rh2 = nr; }
+                else { lon = nlo; hin = nhi; hpp = nh; rhn = nr; }
+            }
+            const int b = z & 1;
+            if (elo) sts4(&A[b][0][4 + 4 * lane], lo);
+            if (ehi) sts4(&A[b][W + 3][4 + 4 * lane], hi);
+            if (hon) sts4(&A[b][r][col], hc);
+            __syncthreads();
+            // phi^(k+1) of the halo columns (x0-1 / x0+256) for rows y0-1 .. y0+W
+            if (hon && l1row) {
+                const bool fixed = (z == zb - 1 && fixed_lo) || (z == ze && fixed_hi);
+                const float C = side ? hc.x : hc.w;
+                float v = C;
+                const int px = side ? xs + 256 : xs - 1;
+                if (hint && !fixed && px != 0 && px != nx - 1) {
+                    const float E = side ? hc.y : A[b][r][4];
+                    const float Wn = side ? A[b][r][259] : hc.z;
+                    const int cc_ = side ? 260 : 3;
+                    v = jac7<PRE>(E, Wn, A[b][r + 1][cc_], A[b][r - 1][cc_], side ? hp.x : hp.w,
+                                  side ? hm.x : hm.w, rh, h2, dt);
+                }
+                B[b][r - 1][side ? 260 : 3] = v;
+            }
+            lo = lon; hi = hin;
+            hm = hc; hc = hp; hp = hpp;
+            rh = rhn;
+            if constexpr (PD == 2) { lon = lo2; hin = hi2; hpp = h3; rhn = rh2; }
+        }
     }
 }
 
@@ -219,39 +258,43 @@ __global__ __launch_bounds__((W + 2) * 64) void jacobi3d_tb2(
 int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, float h2, float dt, int W, int zchunk,
                       bool pre, hipStream_t s) {
+    const int pd = jacobi3d_tb_prefetch();
     if (ze <= zb || ny < 3) return CFD_OK;
     const int nseg = ceil_div(nx, 256);
     const int ntile_y = ceil_div(ny - 2, W);
     const int L = ze - zb;
     if (zchunk <= 0) {
+        // >= ~1024 workgroups (4 per CU) when the grid allows; 16..128 planes
+        // per march (r01 sweep at 1024^3: 64-128 best on one GPU)
         const long tiles = (long)nseg * ntile_y;
         int nzc = (int)((1024 + tiles - 1) / tiles);
         if (nzc < 1) nzc = 1;
         zchunk = ceil_div(L, nzc);
+        if (zchunk > 128) zchunk = 128;
         if (zchunk < 16) zchunk = 16;
     }
     if (zchunk > L) zchunk = L;
     const int blocks = nseg * ntile_y * ceil_div(L, zchunk);
+#define CFD_TB2_L(WV, PR, PDV)                                                                \
+    hipLaunchKernelGGL((jacobi3d_tb2<WV, PR, PDV>), dim3(blocks), dim3((WV + 3) * 64), 0, s, in, out, \
+                       div, nz, ny, nx, nseg, ntile_y, zb, ze, zchunk, fixed_lo, fixed_hi, h2, dt)
 #define CFD_TB2(WV)                                                                             \
     case WV:                                                                                    \
-        if (pre)                                                                                \
-            hipLaunchKernelGGL((jacobi3d_tb2<WV, true>), dim3(blocks), dim3((WV + 2) * 64), 0, s, in, \
-                               out, div, nz, ny, nx, nseg, ntile_y, zb, ze, zchunk, fixed_lo,      \
-                               fixed_hi, h2, dt);                                               \
-        else                                                                                    \
-            hipLaunchKernelGGL((jacobi3d_tb2<WV, false>), dim3(blocks), dim3((WV + 2) * 64), 0, s, in, \
-                               out, div, nz, ny, nx, nseg, ntile_y, zb, ze, zchunk, fixed_lo,      \
-                               fixed_hi, h2, dt);                                               \
+        if (pd == 2) {                                                                          \
+            if (pre) CFD_TB2_L(WV, true, 2); else CFD_TB2_L(WV, false, 2);                      \
+        } else {                                                                                \
+            if (pre) CFD_TB2_L(WV, true, 1); else CFD_TB2_L(WV, false, 1);                      \
+        }                                                                                       \
         break;
     switch (W) {
-        CFD_TB2(2)
-        CFD_TB2(6)
-        CFD_TB2(14)
+        CFD_TB2(5)
+        CFD_TB2(13)
         default:
-            set_error("jacobi3d_tb2: unsupported rows per tile %d (2, 6, 14)", W);
+            set_error("jacobi3d_tb2: unsupported rows per tile %d (5, 13)", W);
             return CFD_E_INVALID;
     }
 #undef CFD_TB2
+#undef CFD_TB2_L
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }

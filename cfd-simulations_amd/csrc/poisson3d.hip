@@ -67,13 +67,16 @@ struct J3Config {
     int tb_steps = 0; // sweeps fused per pass: 0 auto (2), 1 off, 2 on
     int tb_rows = 0;  // output rows per temporally blocked tile (0 = auto)
     int tb_zchunk = 0;
+    int tb_prefetch = 0;  // 0 auto (2), 1, 2
 };
 static J3Config g_j3;
 
-// defaults from the r01 tile sweep (1024^3): 14 output rows per tile, 64 planes
-int jacobi3d_tb_rows() { return g_j3.tb_rows ? g_j3.tb_rows : 14; }
-int jacobi3d_tb_zchunk() { return g_j3.tb_zchunk ? g_j3.tb_zchunk : 64; }
+// defaults from the r01 tile sweep (1024^3): 13 output rows per tile, prefetch
+// 1 plane ahead; planes per tile chosen by jacobi3d_tb2_pass (0 = auto)
+int jacobi3d_tb_rows() { return g_j3.tb_rows ? g_j3.tb_rows : 13; }
+int jacobi3d_tb_zchunk() { return g_j3.tb_zchunk; }
 bool jacobi3d_tb_enabled() { return g_j3.tb_steps != 1; }
+int jacobi3d_tb_prefetch() { return g_j3.tb_prefetch == 2 ? 2 : 1; }
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
@@ -410,9 +413,15 @@ using namespace cfd;
 
 extern "C" {
 
+int cfd_set_jacobi3d_prefetch(int planes) {
+    CFD_REQUIRE(planes >= 0 && planes <= 2, "prefetch planes must be 0 (auto), 1 or 2");
+    g_j3.tb_prefetch = planes;
+    return CFD_OK;
+}
+
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
     CFD_REQUIRE(steps >= 0 && steps <= 2, "blocking steps must be 0 (auto), 1 or 2");
-    CFD_REQUIRE(rows == 0 || rows == 2 || rows == 6 || rows == 14, "blocking rows must be 0, 2, 6, 14");
+    CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13, "blocking rows must be 0, 5, 13");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
     g_j3.tb_steps = steps;
     g_j3.tb_rows = rows;

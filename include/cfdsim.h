@@ -202,9 +202,11 @@ int cfd_jacobi3d_sweep_f32(const float *in, float *out, const float *div, const 
 int cfd_set_jacobi3d_config(int variant, int waves, int zchunk);
 /* Temporal blocking of the 3-D Jacobi solve (cfd_jacobi3d_f32 without mask
  * or residual): steps = sweeps fused per HBM pass (0 = auto = 2, 1 = off);
- * rows = output rows per tile (0 auto, 2, 6, 14); zchunk = planes per tile.
+ * rows = output rows per tile (0 auto, 5, 13); zchunk = planes per tile.
  * Fused or not, results are bit-identical. */
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk);
+/* Prefetch distance of the blocked kernel in planes (0 = auto = 1, 1, 2). */
+int cfd_set_jacobi3d_prefetch(int planes);
 
 /* Sweep timing (bench harness): while enabled, every solve records a HIP
  * event pair on its stream around its sweep launches.  cfd_timing_read

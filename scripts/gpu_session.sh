@@ -31,6 +31,11 @@ for s in "$@"; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
     pmc_write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    sq_tb) step sq_tb 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES -d gpurun_out/sq_tb -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    sq_march) step sq_march 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES -d gpurun_out/sq_march -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --tb 1 --no-cpu-baseline ;;
+    pmc_fetch_tb) step pmc_fetch_tb 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_tb -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    pmc_write_tb) step pmc_write_tb 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_tb -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    prof_tb) step prof_tb 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_tb -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -39,6 +39,7 @@ def host(t):
 def _reset_j3():
     call("cfd_set_jacobi3d_config", 0, 0, 0)
     call("cfd_set_jacobi3d_blocking", 0, 0, 0)
+    call("cfd_set_jacobi3d_prefetch", 0)
     yield
     call("cfd_set_jacobi3d_config", 0, 0, 0)
     call("cfd_set_jacobi3d_blocking", 0, 0, 0)
@@ -145,13 +146,15 @@ def test_jacobi3d_bitexact(shape, masked, variant, waves, zchunk):
     assert np.array_equal(host(phi), ref)
 
 
-@pytest.mark.parametrize("rows,zchunk", [(2, 0), (6, 0), (14, 0), (6, 3), (2, 1), (14, 5)])
+@pytest.mark.parametrize("prefetch", [1, 2])
+@pytest.mark.parametrize("rows,zchunk", [(5, 0), (13, 0), (5, 3), (13, 1), (5, 1), (13, 5)])
 @pytest.mark.parametrize("shape,iters", [((10, 12, 16), 6), ((9, 11, 20), 7), ((34, 40, 260), 4),
                                          ((6, 7, 520), 5), ((20, 19, 8), 2), ((5, 33, 768), 9),
                                          ((3, 3, 4), 4)])
-def test_jacobi3d_temporal_blocking_bitexact(shape, iters, rows, zchunk):
+def test_jacobi3d_temporal_blocking_bitexact(shape, iters, rows, zchunk, prefetch):
     """Two sweeps fused per pass (jacobi3d_tb2) == two single sweeps, bitwise."""
     call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
+    call("cfd_set_jacobi3d_prefetch", prefetch)
     rng = np.random.default_rng(sum(shape) + iters)
     div = rng.standard_normal(shape).astype(np.float32)
     phi0 = rng.standard_normal(shape).astype(np.float32)
@@ -195,7 +198,7 @@ def test_jacobi3d_variants_agree_at_1024():
     div = torch.randn((n, n, n), generator=g, device=DEV, dtype=torch.float32)
     outs = []
     for cfgv, tb in [((1, 4, 0), 1), ((2, 4, 0), 1), ((1, 8, 64), 1), ((2, 16, 0), 1), ((0, 0, 0), 2),
-                     ((0, 0, 0), (2, 14, 0)), ((0, 0, 0), (2, 2, 40))]:
+                     ((0, 0, 0), (2, 13, 0)), ((0, 0, 0), (2, 5, 40))]:
         call("cfd_set_jacobi3d_config", *cfgv)
         call("cfd_set_jacobi3d_blocking", *(tb if isinstance(tb, tuple) else (tb, 0, 0)))
         phi = torch.zeros_like(div)
