@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-rhs-ws", action="store_true", help="form the RHS in-register every sweep")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true", help="skip the N>1 parity check")
+    ap.add_argument("--force-slab", action="store_true",
+                    help="use the RCCL slab path even on one rank (launch under torch.distributed.run)")
     ap.add_argument("--cpu-sample-planes", type=int, default=256)
     ap.add_argument("--sweep-tiles", action="store_true", help="print a tile-size sweep (N=1, 3-D)")
     return ap.parse_args()
@@ -131,7 +134,8 @@ def main():
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_slab = world > 1 or ARGS.force_slab
+    if use_slab:
         dist.init_process_group("nccl", device_id=dev)
 
     shape, dt_name, iters_default, bpc = WORKLOADS[ARGS.workload]
@@ -146,7 +150,7 @@ def main():
         nz, ny, nx = shape
         h = 1.0 / (nx - 1)
         plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else 2)
-        if world == 1:
+        if not use_slab:
             div = torch.randn(shape, generator=g, device=dev, dtype=torch.float32)
             phi = torch.zeros_like(div)
             tmp = torch.zeros_like(div)
@@ -185,8 +189,12 @@ def main():
         dtype = "f64"
 
     def barrier():
-        if world > 1:
+        if use_slab:
             dist.barrier()
+
+    verified = None
+    if use_slab and len(shape) == 3 and not ARGS.no_verify:
+        verified = verify_slabs(S, K, dist, comm, world, rank, dev)
 
     if ARGS.sweep_tiles and world == 1 and len(shape) == 3:
         tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells_rank, rhs)
@@ -210,7 +218,7 @@ def main():
     call("cfd_timing_enable", 0)
     sweep_ms = ms.value / max(nsw.value, 1)
 
-    if world > 1:
+    if use_slab:
         t = torch.tensor([elapsed, sweep_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, sweep_ms_max = float(t[0]), float(t[1])
@@ -243,7 +251,7 @@ def main():
         "config": {"workload": workload, "grid": list(shape), "iters_per_step": iters,
                    "decomposition": "z-slab" if len(shape) == 3 else "none",
                    "halo": ("rccl send/recv, overlapped" if not ARGS.no_overlap else "rccl send/recv")
-                   if world > 1 else "none",
+                   if use_slab else "none",
                    "kernel_variant": ARGS.variant, "waves": ARGS.waves, "zchunk": ARGS.zchunk,
                    "temporal_blocking": ARGS.tb, "tb_rows": ARGS.tb_rows,
                    "rhs_workspace": not ARGS.no_rhs_ws},
@@ -258,13 +266,56 @@ def main():
                      "max_rank_avg_launch_ms": round(sweep_ms_max * spl, 4)},
         "cpu_baseline": None,
     }
+    if verified is not None:
+        out["config"]["multi_gpu_parity"] = ("bit-exact vs 1-GPU solve (96^3, 7+8 sweeps, both ghost depths)"
+                                             if verified else "MISMATCH")
     if rank == 0 and world == 1 and not ARGS.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(shape, iters)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_slab and len(shape) == 3:
         sj.comm.close()
+    if use_slab:
         dist.destroy_process_group()
+
+
+def verify_slabs(S, K, dist, comm, world, rank, dev):
+    """Multi-GPU parity on a small grid before timing: every rank solves its
+    slab through RCCL, rank 0 solves the whole grid on its own GPU, and the
+    gathered owned planes must match bit-for-bit."""
+    import torch
+    nz, ny, nx = 96, 90, 104
+    g = torch.Generator(device=dev).manual_seed(99)
+    div = torch.randn((nz, ny, nx), generator=g, device=dev, dtype=torch.float32)  # same on every rank
+    ok = True
+    for ghost, iters in ((1, 7), (2, 8)):
+        plan = S.SlabPlan(nz, world, rank, ghost=ghost)
+        sj = S.SlabJacobi3D(plan, ny, nx, 0.03, np.float32(1e-3), comm, device=dev)
+        lo = plan.z_lo - ghost
+        for k in range(plan.nz_total):
+            if 0 <= lo + k < nz:
+                sj.div[k].copy_(div[lo + k])
+        sj.solve(iters, overlap=True)
+        mine = sj.owned().contiguous()
+        sizes = [S.SlabPlan(nz, world, r, ghost=ghost).nz_local for r in range(world)]
+        parts = [torch.empty((n, ny, nx), dtype=torch.float32, device=dev) for n in sizes]
+        dist.all_gather(parts, mine) if len(set(sizes)) == 1 else _gather_uneven(dist, parts, mine, rank)
+        if rank == 0:
+            ref = torch.zeros_like(div)
+            K.solve_pressure_jacobi3d(ref, div, 0.03, np.float32(1e-3), None, iters)
+            ok &= bool(torch.equal(torch.cat(parts), ref))
+    flag = torch.tensor([1 if ok else 0], device=dev)
+    dist.broadcast(flag, src=0)
+    if not bool(flag.item()) and rank == 0:
+        print("WARNING: multi-GPU slab result differs from the single-GPU solve", file=sys.stderr)
+    return bool(flag.item())
+
+
+def _gather_uneven(dist, parts, mine, rank):
+    for r, p in enumerate(parts):
+        if r == rank:
+            p.copy_(mine)
+        dist.broadcast(p, src=r)
 
 
 def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):

@@ -36,6 +36,7 @@ for s in "$@"; do
     pmc_fetch_tb) step pmc_fetch_tb 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_tb -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
     pmc_write_tb) step pmc_write_tb 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_tb -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
     prof_tb) step prof_tb 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_tb -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    slab1) step slab1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --force-slab --steps 3 --warmup 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
