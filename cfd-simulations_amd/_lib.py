@@ -65,6 +65,7 @@ PROTOTYPES = {
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_blocking": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_prefetch": (c_int, [c_int]),
+    "cfd_set_jacobi2d_blocking": (c_int, [c_int]),
     "cfd_timing_enable": (c_int, [c_int]),
     "cfd_timing_read": (c_int, [ctypes.POINTER(c_double), ctypes.POINTER(ctypes.c_longlong), c_int]),
 }

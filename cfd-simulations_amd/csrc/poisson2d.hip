@@ -203,6 +203,146 @@ static int jacobi2d_sweep(const T *in, T *out, const T *div, const uint8_t *mask
     return CFD_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Temporally blocked 2-D Jacobi: TWO sweeps per pass (12 B per two f32
+// cell-updates, 24 B per two f64 updates).  A wave owns 64 lanes x VEC cells
+// but its x-segments OVERLAP by VEC cells on each side: it writes only the
+// inner 64*VEC - 2*VEC cells, so every lane runs the same code and the
+// intermediate level phi^(k+1) it needs one cell beyond its output is
+// computed in-wave (lane 0 / lane 63's chunks), never exchanged.  Rows march
+// with register queues: phi^k rows r-1..r+1 (+ r+2 prefetched) and
+// phi^(k+1) rows r-2..r.  Bit-identical to two single sweeps.
+template <typename T>
+__device__ inline T jac5(T E, T W, T N, T S, T d, T dx2, T dtv, bool pre) {
+    T s = E + W;
+    s = s + N;
+    s = s + S;
+    const T rhs = pre ? d : (dx2 * d) / dtv;
+    return T(0.25) * (s - rhs);
+}
+
+template <typename T, int VEC, bool PRE, bool MASK>
+__global__ __launch_bounds__(256) void jacobi2d_tb2(const T *__restrict__ in, T *__restrict__ out,
+                                                    const T *__restrict__ div,
+                                                    const uint8_t *__restrict__ mask, int ny,
+                                                    int nx, int nseg, int rows_per_chunk, T dx2,
+                                                    T dtv) {
+    static_assert(VEC >= 2, "the overlapped segment needs 2+ cells per lane");
+    constexpr int SOUT = 64 * VEC - 2 * VEC;  // cells written per wave
+    const int lane = threadIdx.x & 63;
+    const int wpb = blockDim.x / 64;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const long wave = (long)bid * wpb + threadIdx.x / 64;
+    const int seg = (int)(wave % nseg);
+    const int chunk = (int)(wave / nseg);
+    const int y0 = 1 + chunk * rows_per_chunk;
+    if (y0 >= ny - 1) return;  // wave-uniform
+    const int y1 = min(y0 + rows_per_chunk, ny - 1);
+    const int xs = seg * SOUT;
+    const int x0 = xs - VEC + lane * VEC;  // this lane's first cell
+    const bool valid = x0 >= 0 && x0 < nx;
+    const bool writer = lane >= 1 && lane <= 62 && valid;
+    T am[VEC], ac[VEC], ap[VEC], app[VEC];    // phi^k rows r-1, r, r+1, r+2
+    T bm[VEC], bc[VEC], bp[VEC];              // phi^(k+1) rows r-2, r-1, r
+    T dm[VEC], dc[VEC], dn[VEC];              // rhs/div rows r-1, r, r+1
+    uint8_t mm[VEC], mc[VEC], mn[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        am[k] = ac[k] = ap[k] = app[k] = bm[k] = bc[k] = bp[k] = dm[k] = dc[k] = dn[k] = T(0);
+        mm[k] = mc[k] = mn[k] = 0;
+    }
+    const int rs = y0 - 1;  // first front row
+    auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
+    if (valid) {
+        if (rs - 1 >= 0) ld<T, VEC>(in + row(rs - 1), am);
+        ld<T, VEC>(in + row(rs), ac);
+        ld<T, VEC>(in + row(rs + 1), ap);  // rs + 1 = y0 <= ny - 2
+        ld<T, VEC>(div + row(rs), dc);
+        ld<T, VEC>(div + row(rs + 1), dn);
+        if (MASK) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) { mc[k] = mask[row(rs) + k]; mn[k] = mask[row(rs + 1) + k]; }
+        }
+    }
+    for (int r = rs; r <= y1; ++r) {
+        // prefetch phi^k row r+2 (needed as the N neighbour next step)
+        if (valid && r + 1 <= y1 && r + 2 <= ny - 1) ld<T, VEC>(in + row(r + 2), app);
+        // phi^(k+1) of row r
+        const bool fixed = r == 0 || r == ny - 1;
+        T wl = __shfl_up(ac[VEC - 1], 1, 64);
+        T er = __shfl_down(ac[0], 1, 64);
+        T l1[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const T E = (k + 1 < VEC) ? ac[k + 1] : er;
+            const T W = (k > 0) ? ac[k - 1] : wl;
+            const int x = x0 + k;
+            T v = (fixed || x == 0 || x >= nx - 1) ? ac[k] : jac5<T>(E, W, ap[k], am[k], dc[k], dx2, dtv, PRE);
+            if (MASK && mc[k]) v = T(0);
+            l1[k] = v;
+        }
+        // phi^(k+2) of row r-1
+        T wl1 = __shfl_up(bc[VEC - 1], 1, 64);
+        T er1 = __shfl_down(bc[0], 1, 64);
+        if (r >= y0 + 1 && writer) {
+            T o[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const T E = (k + 1 < VEC) ? bc[k + 1] : er1;
+                const T W = (k > 0) ? bc[k - 1] : wl1;
+                const int x = x0 + k;
+                T v = (x == 0 || x >= nx - 1) ? bc[k] : jac5<T>(E, W, l1[k], bm[k], dm[k], dx2, dtv, PRE);
+                if (MASK && mm[k]) v = T(0);
+                o[k] = v;
+            }
+            st<T, VEC>(out + row(r - 1), o);
+        }
+        // rotate (rhs/mask for row r+2 loaded here: used two steps on)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            am[k] = ac[k]; ac[k] = ap[k]; ap[k] = app[k];
+            bm[k] = bc[k]; bc[k] = l1[k];
+            dm[k] = dc[k]; dc[k] = dn[k];
+            if (MASK) { mm[k] = mc[k]; mc[k] = mn[k]; }
+        }
+        if (valid && r + 2 <= y1 + 0 && r + 2 <= ny - 1) {
+            ld<T, VEC>(div + row(r + 2), dn);
+            if (MASK) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) mn[k] = mask[row(r + 2) + k];
+            }
+        }
+    }
+}
+
+template <typename T, int VEC>
+static int jacobi2d_tb2_pass(const T *in, T *out, const T *div, const uint8_t *mask, int ny, int nx,
+                             T dx2, T dtv, bool pre, hipStream_t s) {
+    constexpr int SOUT = 64 * VEC - 2 * VEC;
+    const int nseg = ceil_div(nx, SOUT);
+    const int rows = ny - 2;
+    if (rows <= 0) return CFD_OK;
+    int rpc = ceil_div((long)rows * nseg, 8192);
+    if (rpc < 8) rpc = 8;
+    if (rpc > 64) rpc = 64;
+    const int nchunk = ceil_div(rows, rpc);
+    const int wpb = 4;
+    const int blocks = ceil_div((long)nseg * nchunk, wpb);
+#define CFD_J2TB(PR, M)                                                                          \
+    hipLaunchKernelGGL((jacobi2d_tb2<T, VEC, PR, M>), dim3(blocks), dim3(wpb * 64), 0, s, in, out, \
+                       div, mask, ny, nx, nseg, rpc, dx2, dtv)
+    if (mask) {
+        if (pre) CFD_J2TB(true, true); else CFD_J2TB(false, true);
+    } else {
+        if (pre) CFD_J2TB(true, false); else CFD_J2TB(false, false);
+    }
+#undef CFD_J2TB
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+static int g_j2_blocking = 0;  // 0 auto (on), 1 off
+
 template <typename T>
 __global__ void k_rhs2d(const T *__restrict__ div, T *__restrict__ rhs, size_t n, T dx2, T dtv) {
     for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
@@ -239,6 +379,22 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
     const bool vec_ok = (nx % V == 0) && aligned16(src) && aligned16(phi) && aligned16(tmp);
     T *a = phi, *b = tmp;
     const int tk = timing_begin(s);
+    if (g_j2_blocking != 1 && vec_ok && resid_every <= 0 && iters >= 2 && ny >= 3) {
+        // temporally blocked: one single sweep if iters is odd, then fused pairs
+        int done = 0;
+        while (done < iters) {
+            const bool single = (iters - done) & 1;
+            rc = single ? jacobi2d_sweep<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, nullptr, s)
+                        : jacobi2d_tb2_pass<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, s);
+            if (rc) return rc;
+            if (done == 0 && (rc = fix_edge_rows<T>(tmp, phi, nullptr, ny, nx, s))) return rc;
+            done += single ? 1 : 2;
+            T *t = a; a = b; b = t;
+        }
+        timing_end(tk, s, iters);
+        if (a != phi) CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(T) * (size_t)ny * nx, hipMemcpyDeviceToDevice, s));
+        return CFD_OK;
+    }
     for (int it = 0; it < iters; ++it) {
         T *r = (resid_every > 0 && (it + 1) % resid_every == 0) ? resid_out + ((it + 1) / resid_every - 1)
                                                                  : nullptr;
@@ -367,6 +523,12 @@ int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rh
                      int resid_every, double *resid_out, void *stream) {
     return jacobi2d_solve<double>(div, phi, phi_tmp, rhs_ws, mask, ny, nx, dx * dx, (double)dt,
                                   iters, resid_every, resid_out, as_stream(stream));
+}
+
+int cfd_set_jacobi2d_blocking(int steps) {
+    CFD_REQUIRE(steps >= 0 && steps <= 2, "blocking steps must be 0 (auto), 1 or 2");
+    g_j2_blocking = steps;
+    return CFD_OK;
 }
 
 size_t cfd_rbgs_workspace_bytes(int iterations) {

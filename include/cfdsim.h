@@ -69,6 +69,10 @@ int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, float *resid_out, void *stream);
 /* fp64 fields (memory_efficient=False, v5.py:287); dt promotes exactly. */
+/* Both 2-D solves fuse two sweeps per HBM pass (temporal blocking, same bits)
+ * unless disabled: steps = 0 auto (on), 1 off, 2 on.  Residual requests and
+ * unaligned / nx % (16/sizeof(T)) != 0 arrays always run single sweeps. */
+int cfd_set_jacobi2d_blocking(int steps);
 int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, double *resid_out, void *stream);

@@ -40,7 +40,9 @@ def _reset_j3():
     call("cfd_set_jacobi3d_config", 0, 0, 0)
     call("cfd_set_jacobi3d_blocking", 0, 0, 0)
     call("cfd_set_jacobi3d_prefetch", 0)
+    call("cfd_set_jacobi2d_blocking", 0)
     yield
+    call("cfd_set_jacobi2d_blocking", 0)
     call("cfd_set_jacobi3d_config", 0, 0, 0)
     call("cfd_set_jacobi3d_blocking", 0, 0, 0)
 
@@ -60,10 +62,13 @@ def test_jacobi2d_golden_bitexact(golden, name):
     assert np.array_equal(out, d["phi"])
 
 
+@pytest.mark.parametrize("blocking", [1, 2])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("shape,iters", [((37, 53), 17), ((3, 3), 4), ((130, 260), 31),
-                                         ((66, 516), 8), ((2, 9), 3)])
-def test_jacobi2d_random_bitexact(dtype, shape, iters):
+                                         ((66, 516), 8), ((2, 9), 3), ((200, 248), 10), ((9, 124), 6),
+                                         ((71, 1000), 12)])
+def test_jacobi2d_random_bitexact(dtype, shape, iters, blocking):
+    call("cfd_set_jacobi2d_blocking", blocking)
     rng = np.random.default_rng(11)
     div = rng.standard_normal(shape).astype(dtype)
     phi0 = rng.standard_normal(shape).astype(dtype)  # nonzero edges + initial guess
