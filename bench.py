@@ -143,6 +143,7 @@ def main():
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
     call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
     call("cfd_set_jacobi3d_prefetch", ARGS.tb_prefetch)
+    call("cfd_set_jacobi2d_blocking", ARGS.tb)
     dt = np.float32(5e-5)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
@@ -229,10 +230,10 @@ def main():
     # roofline of the dominant kernel, per launch.  A temporally blocked launch
     # (jacobi3d_tb2) performs 2 sweeps in one HBM pass: 12 B of algorithmic
     # traffic per cell per launch = 6 B per cell-update.
-    blocked = len(shape) == 3 and ARGS.tb != 1 and iters >= 2
+    blocked = ARGS.tb != 1 and iters >= 2
     spl = 2 if blocked else 1
     launch_ms = sweep_ms * spl
-    alg_bytes = cells_rank * 12 if blocked else cells_rank * bpc
+    alg_bytes = cells_rank * bpc  # one pass moves bpc bytes per cell whatever it fuses
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
     traffic = load_traffic(ARGS.workload, world)
     out = {
@@ -259,7 +260,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
                      "kernel": ("jacobi3d_tb2" if blocked else "jacobi3d_march") if len(shape) == 3
-                     else "jacobi2d_march",
+                     else ("jacobi2d_tb2" if blocked else "jacobi2d_march"),
                      "sweeps_per_launch": spl, "bytes_per_cell_update": bpc / spl,
                      "cells_per_launch": cells_rank, "algorithmic_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": round(launch_ms, 4),
