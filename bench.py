@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Benchmark: Gcell-updates/s of the pressure-Poisson Jacobi sweep on MI355X.
+"""Benchmark: Gcell-updates/s of the pressure-Poisson solve on MI355X.
 
 Default workload (north_star, BASELINE.json): 7-point Jacobi on a 1024^3 fp32
 grid, one "step" = one pressure solve = zero-fill phi + ITERS (200) Jacobi
@@ -17,6 +17,11 @@ dominant kernel (the sweep) at 12 algorithmic bytes per fp32 cell-update
 stream around its launches.  `cpu_baseline` times the NumPy restatement of the
 reference's Jacobi branch (oracle/, bit-exact to v5.py:336-346) on a bounded
 sample of the same grid, on this host, at N=1 only.
+
+`--workload rbgs3d_1024` is config 5: red-black Gauss-Seidel (the 3-D
+generalisation of v5.py:202-226) on the 1024^3 grid, one step = zero-fill +
+200 iterations at the reference's tolerance 1e-8 (stop rule evaluated on device
+every iteration; one cell-update per cell per iteration).
 """
 from __future__ import annotations
 
@@ -41,7 +46,9 @@ WORKLOADS = {
     "jacobi3d_1024": ((1024, 1024, 1024), "f32", 200, 12),
     "jacobi3d_512": ((512, 512, 512), "f32", 200, 12),
     "jacobi2d_8192_f64": ((8192, 8192), "f64", 1000, 24),
+    "rbgs3d_1024": ((1024, 1024, 1024), "f32", 200, 12),
 }
+GS_TOL = 1e-8  # OptimizedTurbulentConfig.pressure_tolerance (v5.py)
 
 
 def parse():
@@ -86,9 +93,25 @@ def load_traffic(workload: str, n_gpus: int):
     return None
 
 
-def cpu_baseline(shape, iters_total_hint):
-    """NumPy restatement timed on this host (1 thread: NumPy ufuncs)."""
+def cpu_baseline(shape, iters_total_hint, gs=False):
+    """NumPy restatement timed on this host (1 thread: NumPy ufuncs); for the
+    red-black GS workload the oracle's C restatement (serial, 1 thread: the
+    reference's numba build is not installed here)."""
     import oracle
+    if gs:
+        sample = (min(shape[0], 128), shape[1], shape[2])
+        rng = np.random.default_rng(1234)
+        div = rng.standard_normal(sample, dtype=np.float32)
+        it = 3
+        h = 1.0 / (shape[2] - 1)
+        t0 = time.perf_counter()
+        oracle.rbgs3d(div, dx=h, dy=h, dz=h, dt=np.float32(5e-5), iters=it, tol=GS_TOL)
+        t = time.perf_counter() - t0
+        cells = (sample[0] - 2) * (sample[1] - 2) * (sample[2] - 2) * it
+        return {"value": cells / t / 1e9, "unit": "Gcell-updates/s", "cores": 1, "kind": "port",
+                "sample": f"{sample[0]}x{sample[1]}x{sample[2]} slab of the grid, {it} iterations, "
+                          f"oracle_rbgs3d_f32 (C, serial red-black order); {t:.2f} s; host has "
+                          f"{os.cpu_count()} logical CPUs, 1 used"}
     if len(shape) == 3:
         nz = min(shape[0], ARGS.cpu_sample_planes)
         sample = (nz, shape[1], shape[2])
@@ -147,7 +170,36 @@ def main():
     dt = np.float32(5e-5)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
-    if len(shape) == 3:
+    gs = ARGS.workload.startswith("rbgs")
+    gs_done = None
+    if gs:
+        nz, ny, nx = shape
+        h = 1.0 / (nx - 1)
+        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else 2)
+        if not use_slab:
+            div = torch.randn(shape, generator=g, device=dev, dtype=torch.float32)
+            phi = torch.zeros_like(div)
+            tmp = torch.zeros_like(div)
+            gs_ws = torch.empty(int(lib().cfd_rbgs_workspace_bytes(iters)), dtype=torch.uint8, device=dev)
+            gs_done = torch.zeros(1, dtype=torch.int32, device=dev)
+
+            def step():
+                phi.zero_()
+                K.solve_pressure_gauss_seidel3d(phi, div, h, h, h, dt, None, iters, GS_TOL, workspace=gs_ws,
+                                                iters_done=gs_done, phi_tmp=tmp)
+        else:
+            comm = S.RcclComm(rank, world)
+            sj = S.SlabRBGS3D(plan, ny, nx, h, h, h, dt, comm, device=dev)
+            sj.div.copy_(torch.randn(sj.div.shape, generator=g, device=dev, dtype=torch.float32))
+            gs_done = sj.iters_done
+
+            def step():
+                sj.solve(iters, tolerance=GS_TOL, overlap=not ARGS.no_overlap)
+        cells_all = (nz - 2) * (ny - 2) * (nx - 2) * iters
+        cells_rank = (plan.z_update_end - plan.z_update_begin) * (ny - 2) * (nx - 2)
+        workload = f"rbgs3d_7pt_{nz}x{ny}x{nx}_f32"
+        dtype = "f32"
+    elif len(shape) == 3:
         nz, ny, nx = shape
         h = 1.0 / (nx - 1)
         plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else 2)
@@ -195,9 +247,9 @@ def main():
 
     verified = None
     if use_slab and len(shape) == 3 and not ARGS.no_verify:
-        verified = verify_slabs(S, K, dist, comm, world, rank, dev)
+        verified = (verify_slabs_rbgs if gs else verify_slabs)(S, K, dist, comm, world, rank, dev)
 
-    if ARGS.sweep_tiles and world == 1 and len(shape) == 3:
+    if ARGS.sweep_tiles and world == 1 and len(shape) == 3 and not gs:
         tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells_rank, rhs)
 
     for _ in range(ARGS.warmup):
@@ -230,8 +282,10 @@ def main():
     # roofline of the dominant kernel, per launch.  A temporally blocked launch
     # (jacobi3d_tb2) performs 2 sweeps in one HBM pass: 12 B of algorithmic
     # traffic per cell per launch = 6 B per cell-update.
-    blocked = ARGS.tb != 1 and iters >= 2
-    spl = 2 if blocked else 1
+    blocked = ARGS.tb != 1 and (iters >= 2 or gs)
+    # sweeps per launch: 2 Jacobi sweeps per blocked pass; the GS timing
+    # counts iterations, and a fused GS pass is one iteration (both colours)
+    spl = 2 if blocked and not gs else 1
     launch_ms = sweep_ms * spl
     alg_bytes = cells_rank * bpc  # one pass moves bpc bytes per cell whatever it fuses
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
@@ -259,7 +313,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": ("jacobi3d_tb2" if blocked else "jacobi3d_march") if len(shape) == 3
+                     "kernel": ("jacobi3d_tb2<MODE_RBGS>" if blocked else "rbgs3d_color x2") if gs
+                     else ("jacobi3d_tb2" if blocked else "jacobi3d_march") if len(shape) == 3
                      else ("jacobi2d_tb2" if blocked else "jacobi2d_march"),
                      "sweeps_per_launch": spl, "bytes_per_cell_update": bpc / spl,
                      "cells_per_launch": cells_rank, "algorithmic_bytes_per_launch": alg_bytes,
@@ -267,15 +322,22 @@ def main():
                      "max_rank_avg_launch_ms": round(sweep_ms_max * spl, 4)},
         "cpu_baseline": None,
     }
+    if gs:
+        out["metric"] = METRIC.replace("Jacobi", "red-black Gauss-Seidel")
+        out["config"]["tolerance"] = GS_TOL
+        out["config"]["iterations_done_last_step"] = int(gs_done.item())
+        out["roofline"]["bytes_per_cell_update"] = bpc if blocked else 2 * bpc
     if verified is not None:
-        out["config"]["multi_gpu_parity"] = ("bit-exact vs 1-GPU solve (96^3, 7+8 sweeps, both ghost depths)"
+        out["config"]["multi_gpu_parity"] = (("bit-exact vs 1-GPU solve (96^3, 9 its + early stop, both ghost depths)"
+                                              if gs else
+                                              "bit-exact vs 1-GPU solve (96^3, 7+8 sweeps, both ghost depths)")
                                              if verified else "MISMATCH")
     if rank == 0 and world == 1 and not ARGS.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(shape, iters)
+        out["cpu_baseline"] = cpu_baseline(shape, iters, gs)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if use_slab and len(shape) == 3:
-        sj.comm.close()
+        comm.close()
     if use_slab:
         dist.destroy_process_group()
 
@@ -309,6 +371,40 @@ def verify_slabs(S, K, dist, comm, world, rank, dev):
     dist.broadcast(flag, src=0)
     if not bool(flag.item()) and rank == 0:
         print("WARNING: multi-GPU slab result differs from the single-GPU solve", file=sys.stderr)
+    return bool(flag.item())
+
+
+def verify_slabs_rbgs(S, K, dist, comm, world, rank, dev):
+    """verify_slabs for the distributed red-black GS: both ghost depths, a
+    fixed count and an early stop (global max|change| < tol)."""
+    import torch
+    nz, ny, nx = 96, 90, 104
+    g = torch.Generator(device=dev).manual_seed(98)
+    div = torch.randn((nz, ny, nx), generator=g, device=dev, dtype=torch.float32) * 1e-3
+    ok = True
+    for ghost, iters, tol in ((1, 9, 0.0), (2, 9, 0.0), (2, 400, 2e-5)):
+        plan = S.SlabPlan(nz, world, rank, ghost=ghost)
+        sg = S.SlabRBGS3D(plan, ny, nx, 0.05, 0.05, 0.05, np.float32(1e-2), comm, device=dev)
+        lo = plan.z_lo - ghost
+        for k in range(plan.nz_total):
+            if 0 <= lo + k < nz:
+                sg.div[k].copy_(div[lo + k])
+        sg.solve(iters, tolerance=tol, overlap=True)
+        mine = sg.owned().contiguous()
+        sizes = [S.SlabPlan(nz, world, r, ghost=ghost).nz_local for r in range(world)]
+        parts = [torch.empty((n, ny, nx), dtype=torch.float32, device=dev) for n in sizes]
+        dist.all_gather(parts, mine) if len(set(sizes)) == 1 else _gather_uneven(dist, parts, mine, rank)
+        n_mine = int(sg.iters_done.item())
+        if rank == 0:
+            ref = torch.zeros_like(div)
+            done = torch.zeros(1, dtype=torch.int32, device=dev)
+            K.solve_pressure_gauss_seidel3d(ref, div, 0.05, 0.05, 0.05, np.float32(1e-2), None, iters, tol,
+                                            iters_done=done)
+            ok &= bool(torch.equal(torch.cat(parts), ref)) and n_mine == int(done.item())
+    flag = torch.tensor([1 if ok else 0], device=dev)
+    dist.broadcast(flag, src=0)
+    if not bool(flag.item()) and rank == 0:
+        print("WARNING: multi-GPU RB-GS result differs from the single-GPU solve", file=sys.stderr)
     return bool(flag.item())
 
 

@@ -10,13 +10,15 @@ device pointer in the process.
 from __future__ import annotations
 
 import ctypes
+import os
 from ctypes import c_double, c_float, c_int, c_size_t, c_void_p, c_char_p
 from pathlib import Path
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "libcfdsim.so"
+# CFDSIM_LIB selects another in-tree build of the same ABI (tuning experiments)
+LIB_PATH = Path(os.environ.get("CFDSIM_LIB", PKG_DIR / "libcfdsim.so"))
 ABI_VERSION = 1
 
 P = c_void_p  # device pointer / stream / opaque handle
@@ -62,6 +64,13 @@ PROTOTYPES = {
                                       c_int, c_double, c_float, c_int, c_int, P, P]),
     "cfd_jacobi3d_sweep_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_double,
                                        c_float, P, P]),
+    "cfd_slab_rbgs3d_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, c_double, c_double, c_double, c_float, c_int, c_double, P, P,
+                                    c_int, P, P]),
+    "cfd_rbgs3d_pass_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_double, c_double, c_double, c_float, c_double, c_int, P, P]),
+    "cfd_rbgs_init": (c_int, [P, c_int, P, P]),
+    "cfd_rbgs_finish": (c_int, [P, P, P, c_size_t, P, P]),
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_blocking": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_prefetch": (c_int, [c_int]),

@@ -18,4 +18,34 @@ int jacobi3d_tb_prefetch();  // planes of prefetch in the blocked kernel (1 or 2
 int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, float h2, float dt, int W, int zchunk,
                       bool pre, hipStream_t s);
+// red-black GS workspace (cfd_rbgs_workspace_bytes): flags[1] = iterations
+// done (the fused kernels' stop counter), float maxc[iterations] at byte 16
+struct RbgsWs {
+    int flags[4];
+    float maxc[1];
+};
+// poisson2d.hip
+int launch_rbgs_init(RbgsWs *ws, int iterations, int *iters_done, hipStream_t s);
+// after fused (out-of-place) iterations: phi <- phi_tmp when an odd number
+// ran, and *iters_done <- the count (both read on device: no host sync)
+int launch_rbgs_finish(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n,
+                       int *iters_done, hipStream_t s);
+
+// 3-D red-black GS (poisson3d.hip / jacobi3d_tb.hip)
+struct RbgsConsts {
+    float cx, cy, cz, cd, dt_inv, tol;
+};
+RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double tolerance);
+// whether the fused out-of-place pass applies (no mask, float4 layout, blocking on)
+bool rbgs3d_fused_ok(const float *phi, const float *phi_tmp, const float *div, const uint8_t *mask,
+                     int nx);
+// in-place colour pass over planes [z0, z1); local plane 0 = global plane zoff
+int rbgs3d_colour_pass(int colour, float *phi, const float *div, const uint8_t *mask, int ny,
+                       int nx, int z0, int z1, int zoff, const RbgsConsts &k, RbgsWs *ws, int it,
+                       hipStream_t s);
+// one fused iteration (both colours) of planes [zb, ze) of `out` from `in`;
+// max|change| into ws->maxc[it], stop counter ws->flags[1]
+int rbgs3d_tb_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
+                   int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
+                   RbgsWs *ws, hipStream_t s);
 }  // namespace cfd

@@ -15,7 +15,7 @@
 //  (f32(dx^2)*div)/dt is recomputed in-register from div every sweep: the same
 //  4 B of traffic as reading a precomputed rhs array, bit-identical to NumPy,
 //  and no prologue pass or workspace.
-#include "common.hpp"
+#include "internal.hpp"
 
 namespace cfd {
 
@@ -411,12 +411,8 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
 }
 
 // ----------------------------------------------------------- red-black GS
-// Workspace layout: [0] int stop flag (unused by kernels, kept for ABI room),
-// [1] int iters_done scratch, then float maxc[iterations] at byte 16.
-struct RbgsWs {
-    int flags[4];
-    float maxc[1];
-};
+// Workspace layout (RbgsWs, internal.hpp): flags[1] = iterations done by the
+// fused path, then float maxc[iterations] at byte 16.
 
 // Colour pass, in place.  Each thread owns a 4-cell x-vector of one row and
 // rewrites it whole (cells of the other colour unchanged; nobody else writes
@@ -429,12 +425,180 @@ __device__ inline bool rbgs_stopped(const RbgsWs *ws, int it, float tol) {
 
 __global__ void rbgs_init(RbgsWs *ws, int iterations, int *iters_done) {
     for (int k = threadIdx.x; k < iterations; k += blockDim.x) ws->maxc[k] = 0.0f;
-    if (threadIdx.x < 4) ws->flags[threadIdx.x] = 0;
+    if (threadIdx.x < 4) ws->flags[threadIdx.x] = threadIdx.x == 1 ? iterations : 0;
     if (threadIdx.x == 0 && iters_done) *iters_done = iterations;
 }
 
 int launch_rbgs_init(RbgsWs *ws, int iterations, int *iters_done, hipStream_t s) {
     hipLaunchKernelGGL(rbgs_init, dim3(1), dim3(1024), 0, s, ws, iterations, iters_done);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// The fused path ping-pongs phi / phi_tmp, one buffer per iteration; where the
+// last iteration landed depends on the device-side stop, so the copy-back is
+// decided on device too (no host sync in the solve).
+__global__ void rbgs_finish(const RbgsWs *__restrict__ ws, float *__restrict__ phi,
+                            const float *__restrict__ tmp, size_t n, int *iters_done) {
+    const int done = ws->flags[1];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && iters_done) *iters_done = done;
+    if (!tmp || !(done & 1)) return;
+    const size_t n4 = n / 4;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (size_t k = t0; k < n4; k += stride)
+        reinterpret_cast<float4 *>(phi)[k] = reinterpret_cast<const float4 *>(tmp)[k];
+    for (size_t k = 4 * n4 + t0; k < n; k += stride) phi[k] = tmp[k];
+}
+
+int launch_rbgs_finish(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n,
+                       int *iters_done, hipStream_t s) {
+    long blocks = (long)((n / 4 + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(rbgs_finish, dim3(blocks), dim3(256), 0, s, ws, phi, phi_tmp, n, iters_done);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// Fused red-black iteration, 2-D: the overlapped-segment row march of
+// jacobi2d_tb2 with the colour-0 half-sweep as the first level and the
+// colour-1 half-sweep as the second, out of place (12 B per cell per
+// iteration instead of ~2 x 12 B for two in-place colour passes).  Masked
+// cells keep their value (v5.py:216).  Bit-identical to rbgs2d_color<0/1>.
+__device__ inline float gs5(float E, float W, float N, float S, float d, float cx, float cy,
+                            float cd, float dt_inv) {
+    const float rhs = -d * dt_inv;
+    const float a = cx * (E + W);
+    const float b = cy * (N + S);
+    return ((a + b) - rhs) * cd;
+}
+
+template <bool MASK>
+__global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
+                                                 float *__restrict__ out,
+                                                 const float *__restrict__ div,
+                                                 const uint8_t *__restrict__ mask, int ny, int nx,
+                                                 int nseg, int rows_per_chunk, float cx, float cy,
+                                                 float cd, float dt_inv, float tol, RbgsWs *ws,
+                                                 int it) {
+    constexpr int VEC = 4;
+    constexpr int SOUT = 64 * VEC - 2 * VEC;
+    if (it > 0 && ws->maxc[it - 1] < tol) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&ws->flags[1], it);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    const int wpb = blockDim.x / 64;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const long wave = (long)bid * wpb + threadIdx.x / 64;
+    const int seg = (int)(wave % nseg);
+    const int chunk = (int)(wave / nseg);
+    const int y0 = 1 + chunk * rows_per_chunk;
+    float mx = 0.f;
+    if (y0 < ny - 1) {  // wave-uniform
+        const int y1 = min(y0 + rows_per_chunk, ny - 1);
+        const int xs = seg * SOUT;
+        const int x0 = xs - VEC + lane * VEC;
+        const bool valid = x0 >= 0 && x0 < nx;
+        const bool writer = lane >= 1 && lane <= 62 && valid;
+        float am[VEC], ac[VEC], ap[VEC], app[VEC];  // level 0 rows r-1, r, r+1, r+2
+        float bm[VEC], bc[VEC];                     // level 1 rows r-2, r-1
+        float dm[VEC], dc[VEC], dn[VEC];            // div rows r-1, r, r+1
+        uint8_t mm[VEC], mc[VEC], mn[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            am[k] = ac[k] = ap[k] = app[k] = bm[k] = bc[k] = dm[k] = dc[k] = dn[k] = 0.f;
+            mm[k] = mc[k] = mn[k] = 0;
+        }
+        const int rs = y0 - 1;
+        auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
+        if (valid) {
+            if (rs - 1 >= 0) ld<float, VEC>(in + row(rs - 1), am);
+            ld<float, VEC>(in + row(rs), ac);
+            ld<float, VEC>(in + row(rs + 1), ap);
+            ld<float, VEC>(div + row(rs), dc);
+            ld<float, VEC>(div + row(rs + 1), dn);
+            if (MASK) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) { mc[k] = mask[row(rs) + k]; mn[k] = mask[row(rs + 1) + k]; }
+            }
+        }
+        for (int r = rs; r <= y1; ++r) {
+            if (valid && r + 1 <= y1 && r + 2 <= ny - 1) ld<float, VEC>(in + row(r + 2), app);
+            // level 1 (colour 0) of row r
+            const bool edge = r == 0 || r == ny - 1;
+            const float wl = __shfl_up(ac[VEC - 1], 1, 64);
+            const float er = __shfl_down(ac[0], 1, 64);
+            float l1[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const int x = x0 + k;
+                l1[k] = ac[k];
+                if (!edge && x >= 1 && x < nx - 1 && ((r + x + 1) & 1) == 0 && !(MASK && mc[k])) {
+                    const float E = (k + 1 < VEC) ? ac[k + 1] : er;
+                    const float W = (k > 0) ? ac[k - 1] : wl;
+                    l1[k] = gs5(E, W, ap[k], am[k], dc[k], cx, cy, cd, dt_inv);
+                    const float ch = fabsf(l1[k] - ac[k]);
+                    if (valid && ch > mx) mx = ch;
+                }
+            }
+            // level 2 (colour 1) of row r-1
+            const float wl1 = __shfl_up(bc[VEC - 1], 1, 64);
+            const float er1 = __shfl_down(bc[0], 1, 64);
+            if (r >= y0 + 1 && writer) {
+                float o[VEC];
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const int x = x0 + k;
+                    o[k] = bc[k];
+                    if (x >= 1 && x < nx - 1 && ((r - 1 + x + 2) & 1) == 0 && !(MASK && mm[k])) {
+                        const float E = (k + 1 < VEC) ? bc[k + 1] : er1;
+                        const float W = (k > 0) ? bc[k - 1] : wl1;
+                        o[k] = gs5(E, W, l1[k], bm[k], dm[k], cx, cy, cd, dt_inv);
+                        const float ch = fabsf(o[k] - bc[k]);
+                        if (ch > mx) mx = ch;
+                    }
+                }
+                st<float, VEC>(out + row(r - 1), o);
+            }
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                am[k] = ac[k]; ac[k] = ap[k]; ap[k] = app[k];
+                bm[k] = bc[k]; bc[k] = l1[k];
+                dm[k] = dc[k]; dc[k] = dn[k];
+                if (MASK) { mm[k] = mc[k]; mc[k] = mn[k]; }
+            }
+            if (valid && r + 2 <= y1 && r + 2 <= ny - 1) {
+                ld<float, VEC>(div + row(r + 2), dn);
+                if (MASK) {
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) mn[k] = mask[row(r + 2) + k];
+                }
+            }
+        }
+    }
+    wave_reduce_max_store(mx, &ws->maxc[it]);
+}
+
+static int rbgs2d_tb_pass(const float *in, float *out, const float *div, const uint8_t *mask,
+                          int ny, int nx, float cx, float cy, float cd, float dt_inv, float tol,
+                          RbgsWs *ws, int it, hipStream_t s) {
+    constexpr int SOUT = 64 * 4 - 2 * 4;
+    const int nseg = ceil_div(nx, SOUT);
+    const int rows = ny - 2;
+    int rpc = ceil_div((long)rows * nseg, 8192);
+    if (rpc < 8) rpc = 8;
+    if (rpc > 64) rpc = 64;
+    const int nchunk = ceil_div(rows, rpc);
+    const int wpb = 4;
+    const int blocks = ceil_div((long)nseg * nchunk, wpb);
+    if (mask)
+        hipLaunchKernelGGL(rbgs2d_tb<true>, dim3(blocks), dim3(wpb * 64), 0, s, in, out, div, mask,
+                           ny, nx, nseg, rpc, cx, cy, cd, dt_inv, tol, ws, it);
+    else
+        hipLaunchKernelGGL(rbgs2d_tb<false>, dim3(blocks), dim3(wpb * 64), 0, s, in, out, div, mask,
+                           ny, nx, nseg, rpc, cx, cy, cd, dt_inv, tol, ws, it);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }
@@ -538,7 +702,6 @@ size_t cfd_rbgs_workspace_bytes(int iterations) {
 int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
                    double dy, float dt, int iterations, double tolerance, float *phi_tmp, void *ws,
                    int *iters_done, void *stream) {
-    (void)phi_tmp;  // the in-place colour passes need no second buffer
     CFD_REQUIRE(phi && div && ws, "rbgs2d: null pointer");
     CFD_REQUIRE(ny >= 1 && nx >= 1 && iterations >= 0, "rbgs2d: bad arguments");
     hipStream_t s = as_stream(stream);
@@ -554,12 +717,24 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
     if (ny < 3 || nx < 3 || iterations == 0) return CFD_OK;
     const bool vec_ok = (nx % 4 == 0) && aligned16(phi) && aligned16(div);
     const int tk = timing_begin(s);
+    if (phi_tmp && g_j2_blocking != 1 && vec_ok && aligned16(phi_tmp)) {
+        // fused: one out-of-place pass per iteration (both colours), ping-pong
+        if ((rc = fix_edge_rows<float>(phi, phi_tmp, nullptr, ny, nx, s))) return rc;
+        float *a = phi, *b = phi_tmp;
+        for (int it = 0; it < iterations; ++it) {
+            if ((rc = rbgs2d_tb_pass(a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, s)))
+                return rc;
+            float *t = a; a = b; b = t;
+        }
+        timing_end(tk, s, iterations);
+        return launch_rbgs_finish(w, phi, phi_tmp, (size_t)ny * nx, iters_done, s);
+    }
     for (int it = 0; it < iterations; ++it) {
         rc = vec_ok ? rbgs2d_iter<4>(phi, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, iters_done, s)
                         : rbgs2d_iter<1>(phi, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, iters_done, s);
         if (rc) return rc;
     }
-    timing_end(tk, s, 2LL * iterations);
+    timing_end(tk, s, iterations);
     return CFD_OK;
 }
 

@@ -76,6 +76,11 @@ static J3Config g_j3;
 int jacobi3d_tb_rows() { return g_j3.tb_rows ? g_j3.tb_rows : 13; }
 int jacobi3d_tb_zchunk() { return g_j3.tb_zchunk; }
 bool jacobi3d_tb_enabled() { return g_j3.tb_steps != 1; }
+bool rbgs3d_fused_ok(const float *phi, const float *phi_tmp, const float *div, const uint8_t *mask,
+                     int nx) {
+    return phi_tmp && jacobi3d_tb_enabled() && !mask && nx % 4 == 0 && aligned16(phi) &&
+           aligned16(phi_tmp) && aligned16(div);
+}
 int jacobi3d_tb_prefetch() { return g_j3.tb_prefetch == 2 ? 2 : 1; }
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -366,31 +371,28 @@ int launch_rhs_f32(const float *div, float *rhs, size_t n, float h2, float dt, h
 }
 
 // ----------------------------------------------------------- red-black GS 3-D
-struct RbgsWs {
-    int flags[4];
-    float maxc[1];
-};
-int launch_rbgs_init(RbgsWs *ws, int iterations, int *iters_done, hipStream_t s);
-
+// In-place colour pass over planes [z0, z0 + gridDim.z) of a local array whose
+// plane 0 is global plane zoff (colour parity is global, so a slab's cells get
+// the colours they have in the whole grid).  The fused out-of-place pass is
+// jacobi3d_tb2<.., MODE_RBGS, ..> (jacobi3d_tb.hip); this one serves masks.
 template <int C>
 __global__ __launch_bounds__(256) void rbgs3d_color(float *__restrict__ phi,
                                                     const float *__restrict__ div,
                                                     const uint8_t *__restrict__ mask, int ny,
-                                                    int nx, float cx, float cy, float cz, float cd,
-                                                    float dt_inv, float tol, RbgsWs *ws, int it,
-                                                    int *iters_done) {
+                                                    int nx, int z0, int zoff, float cx, float cy,
+                                                    float cz, float cd, float dt_inv, float tol,
+                                                    RbgsWs *ws, int it) {
     if (it > 0 && ws->maxc[it - 1] < tol) {
-        if (C == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0 &&
-            iters_done)
-            atomicMin(iters_done, it);
+        if (C == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+            atomicMin(&ws->flags[1], it);
         return;
     }
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = blockIdx.y + 1;
-    const int z = blockIdx.z + 1;
+    const int z = z0 + blockIdx.z;
     float mx = 0.f;
-    // colour c: (z + i + j + 1 + c) even; j from the first cell of that colour
-    if (x < nx - 1 && x >= 1 && ((z + i + x + 1 + C) & 1) == 0) {
+    // colour c: (zg + i + j + 1 + c) even
+    if (x < nx - 1 && x >= 1 && ((zoff + z + i + x + 1 + C) & 1) == 0) {
         const size_t plane = (size_t)ny * nx;
         const size_t c = (size_t)z * plane + (size_t)i * nx + x;
         if (!(mask && mask[c])) {
@@ -405,6 +407,36 @@ __global__ __launch_bounds__(256) void rbgs3d_color(float *__restrict__ phi,
         }
     }
     wave_reduce_max_store(mx, &ws->maxc[it]);
+}
+
+int rbgs3d_colour_pass(int colour, float *phi, const float *div, const uint8_t *mask, int ny,
+                       int nx, int z0, int z1, int zoff, const RbgsConsts &k, RbgsWs *ws, int it,
+                       hipStream_t s) {
+    if (z1 <= z0 || ny < 3 || nx < 3) return CFD_OK;
+    dim3 grid(ceil_div(nx, 256), ny - 2, z1 - z0);
+    if (colour == 0)
+        hipLaunchKernelGGL(rbgs3d_color<0>, grid, dim3(256), 0, s, phi, div, mask, ny, nx, z0, zoff,
+                           k.cx, k.cy, k.cz, k.cd, k.dt_inv, k.tol, ws, it);
+    else
+        hipLaunchKernelGGL(rbgs3d_color<1>, grid, dim3(256), 0, s, phi, div, mask, ny, nx, z0, zoff,
+                           k.cx, k.cy, k.cz, k.cd, k.dt_inv, k.tol, ws, it);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// v5.py:205-210 generalised to 3-D: Python-float constants, rounded to f32
+// where they meet f32 data; 1.0 / np.float32(dt) stays float32
+RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double tolerance) {
+    const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy), dz2_inv = 1.0 / (dz * dz);
+    const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv + dz2_inv));
+    RbgsConsts k;
+    k.cx = (float)dx2_inv;
+    k.cy = (float)dy2_inv;
+    k.cz = (float)dz2_inv;
+    k.cd = (float)denom_inv;
+    k.dt_inv = 1.0f / dt;
+    k.tol = (float)tolerance;
+    return k;
 }
 
 }  // namespace cfd
@@ -519,30 +551,64 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
 int cfd_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask, int nz, int ny, int nx,
                    double dx, double dy, double dz, float dt, int iterations, double tolerance,
                    float *phi_tmp, void *ws, int *iters_done, void *stream) {
-    (void)phi_tmp;
     CFD_REQUIRE(phi && div && ws, "rbgs3d: null pointer");
     CFD_REQUIRE(nz >= 1 && ny >= 1 && nx >= 1 && iterations >= 0, "rbgs3d: bad arguments");
     hipStream_t s = as_stream(stream);
-    const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy), dz2_inv = 1.0 / (dz * dz);
-    const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv + dz2_inv));
-    const float cx = (float)dx2_inv, cy = (float)dy2_inv, cz = (float)dz2_inv, cd = (float)denom_inv;
-    const float dt_inv = 1.0f / dt;
-    const float tol = (float)tolerance;
+    const RbgsConsts k = rbgs3d_consts(dx, dy, dz, dt, tolerance);
     RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
     int rc = launch_rbgs_init(w, iterations, iters_done, s);
     if (rc) return rc;
-    if (nz < 3 || ny < 3 || nx < 3) return CFD_OK;
-    dim3 grid(ceil_div(nx, 256), ny - 2, nz - 2);
+    if (nz < 3 || ny < 3 || nx < 3 || iterations == 0) return CFD_OK;
+    const size_t n = (size_t)nz * ny * nx;
     const int tk = timing_begin(s);
-    for (int it = 0; it < iterations; ++it) {
-        hipLaunchKernelGGL(rbgs3d_color<0>, grid, dim3(256), 0, s, phi, div, mask, ny, nx, cx, cy,
-                           cz, cd, dt_inv, tol, w, it, iters_done);
-        hipLaunchKernelGGL(rbgs3d_color<1>, grid, dim3(256), 0, s, phi, div, mask, ny, nx, cx, cy,
-                           cz, cd, dt_inv, tol, w, it, iters_done);
-        CFD_LAUNCH_CHECK();
+    if (rbgs3d_fused_ok(phi, phi_tmp, div, mask, nx)) {
+        // fused: one out-of-place pass per iteration (both colours), ping-pong
+        if ((rc = launch_fix_faces3d(phi, phi_tmp, nullptr, ny, nx, 0, nz, 0, nz - 1, s))) return rc;
+        float *a = phi, *b = phi_tmp;
+        for (int it = 0; it < iterations; ++it) {
+            if ((rc = rbgs3d_tb_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, it, w, s))) return rc;
+            float *t = a; a = b; b = t;
+        }
+        timing_end(tk, s, iterations);
+        return launch_rbgs_finish(w, phi, phi_tmp, n, iters_done, s);
     }
-    timing_end(tk, s, 2LL * iterations);
-    return CFD_OK;
+    for (int it = 0; it < iterations; ++it) {
+        if ((rc = rbgs3d_colour_pass(0, phi, div, mask, ny, nx, 1, nz - 1, 0, k, w, it, s))) return rc;
+        if ((rc = rbgs3d_colour_pass(1, phi, div, mask, ny, nx, 1, nz - 1, 0, k, w, it, s))) return rc;
+    }
+    timing_end(tk, s, iterations);
+    return launch_rbgs_finish(w, phi, nullptr, n, iters_done, s);
+}
+
+int cfd_rbgs3d_pass_f32(const float *in, float *out, const float *div, int nz, int ny, int nx,
+                        int z_begin, int z_end, int fixed_lo, int fixed_hi, int z_global_offset,
+                        double dx, double dy, double dz, float dt, double tolerance, int iteration,
+                        void *ws, void *stream) {
+    CFD_REQUIRE(in && out && div && ws, "rbgs3d_pass: null pointer");
+    CFD_REQUIRE(in != out, "rbgs3d_pass: out of place only");
+    CFD_REQUIRE(nz >= 1 && ny >= 3 && nx >= 1 && iteration >= 0, "rbgs3d_pass: bad arguments");
+    CFD_REQUIRE(nx % 4 == 0 && aligned16(in) && aligned16(out) && aligned16(div),
+                "rbgs3d_pass: needs nx %% 4 == 0 and 16-byte aligned arrays");
+    // a non-fixed neighbour plane is itself updated from the plane beyond it
+    CFD_REQUIRE(z_begin >= (fixed_lo ? 1 : 2) && z_end <= nz - (fixed_hi ? 1 : 2) && z_begin <= z_end,
+                "rbgs3d_pass: planes [%d,%d) need 1 (fixed) or 2 readable planes on each side (nz %d)",
+                z_begin, z_end, nz);
+    const RbgsConsts k = rbgs3d_consts(dx, dy, dz, dt, tolerance);
+    return rbgs3d_tb_pass(in, out, div, nz, ny, nx, z_begin, z_end, fixed_lo, fixed_hi,
+                          z_global_offset, k, iteration, reinterpret_cast<RbgsWs *>(ws),
+                          as_stream(stream));
+}
+
+int cfd_rbgs_init(void *ws, int iterations, int *iters_done, void *stream) {
+    CFD_REQUIRE(ws && iterations >= 0, "rbgs_init: bad arguments");
+    return launch_rbgs_init(reinterpret_cast<RbgsWs *>(ws), iterations, iters_done, as_stream(stream));
+}
+
+int cfd_rbgs_finish(void *ws, float *phi, const float *phi_tmp, size_t n, int *iters_done,
+                    void *stream) {
+    CFD_REQUIRE(ws && phi, "rbgs_finish: null pointer");
+    return launch_rbgs_finish(reinterpret_cast<const RbgsWs *>(ws), phi, phi_tmp, n, iters_done,
+                              as_stream(stream));
 }
 
 }  // extern "C"

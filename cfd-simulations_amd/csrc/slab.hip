@@ -203,4 +203,109 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
     return CFD_OK;
 }
 
+// Distributed red-black GS (config 5).  Colours are global: local plane k is
+// global plane z_global_offset + k, so the decomposed sweep updates exactly
+// the cells the single-GPU sweep updates, from the same neighbour values
+// (bit-identical for every rank count).  The stop rule needs the GLOBAL
+// max|change| of each iteration: one ncclAllReduce(max) of 4 bytes per
+// iteration (skipped when tolerance <= 0, which can never stop).
+//  * fused (ghost 2, no mask): one out-of-place pass per iteration; its two
+//    owned boundary planes per side go out while the interior runs.
+//  * otherwise: in-place colour passes, a G-plane exchange after each colour.
+int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
+                        const uint8_t *mask, int nz_local, int ghost, int ny, int nx, int lo_peer,
+                        int hi_peer, int z_update_begin, int z_update_end, int z_global_offset,
+                        double dx, double dy, double dz, float dt, int iterations,
+                        double tolerance, void *ws, int *iters_done, int overlap, void *stream,
+                        void *comm_stream) {
+    SlabComm *c = reinterpret_cast<SlabComm *>(comm);
+    CFD_REQUIRE(c && div && phi && ws, "slab_rbgs3d: null pointer");
+    CFD_REQUIRE(ghost == 1 || ghost == 2, "slab_rbgs3d: ghost depth must be 1 or 2");
+    CFD_REQUIRE(nz_local >= ghost && ny >= 1 && nx >= 1 && iterations >= 0, "slab_rbgs3d: bad shape");
+    const int G = ghost;
+    CFD_REQUIRE(z_update_begin >= G && z_update_end <= nz_local + G &&
+                    z_update_begin <= z_update_end,
+                "slab_rbgs3d: update range [%d,%d) outside owned planes %d..%d", z_update_begin,
+                z_update_end, G, nz_local + G - 1);
+    CFD_REQUIRE(lo_peer < c->nranks && hi_peer < c->nranks, "slab_rbgs3d: bad peer");
+    hipStream_t s = as_stream(stream);
+    hipStream_t cs = comm_stream ? as_stream(comm_stream) : s;
+    RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
+    const RbgsConsts k = rbgs3d_consts(dx, dy, dz, dt, tolerance);
+    int rc = launch_rbgs_init(w, iterations, iters_done, s);
+    if (rc || iterations == 0 || ny < 3 || nx < 3) return rc;
+    const int nzt = nz_local + 2 * G;
+    const size_t plane = (size_t)ny * nx;
+    const int zb = z_update_begin, ze = z_update_end, zoff = z_global_offset;
+    const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
+    const bool reduce = c->nranks > 1 && k.tol > 0.0f;
+    auto allreduce = [&](int it, hipStream_t st) -> int {
+        if (reduce)
+            CFD_CHECK_NCCL(ncclAllReduce(w->maxc + it, w->maxc + it, 1, ncclFloat32, ncclMax, c->comm, st));
+        return CFD_OK;
+    };
+    // ghosts of the initial guess
+    if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
+    const int tk = timing_begin(s);
+    const bool fused = G == 2 && rbgs3d_fused_ok(phi, phi_tmp, div, mask, nx);
+    if (!fused) {
+        for (int it = 0; it < iterations; ++it) {
+            for (int colour = 0; colour < 2; ++colour) {
+                if ((rc = rbgs3d_colour_pass(colour, phi, div, mask, ny, nx, zb, ze, zoff, k, w, it, s)))
+                    return rc;
+                if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
+            }
+            if ((rc = allreduce(it, s))) return rc;
+        }
+        timing_end(tk, s, iterations);
+        return launch_rbgs_finish(w, phi, nullptr, plane * nzt, iters_done, s);
+    }
+    // owned faces the passes never write, in both buffers
+    const int full_lo = fixed_lo ? G : -1;
+    const int full_hi = fixed_hi ? nz_local + G - 1 : -1;
+    if ((rc = launch_fix_faces3d(phi, phi_tmp, nullptr, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
+        return rc;
+    const bool can_overlap = overlap && c->nranks > 1 && (ze - zb) >= 2 * G + 1;
+    float *a = phi, *b = phi_tmp;
+    for (int it = 0; it < iterations; ++it) {
+        auto run = [&](int z0, int z1) -> int {
+            if (z1 <= z0) return CFD_OK;
+            return rbgs3d_tb_pass(a, b, div, nzt, ny, nx, z0, z1, z0 == zb && fixed_lo,
+                                  z1 == ze && fixed_hi, zoff, k, it, w, s);
+        };
+        if (!can_overlap) {
+            if ((rc = run(zb, ze))) return rc;
+            if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
+            if ((rc = allreduce(it, s))) return rc;
+        } else {
+            int ib = zb, ie = ze;
+            if (lo_peer >= 0) {
+                if ((rc = run(zb, zb + G))) return rc;
+                ib = zb + G;
+            }
+            if (hi_peer >= 0) {
+                if ((rc = run(ze - G, ze))) return rc;
+                ie = ze - G;
+            }
+            CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
+            CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
+            if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, cs))) return rc;
+            if ((rc = run(ib, ie))) return rc;
+            if (reduce) {
+                // the global max needs the interior's contribution too
+                CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
+                CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
+                if ((rc = allreduce(it, cs))) return rc;
+            }
+            CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
+            CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
+        }
+        float *t = a;
+        a = b;
+        b = t;
+    }
+    timing_end(tk, s, iterations);
+    return launch_rbgs_finish(w, phi, phi_tmp, plane * nzt, iters_done, s);
+}
+
 }  // extern "C"

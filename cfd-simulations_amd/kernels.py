@@ -112,17 +112,21 @@ def compute_gradient_fast(phi, dx, dy):
 
 
 def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iterations, tolerance,
-                                     workspace=None, iters_done=None):
+                                     workspace=None, iters_done=None, phi_tmp=None):
     """v5.py:202-226: red-black GS, in place on ``phi``; returns ``phi``.
-    ``iters_done`` (optional int32 device scalar) receives the iteration count."""
+    ``iters_done`` (optional int32 device scalar) receives the iteration count.
+    ``phi_tmp`` (same-size scratch field, allocated if omitted) lets every
+    iteration run as one fused out-of-place pass; the result still lands in
+    ``phi``, bit-identical to the in-place colour passes."""
     ny, nx = _shape2d(phi)
     m = _mask_u8(mask, phi.shape)
     ws = workspace
     need = int(lib().cfd_rbgs_workspace_bytes(int(iterations)))
     if ws is None or ws.numel() * ws.element_size() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
+    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
     call("cfd_rbgs2d_f32", ptr(_f32(phi, "phi")), ptr(_f32(div_u_star, "div_u_star")), ptr(m), ny, nx,
-         float(dx), float(dy), float(np.float32(dt)), int(iterations), float(tolerance), None,
+         float(dx), float(dy), float(np.float32(dt)), int(iterations), float(tolerance), ptr(_f32(tmp, "phi_tmp")),
          ptr(ws), ptr(iters_done), stream_handle())
     return phi
 
@@ -160,17 +164,19 @@ def solve_pressure_jacobi3d(phi, div, h, dt, mask, iterations, phi_tmp=None, res
 
 
 def solve_pressure_gauss_seidel3d(phi, div, dx, dy, dz, dt, mask, iterations, tolerance,
-                                  workspace=None, iters_done=None):
-    """3-D red-black generalisation of v5.py:202-226, in place on ``phi``."""
+                                  workspace=None, iters_done=None, phi_tmp=None):
+    """3-D red-black generalisation of v5.py:202-226, in place on ``phi``
+    (``phi_tmp``: as in solve_pressure_gauss_seidel_fast)."""
     nz, ny, nx = (int(s) for s in phi.shape)
     m = _mask_u8(mask, phi.shape)
     need = int(lib().cfd_rbgs_workspace_bytes(int(iterations)))
     ws = workspace
     if ws is None or ws.numel() * ws.element_size() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
+    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
     call("cfd_rbgs3d_f32", ptr(_f32(phi, "phi")), ptr(_f32(div, "div")), ptr(m), nz, ny, nx, float(dx),
-         float(dy), float(dz), float(np.float32(dt)), int(iterations), float(tolerance), None, ptr(ws),
-         ptr(iters_done), stream_handle())
+         float(dy), float(dz), float(np.float32(dt)), int(iterations), float(tolerance), ptr(_f32(tmp, "phi_tmp")),
+         ptr(ws), ptr(iters_done), stream_handle())
     return phi
 
 

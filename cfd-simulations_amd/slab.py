@@ -197,6 +197,50 @@ class SlabJacobi3D:
         return self.phi[self.plan.owned()]
 
 
+class SlabRBGS3D:
+    """Distributed red-black GS (config 5) on this rank's slab: the 3-D
+    generalisation of solve_pressure_gauss_seidel_fast (v5.py:202-226) with
+    global colours and a global stop rule.  ``plan.ghost == 2`` (and no mask)
+    runs one fused pass per iteration; ghost 1 runs in-place colour passes."""
+
+    def __init__(self, plan: SlabPlan, ny: int, nx: int, dx: float, dy: float, dz: float, dt,
+                 comm: RcclComm | None, device=None, mask=None):
+        self.plan, self.ny, self.nx = plan, ny, nx
+        self.dx, self.dy, self.dz, self.dt = float(dx), float(dy), float(dz), np.float32(dt)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        shape = (plan.nz_total, ny, nx)
+        self.div = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        self.phi = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        self.tmp = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        self.mask = None if mask is None else mask.to(torch.uint8).contiguous()
+        self.iters_done = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.ws = None
+        self.comm = comm
+        self.comm_stream = torch.cuda.Stream(device=self.device)
+
+    @property
+    def z_global_offset(self) -> int:
+        return self.plan.z_lo - self.plan.ghost
+
+    def solve(self, iterations: int, tolerance: float = 1e-8, overlap: bool = True,
+              zero_phi: bool = True):
+        need = int(lib().cfd_rbgs_workspace_bytes(int(iterations)))
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if zero_phi:
+            self.phi.zero_()
+        p = self.plan
+        call("cfd_slab_rbgs3d_f32", self.comm.handle, ptr(self.div), ptr(self.phi), ptr(self.tmp),
+             ptr(self.mask), p.nz_local, p.ghost, self.ny, self.nx, p.lo_peer, p.hi_peer,
+             p.z_update_begin, p.z_update_end, self.z_global_offset, self.dx, self.dy, self.dz,
+             float(self.dt), int(iterations), float(tolerance), ptr(self.ws), ptr(self.iters_done),
+             int(bool(overlap)), stream_handle(), self.comm_stream.cuda_stream)
+        return self.phi
+
+    def owned(self) -> torch.Tensor:
+        return self.phi[self.plan.owned()]
+
+
 def sweep_range(phi_in, phi_out, div, mask, z_begin, z_end, h, dt, resid=None):
     """One Jacobi sweep of planes [z_begin, z_end) of a local (nz, ny, nx) array
     (cfd_jacobi3d_sweep_f32, the slab driver's building block)."""
@@ -206,4 +250,4 @@ def sweep_range(phi_in, phi_out, div, mask, z_begin, z_end, h, dt, resid=None):
          float(np.float32(dt)), ptr(resid), stream_handle())
 
 
-__all__ = ["SlabPlan", "RcclComm", "SlabJacobi3D", "sweep_range", "comm_unique_id", "lib"]
+__all__ = ["SlabPlan", "RcclComm", "SlabJacobi3D", "SlabRBGS3D", "sweep_range", "comm_unique_id", "lib"]

@@ -198,7 +198,7 @@ class OptimizedTurbulentSolver:
             K.solve_pressure_gauss_seidel_fast(self.phi, div_u_star, cfg.dx, cfg.dy, cfg.dt,
                                                self._mask_u8, cfg.pressure_iterations,
                                                cfg.pressure_tolerance, workspace=self._gs_ws,
-                                               iters_done=self._gs_done)
+                                               iters_done=self._gs_done, phi_tmp=self._phi_tmp)
         else:
             K.solve_pressure_jacobi(self.phi, div_u_star, cfg.dx, cfg.dt, self._mask_u8,
                                     cfg.pressure_iterations, phi_tmp=self._phi_tmp, rhs_ws=self._rhs_ws)

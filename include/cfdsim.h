@@ -88,7 +88,13 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
  * use_fast_pressure=True branch, v5.py:330-335): red-black Gauss-Seidel in
  * place on phi; colour 0 = cells with (i+j) odd first; masked cells skipped;
  * stop after the first iteration whose max|change| < tolerance.
- * phi_tmp: same-size scratch.  ws: cfd_rbgs_workspace_bytes(iterations) bytes.
+ * phi_tmp: same-size scratch (optional).  When given (and nx % 4 == 0, 16-byte
+ * aligned arrays, blocking not switched off), each iteration runs as ONE fused
+ * out-of-place pass over both colours (ping-pong phi/phi_tmp; the result
+ * still ends in phi, bit-identical); NULL = in-place colour passes.  3-D:
+ * fused only without a mask.  cfd_set_jacobi2d_blocking(1) /
+ * cfd_set_jacobi3d_blocking(1, ...) switch the fused path off.
+ * ws: cfd_rbgs_workspace_bytes(iterations) bytes.
  * iters_done (device int*, optional) receives the iteration count executed. */
 size_t cfd_rbgs_workspace_bytes(int iterations);
 int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, int nx,
@@ -198,6 +204,36 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
 int cfd_jacobi3d_sweep_f32(const float *in, float *out, const float *div, const uint8_t *mask,
                            int nz, int ny, int nx, int z_begin, int z_end, double h, float dt,
                            float *resid, void *stream);
+/* Distributed red-black GS (config 5), same plan arguments as
+ * cfd_slab_jacobi3d_f32 plus z_global_offset = global index of local plane 0
+ * (SlabPlan.z_lo - ghost): colours are global, so the result is bit-identical
+ * to cfd_rbgs3d_f32 on the whole grid.  ghost 2 + no mask + phi_tmp: one fused
+ * pass per iteration (boundary planes first, their exchange overlapped with
+ * the interior when overlap != 0); otherwise in-place colour passes with a
+ * ghost exchange after each colour.  The stop rule uses the global
+ * max|change| (ncclAllReduce(max) of one float per iteration; none when
+ * tolerance <= 0).  ws / iters_done as in cfd_rbgs3d_f32. */
+int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
+                        const uint8_t *mask, int nz_local, int ghost, int ny, int nx, int lo_peer,
+                        int hi_peer, int z_update_begin, int z_update_end, int z_global_offset,
+                        double dx, double dy, double dz, float dt, int iterations,
+                        double tolerance, void *ws, int *iters_done, int overlap, void *stream,
+                        void *comm_stream);
+/* Fused RB-GS building block (slab tests on one GPU): iteration `iteration`
+ * of planes [z_begin, z_end) of in -> out (both colours; local plane 0 =
+ * global plane z_global_offset).  fixed_lo/hi: plane z_begin-1 / z_end is a
+ * Dirichlet plane (else it is recomputed from the plane beyond it).  Skipped
+ * when ws's max|change| of iteration-1 < tolerance.  nx % 4 == 0, 16-byte
+ * aligned.  ws is prepared by cfd_rbgs_init and read out by cfd_rbgs_finish
+ * (phi <- phi_tmp when an odd number of iterations ran; phi_tmp may be NULL
+ * for in-place solves; n = elements). */
+int cfd_rbgs3d_pass_f32(const float *in, float *out, const float *div, int nz, int ny, int nx,
+                        int z_begin, int z_end, int fixed_lo, int fixed_hi, int z_global_offset,
+                        double dx, double dy, double dz, float dt, double tolerance, int iteration,
+                        void *ws, void *stream);
+int cfd_rbgs_init(void *ws, int iterations, int *iters_done, void *stream);
+int cfd_rbgs_finish(void *ws, float *phi, const float *phi_tmp, size_t n, int *iters_done,
+                    void *stream);
 
 /* ------------------------------------------------------------- tuning */
 /* Select the 3-D Jacobi kernel variant (bench / tile sweep):

@@ -214,9 +214,17 @@ def test_jacobi3d_variants_agree_at_1024():
 
 
 # ------------------------------------------------------------- red-black GS
+def _gs_fused(on):
+    """fused (one out-of-place pass per iteration) or in-place colour passes"""
+    call("cfd_set_jacobi2d_blocking", 0 if on else 1)
+    call("cfd_set_jacobi3d_blocking", 0 if on else 1, 0, 0)
+
+
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("name", ["rbgs2d_f32_64x64_it20_seed7", "rbgs2d_f32_64x64_it20_seed7_mask",
                                   "rbgs2d_f32_48x80_it15_aniso", "rbgs2d_f32_24x24_earlyexit"])
-def test_rbgs2d_golden_bitexact(golden, name):
+def test_rbgs2d_golden_bitexact(golden, name, fused):
+    _gs_fused(fused)
     d = golden(name + ".npz")
     phi = torch.zeros_like(dev(d["div"]))
     done = torch.zeros(1, dtype=torch.int32, device=DEV)
@@ -229,8 +237,10 @@ def test_rbgs2d_golden_bitexact(golden, name):
     assert n == int(d["iters_done"]) if "iters_done" in d else n == int(d["iters"])
 
 
-@pytest.mark.parametrize("shape", [(31, 45), (64, 128), (5, 4)])
-def test_rbgs2d_random_bitexact(shape):
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("shape", [(31, 45), (31, 44), (64, 128), (5, 4), (130, 520), (3, 8)])
+def test_rbgs2d_random_bitexact(shape, fused):
+    _gs_fused(fused)
     rng = np.random.default_rng(4)
     div = rng.standard_normal(shape).astype(np.float32)
     phi0 = rng.standard_normal(shape).astype(np.float32)
@@ -245,19 +255,91 @@ def test_rbgs2d_random_bitexact(shape):
     assert int(host(done)[0]) == n_ref
 
 
-@pytest.mark.parametrize("shape", [(9, 10, 12), (14, 17, 33)])
-def test_rbgs3d_random_bitexact(shape):
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("tol", [3e-5, 1.5e-5])  # stops after 17 / 62 iterations
+def test_rbgs2d_early_exit_both_parities(fused, tol):
+    """The stop iteration decides which ping-pong buffer holds the result
+    (decided on device by the finishing kernel)."""
+    _gs_fused(fused)
+    rng = np.random.default_rng(12)
+    div = rng.standard_normal((66, 132)).astype(np.float32) * np.float32(1e-3)
+    ref, n_ref = oracle.rbgs2d(div, np.zeros_like(div), dx=0.05, dy=0.05, dt=np.float32(1e-2), iters=400,
+                               tol=tol)
+    assert 1 < n_ref < 400
+    phi = torch.zeros_like(dev(div))
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.solve_pressure_gauss_seidel_fast(phi, dev(div), 0.05, 0.05, np.float32(1e-2), None, 400, tol,
+                                       iters_done=done)
+    assert int(host(done)[0]) == n_ref
+    assert np.array_equal(host(phi), ref)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("shape", [(9, 10, 12), (14, 17, 33), (14, 17, 32), (21, 30, 264), (3, 3, 4)])
+def test_rbgs3d_random_bitexact(shape, masked, fused):
+    _gs_fused(fused)
     rng = np.random.default_rng(6)
     div = rng.standard_normal(shape).astype(np.float32)
-    mask = rng.random(shape) < 0.1
+    mask = (rng.random(shape) < 0.1) if masked else None
     ref, n_ref = oracle.rbgs3d(div, dx=0.1, dy=0.12, dz=0.09, dt=np.float32(1e-2), iters=9, tol=1e-8,
                                mask=mask)
     phi = torch.zeros_like(dev(div))
     done = torch.zeros(1, dtype=torch.int32, device=DEV)
-    K.solve_pressure_gauss_seidel3d(phi, dev(div), 0.1, 0.12, 0.09, np.float32(1e-2), dev(mask), 9, 1e-8,
-                                    iters_done=done)
+    K.solve_pressure_gauss_seidel3d(phi, dev(div), 0.1, 0.12, 0.09, np.float32(1e-2),
+                                    None if mask is None else dev(mask), 9, 1e-8, iters_done=done)
     assert np.array_equal(host(phi), ref)
     assert int(host(done)[0]) == n_ref
+
+
+@pytest.mark.parametrize("rows,zchunk", [(5, 0), (13, 0), (13, 3), (5, 1)])
+@pytest.mark.parametrize("prefetch", [1, 2])
+def test_rbgs3d_fused_tiles_bitexact(rows, zchunk, prefetch):
+    """Tile shapes of the fused pass: 5/13 rows, 1..3 planes per march, both
+    prefetch depths; odd iteration count (result copied back from phi_tmp)."""
+    call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
+    call("cfd_set_jacobi3d_prefetch", prefetch)
+    rng = np.random.default_rng(8)
+    div = rng.standard_normal((19, 29, 264)).astype(np.float32)
+    ref, n_ref = oracle.rbgs3d(div, dx=0.1, dy=0.1, dz=0.1, dt=np.float32(1e-2), iters=7, tol=0.0)
+    phi = torch.zeros_like(dev(div))
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.solve_pressure_gauss_seidel3d(phi, dev(div), 0.1, 0.1, 0.1, np.float32(1e-2), None, 7, 0.0,
+                                    iters_done=done)
+    assert n_ref == 7 and int(host(done)[0]) == 7
+    assert np.array_equal(host(phi), ref)
+
+
+@pytest.mark.parametrize("tol", [2e-5, 1.5e-5])  # stops after 6 / 7 iterations
+def test_rbgs3d_early_exit_fused(tol):
+    rng = np.random.default_rng(13)
+    div = rng.standard_normal((24, 26, 40)).astype(np.float32) * np.float32(1e-3)
+    ref, n_ref = oracle.rbgs3d(div, dx=0.05, dy=0.05, dz=0.05, dt=np.float32(1e-2), iters=300, tol=tol)
+    assert 1 < n_ref < 300
+    phi = torch.zeros_like(dev(div))
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.solve_pressure_gauss_seidel3d(phi, dev(div), 0.05, 0.05, 0.05, np.float32(1e-2), None, 300, tol,
+                                    iters_done=done)
+    assert int(host(done)[0]) == n_ref
+    assert np.array_equal(host(phi), ref)
+
+
+def test_rbgs3d_fused_matches_colour_passes_at_512():
+    """Full-size property check (the oracle is too slow here): the fused pass
+    and the in-place colour passes agree bitwise, iteration count included."""
+    n = 512
+    g = torch.Generator(device=DEV).manual_seed(3)
+    div = torch.randn((n, n, n), device=DEV, generator=g)
+    outs = []
+    for fused in (False, True):
+        _gs_fused(fused)
+        phi = torch.zeros_like(div)
+        done = torch.zeros(1, dtype=torch.int32, device=DEV)
+        h = 1.0 / (n - 1)
+        K.solve_pressure_gauss_seidel3d(phi, div, h, h, h, np.float32(5e-5), None, 6, 0.0, iters_done=done)
+        outs.append((phi, int(host(done)[0])))
+    assert outs[0][1] == outs[1][1] == 6
+    assert torch.equal(outs[0][0], outs[1][0])
 
 
 # ------------------------------------------------------------- predictor & co
@@ -383,5 +465,76 @@ def test_slab_rccl_single_rank(overlap, ghost):
         sj.div.copy_(dev(plan.scatter(div)))
         sj.solve(iters, overlap=overlap)
         assert np.array_equal(host(sj.owned()), ref)
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("tol,iters", [(0.0, 7), (2e-5, 300)])
+def test_slab_rbgs_passes_emulated_on_one_gpu(tol, iters):
+    """The fused RB-GS slab pass (cfd_rbgs3d_pass_f32, global colour offset,
+    2-deep ghosts, recomputed inner-ghost colour 0) for 3 slabs on one GPU,
+    the per-iteration max combined across slabs like the ncclAllReduce:
+    bit-identical to the single-domain oracle, stop iteration included."""
+    nz, ny, nx, R = 23, 18, 36, 3
+    dx, dy, dz, dt = 0.05, 0.06, 0.07, np.float32(1e-2)
+    rng = np.random.default_rng(21)
+    div = rng.standard_normal((nz, ny, nx)).astype(np.float32) * np.float32(1e-3)
+    ref, n_ref = oracle.rbgs3d(div, dx=dx, dy=dy, dz=dz, dt=dt, iters=iters, tol=tol)
+    plans = [S.SlabPlan(nz, R, r, ghost=2) for r in range(R)]
+    A = [dev(p.scatter(np.zeros_like(div))) for p in plans]
+    B = [a.clone() for a in A]
+    D = [dev(p.scatter(div)) for p in plans]
+    need = int(lib().cfd_rbgs_workspace_bytes(iters))
+    W = [torch.zeros(need, dtype=torch.uint8, device=DEV) for _ in plans]
+    done = [torch.zeros(1, dtype=torch.int32, device=DEV) for _ in plans]
+    s = stream_handle()
+    for w, dn in zip(W, done):
+        call("cfd_rbgs_init", ptr(w), iters, ptr(dn), s)
+    for it in range(iters):
+        for p, a, b, d_, w in zip(plans, A, B, D, W):
+            call("cfd_rbgs3d_pass_f32", ptr(a), ptr(b), ptr(d_), p.nz_total, ny, nx, p.z_update_begin,
+                 p.z_update_end, int(p.z_lo == 0), int(p.z_hi == nz), p.z_lo - p.ghost, dx, dy, dz,
+                 float(dt), tol, it, ptr(w), s)
+        for p, b in zip(plans, B):
+            for first, count, peer, recv in p.exchanges():
+                B[peer][recv:recv + count].copy_(b[first:first + count])
+        # global max of iteration `it` (float32 maxc array at byte 16)
+        mx = [w[16:].view(torch.float32)[it:it + 1] for w in W]
+        g = torch.stack(mx).max(dim=0).values
+        for m in mx:
+            m.copy_(g)
+        A, B = B, A
+    n = []
+    for p, a, b, w, dn in zip(plans, A, B, W, done):
+        # A holds iteration `iters`; the buffer of iteration k alternates, so
+        # finish against the START buffer (B after an odd count of swaps)
+        start, other = (a, b) if iters % 2 == 0 else (b, a)
+        call("cfd_rbgs_finish", ptr(w), ptr(start), ptr(other), start.numel(), ptr(dn), s)
+        n.append(int(host(dn)[0]))
+        A[plans.index(p)] = start
+    assert n == [n_ref] * R
+    if tol > 0:
+        assert 1 < n_ref < iters
+    got = np.concatenate([host(a)[p.owned()] for p, a in zip(plans, A)])
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("ghost", [1, 2])
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("tol", [0.0, 2e-5])
+def test_slab_rbgs_rccl_single_rank(overlap, ghost, tol):
+    """cfd_slab_rbgs3d_f32 with a one-rank communicator equals the oracle."""
+    nz, ny, nx, iters = 30, 26, 40, 300 if tol > 0 else 9
+    rng = np.random.default_rng(11)
+    div = rng.standard_normal((nz, ny, nx)).astype(np.float32) * np.float32(1e-3)
+    ref, n_ref = oracle.rbgs3d(div, dx=0.05, dy=0.05, dz=0.05, dt=np.float32(1e-2), iters=iters, tol=tol)
+    comm = S.RcclComm(0, 1)
+    try:
+        plan = S.SlabPlan(nz, 1, 0, ghost=ghost)
+        sg = S.SlabRBGS3D(plan, ny, nx, 0.05, 0.05, 0.05, np.float32(1e-2), comm)
+        sg.div.copy_(dev(plan.scatter(div)))
+        sg.solve(iters, tolerance=tol, overlap=overlap)
+        assert int(host(sg.iters_done)[0]) == n_ref
+        assert np.array_equal(host(sg.owned()), ref)
     finally:
         comm.close()

@@ -106,6 +106,118 @@ def test_slab_decomposition_gloo_bitexact(tmp_path, world, nz, ghost, iters):
     assert np.array_equal(got, ref)
 
 
+def _colour_pass(phi, div, c, lo, hi, zoff, k):
+    """Red-black colour c over local planes [lo, hi) with GLOBAL parity
+    (zoff = global index of local plane 0), numpy float32: the cells of one
+    colour only read the other colour, so the vectorised pass equals the
+    serial one.  Returns (new phi, max|change|)."""
+    cx, cy, cz, cd, dt_inv = k
+    out = phi.copy()
+    if hi <= lo:
+        return out, np.float32(0)
+    z = np.arange(lo, hi)[:, None, None] + zoff
+    y = np.arange(1, phi.shape[1] - 1)[None, :, None]
+    x = np.arange(1, phi.shape[2] - 1)[None, None, :]
+    sel = ((z + y + x + 1 + c) % 2) == 0
+    C = phi[lo:hi, 1:-1, 1:-1]
+    rhs = -div[lo:hi, 1:-1, 1:-1] * dt_inv
+    a = cx * (phi[lo:hi, 1:-1, 2:] + phi[lo:hi, 1:-1, :-2])
+    b = cy * (phi[lo:hi, 2:, 1:-1] + phi[lo:hi, :-2, 1:-1])
+    e = cz * (phi[lo + 1:hi + 1, 1:-1, 1:-1] + phi[lo - 1:hi - 1, 1:-1, 1:-1])
+    new = (((a + b) + e) - rhs) * cd
+    out[lo:hi, 1:-1, 1:-1] = np.where(sel, new, C)
+    ch = np.abs(new - C)[sel]
+    return out, (ch.max() if ch.size else np.float32(0))
+
+
+def _rbgs_worker(rank, world, port, nz, ny, nx, iters, tol, ghost, out_dir):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root))
+    import _pkgpath
+    _pkgpath.load()
+    from cfd_simulations_amd.slab import SlabPlan as Plan
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dx, dy, dz, dt = 0.05, 0.06, 0.07, np.float32(1e-2)
+        # constants as cfd_rbgs3d_f32 / the oracle round them (v5.py:205-210)
+        i2 = (1.0 / dx ** 2, 1.0 / dy ** 2, 1.0 / dz ** 2)
+        k = tuple(np.float32(v) for v in i2) + (np.float32(1.0 / (2.0 * sum(i2))),
+                                                np.float32(1.0) / dt)
+        rng = np.random.default_rng(21)
+        div = rng.standard_normal((nz, ny, nx)).astype(np.float32) * np.float32(1e-3)
+        p = Plan(nz, world, rank, ghost)
+        dloc = p.scatter(div)
+        phi = np.zeros_like(dloc)
+        zb, ze, zoff = p.z_update_begin, p.z_update_end, p.z_lo - ghost
+        fixed_lo, fixed_hi = int(p.z_lo == 0), int(p.z_hi == nz)
+
+        def exchange(a):
+            reqs, bufs = [], []
+            for first, count, peer, _ in p.exchanges():
+                reqs.append(dist.isend(torch.from_numpy(a[first:first + count].copy()), dst=peer))
+            for first, count, peer in p.receives():
+                t = torch.empty((count, ny, nx), dtype=torch.float32)
+                reqs.append(dist.irecv(t, src=peer))
+                bufs.append((first, count, t))
+            for r in reqs:
+                r.wait()
+            for first, count, t in bufs:
+                a[first:first + count] = t.numpy()
+
+        done = iters
+        for it in range(iters):
+            if ghost == 2:
+                # the fused pass: colour 0 also on the inner ghost planes
+                # (recomputed, as cfd_rbgs3d_pass_f32 does), colour 1 on the
+                # owned planes, then one 2-plane exchange
+                l1, m0 = _colour_pass(phi, dloc, 0, zb - 1 + fixed_lo, ze + 1 - fixed_hi, zoff, k)
+                l1o, m0o = _colour_pass(phi, dloc, 0, zb, ze, zoff, k)  # owned part of the max
+                l2, m1 = _colour_pass(l1, dloc, 1, zb, ze, zoff, k)
+                phi = phi.copy()
+                phi[zb:ze] = l2[zb:ze]
+                exchange(phi)
+                m = max(m0o, m1)
+            else:
+                phi, m0 = _colour_pass(phi, dloc, 0, zb, ze, zoff, k)
+                exchange(phi)
+                phi, m1 = _colour_pass(phi, dloc, 1, zb, ze, zoff, k)
+                exchange(phi)
+                m = max(m0, m1)
+            t = torch.tensor([float(m)], dtype=torch.float32)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the per-iteration ncclAllReduce(max)
+            if t.item() < tol:
+                done = it + 1
+                break
+        np.save(os.path.join(out_dir, f"rank{rank}.npy"), phi[p.owned()])
+        np.save(os.path.join(out_dir, f"done{rank}.npy"), np.array([done]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nz,ghost,iters,tol", [(2, 17, 1, 6, 0.0), (3, 20, 2, 7, 0.0),
+                                                      (2, 18, 2, 300, 2e-5), (3, 19, 1, 300, 2e-5)])
+def test_slab_rbgs_gloo_bitexact(tmp_path, world, nz, ghost, iters, tol):
+    """Distributed red-black GS: global colours + a global max per iteration
+    reproduce the single-domain oracle bit-for-bit, stop iteration included."""
+    import oracle
+    ny, nx = 10, 12
+    mp.spawn(_rbgs_worker, args=(world, _free_port(), nz, ny, nx, iters, tol, ghost, str(tmp_path)),
+             nprocs=world, join=True)
+    got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
+    dones = {int(np.load(tmp_path / f"done{r}.npy")[0]) for r in range(world)}
+    rng = np.random.default_rng(21)
+    div = rng.standard_normal((nz, ny, nx)).astype(np.float32) * np.float32(1e-3)
+    ref, n_ref = oracle.rbgs3d(div, dx=0.05, dy=0.06, dz=0.07, dt=np.float32(1e-2), iters=iters, tol=tol)
+    assert dones == {n_ref}
+    if tol > 0:
+        assert 1 < n_ref < iters
+    assert np.array_equal(got, ref)
+
+
 @pytest.mark.parametrize("ghost", [1, 2])
 def test_slab_plan_partition(ghost):
     for nz in (7, 64, 1024):
