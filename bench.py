@@ -45,6 +45,8 @@ WORKLOADS = {
     # name: (shape, dtype, iters per step, bytes per cell-update)
     "jacobi3d_1024": ((1024, 1024, 1024), "f32", 200, 12),
     "jacobi3d_512": ((512, 512, 512), "f32", 200, 12),
+    # config 4: 1024 (x) x 1024 (y) x 512 (z) channel, z-slabs (64 planes per GPU at N=8)
+    "jacobi3d_channel": ((512, 1024, 1024), "f32", 200, 12),
     "jacobi2d_8192_f64": ((8192, 8192), "f64", 1000, 24),
     "rbgs3d_1024": ((1024, 1024, 1024), "f32", 200, 12),
 }

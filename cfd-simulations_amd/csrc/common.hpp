@@ -78,10 +78,28 @@ __device__ inline void atomic_max_nonneg(double *dst, double v) {
     atomicMax(reinterpret_cast<unsigned long long *>(dst),
               static_cast<unsigned long long>(__double_as_longlong(v)));
 }
+// The target only grows during a kernel, so a (possibly stale, never larger)
+// read that already covers m makes the atomic redundant: most waves skip it
+// and millions of waves do not serialise on one address.
 template <typename T>
 __device__ inline void wave_reduce_max_store(T local, T *dst) {
     T m = wave_max(local);
-    if ((threadIdx.x & (kWave - 1)) == 0 && m > T(0)) atomic_max_nonneg(dst, m);
+    if ((threadIdx.x & (kWave - 1)) == 0 && m > T(0) && m > *reinterpret_cast<volatile T *>(dst))
+        atomic_max_nonneg(dst, m);
+}
+// Workgroup-wide version: one atomic per workgroup.  Every thread of the
+// workgroup must call it (it synchronises); `red` is __shared__ scratch of
+// blockDim.x / 64 floats.
+__device__ inline void block_reduce_max_store(float local, float *dst, float *red) {
+    const float m = wave_max(local);
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    if (lane == 0) red[wv] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = red[0];
+        for (int k = 1; k < (int)(blockDim.x / kWave); ++k) b = fmaxf(b, red[k]);
+        if (b > 0.0f && b > *reinterpret_cast<volatile float *>(dst)) atomic_max_nonneg(dst, b);
+    }
 }
 
 // XCD-aware remap of a linear block id: blocks b and b+8 share an XCD (observed

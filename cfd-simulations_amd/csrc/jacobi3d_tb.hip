@@ -93,13 +93,8 @@ __device__ inline bool updates(int zg, int y, int x, int lev) {
 // level-0 rows (y0-2, y0+W+1), the 4-float x-halo chunks of all W+4 rows, and
 // the level-1 values of the two halo columns (x0-1, x0+256), one lane per
 // (row, side).  The row waves therefore run identical, branch-free code.
-#ifdef CFD_TB_WPE  // experiment: cap VGPRs for more resident waves per SIMD
-#define CFD_TB_ATTR __attribute__((amdgpu_waves_per_eu(CFD_TB_WPE)))
-#else
-#define CFD_TB_ATTR
-#endif
 template <int W, int MODE, bool PRE, int PD>
-__global__ __launch_bounds__((W + 3) * 64) CFD_TB_ATTR void jacobi3d_tb2(Tb2Args a) {
+__global__ __launch_bounds__((W + 3) * 64) void jacobi3d_tb2(Tb2Args a) {
     constexpr int G = W + 2;  // row waves
     constexpr int RS = 264;   // LDS row: 4 halo | 256 | 4 halo floats
     static_assert(2 * (W + 4) <= 64, "halo wave: one lane per (row, side)");
@@ -313,7 +308,10 @@ __global__ __launch_bounds__((W + 3) * 64) CFD_TB_ATTR void jacobi3d_tb2(Tb2Args
             if constexpr (PD == 2) { lon = lo2; hin = hi2; hpp = h3; rhn = rh2; }
         }
     }
-    if (MODE == MODE_RBGS) wave_reduce_max_store(rmax, a.maxc + a.it);
+    if (MODE == MODE_RBGS) {
+        __shared__ float red[W + 3];
+        block_reduce_max_store(rmax, a.maxc + a.it, red);
+    }
 }
 
 // Launch one fused pass of mode MODE over planes [zb, ze) of `out`.

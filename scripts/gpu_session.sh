@@ -37,13 +37,14 @@ for s in "$@"; do
     pmc_write_tb) step pmc_write_tb 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_tb -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
     prof_tb) step prof_tb 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_tb -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     slab1) step slab1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --force-slab --steps 3 --warmup 1 ;;
+    benchch) step benchch 600 python bench.py --workload jacobi3d_channel --no-cpu-baseline ;;
     testsgs) step pytest_gs 900 python -m pytest tests -m gpu -q -k "rbgs or slab" ;;
     benchgs) step benchgs 600 python bench.py --workload rbgs3d_1024 ;;
     benchgs_inplace) step benchgs_inplace 600 python bench.py --workload rbgs3d_1024 --tb 1 --no-cpu-baseline --steps 3 ;;
     slab1gs) step slab1gs 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29542 bench.py --gpus 1 --force-slab --workload rbgs3d_1024 --steps 3 --warmup 1 ;;
-    wpe8) step wpe8 600 env CFDSIM_LIB="$PWD/cfd-simulations_amd/libcfdsim_wpe8.so" python bench.py --no-cpu-baseline --steps 5 ;;
-    wpe8gs) step wpe8gs 600 env CFDSIM_LIB="$PWD/cfd-simulations_amd/libcfdsim_wpe8.so" python bench.py --workload rbgs3d_1024 --no-cpu-baseline --steps 5 ;;
     prof_gs) step prof_gs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_fetch_gs) step pmc_fetch_gs 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    pmc_write_gs) step pmc_write_gs 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
