@@ -63,7 +63,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="3-D kernel: 0 auto, 1 LDS, 2 cache")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--zchunk", type=int, default=0)
-    ap.add_argument("--tb", type=int, default=0, help="3-D sweeps fused per pass: 0 auto (2), 1 off, 2 on")
+    ap.add_argument("--tb", type=int, default=0,
+                    help="sweeps fused per HBM pass: 0 auto, 1 off, 2..4 (3-D), 2 (2-D)")
     ap.add_argument("--tb-rows", type=int, default=0)
     ap.add_argument("--tb-zchunk", type=int, default=0)
     ap.add_argument("--tb-prefetch", type=int, default=0, help="planes of prefetch in the blocked kernel")
@@ -168,7 +169,7 @@ def main():
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
     call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
     call("cfd_set_jacobi3d_prefetch", ARGS.tb_prefetch)
-    call("cfd_set_jacobi2d_blocking", ARGS.tb)
+    call("cfd_set_jacobi2d_blocking", min(ARGS.tb, 2))
     dt = np.float32(5e-5)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
@@ -204,7 +205,7 @@ def main():
     elif len(shape) == 3:
         nz, ny, nx = shape
         h = 1.0 / (nx - 1)
-        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else 2)
+        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else int(lib().cfd_get_jacobi3d_levels()))
         if not use_slab:
             div = torch.randn(shape, generator=g, device=dev, dtype=torch.float32)
             phi = torch.zeros_like(div)
@@ -285,9 +286,10 @@ def main():
     # (jacobi3d_tb2) performs 2 sweeps in one HBM pass: 12 B of algorithmic
     # traffic per cell per launch = 6 B per cell-update.
     blocked = ARGS.tb != 1 and (iters >= 2 or gs)
+    levels = int(lib().cfd_get_jacobi3d_levels()) if len(shape) == 3 else 2
     # sweeps per launch: 2 Jacobi sweeps per blocked pass; the GS timing
     # counts iterations, and a fused GS pass is one iteration (both colours)
-    spl = 2 if blocked and not gs else 1
+    spl = levels if blocked and not gs else 1
     launch_ms = sweep_ms * spl
     alg_bytes = cells_rank * bpc  # one pass moves bpc bytes per cell whatever it fuses
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
@@ -316,7 +318,8 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
                      "kernel": ("jacobi3d_tb2<MODE_RBGS>" if blocked else "rbgs3d_color x2") if gs
-                     else ("jacobi3d_tb2" if blocked else "jacobi3d_march") if len(shape) == 3
+                     else (("jacobi3d_tb2" if levels == 2 else f"jacobi3d_tbk<{levels}>") if blocked
+                           else "jacobi3d_march") if len(shape) == 3
                      else ("jacobi2d_tb2" if blocked else "jacobi2d_march"),
                      "sweeps_per_launch": spl, "bytes_per_cell_update": bpc / spl,
                      "cells_per_launch": cells_rank, "algorithmic_bytes_per_launch": alg_bytes,
@@ -332,7 +335,7 @@ def main():
     if verified is not None:
         out["config"]["multi_gpu_parity"] = (("bit-exact vs 1-GPU solve (96^3, 9 its + early stop, both ghost depths)"
                                               if gs else
-                                              "bit-exact vs 1-GPU solve (96^3, 7+8 sweeps, both ghost depths)")
+                                              "bit-exact vs 1-GPU solve (96^3, ghost depths 1-4)")
                                              if verified else "MISMATCH")
     if rank == 0 and world == 1 and not ARGS.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(shape, iters, gs)
@@ -353,7 +356,7 @@ def verify_slabs(S, K, dist, comm, world, rank, dev):
     g = torch.Generator(device=dev).manual_seed(99)
     div = torch.randn((nz, ny, nx), generator=g, device=dev, dtype=torch.float32)  # same on every rank
     ok = True
-    for ghost, iters in ((1, 7), (2, 8)):
+    for ghost, iters in ((1, 7), (2, 8), (3, 8), (4, 10)):
         plan = S.SlabPlan(nz, world, rank, ghost=ghost)
         sj = S.SlabJacobi3D(plan, ny, nx, 0.03, np.float32(1e-3), comm, device=dev)
         lo = plan.z_lo - ghost

@@ -13,10 +13,16 @@ int launch_rhs_f32(const float *div, float *rhs, size_t n, float h2, float dt, h
 int jacobi3d_tb_rows();      // configured rows per temporally blocked tile
 int jacobi3d_tb_zchunk();
 bool jacobi3d_tb_enabled();
+int jacobi3d_tb_levels();    // Jacobi sweeps per blocked pass (2..4)
+bool jacobi3d_tb_rows_explicit();  // rows set: 2-sweep passes use jacobi3d_tb2
 int jacobi3d_tb_prefetch();  // planes of prefetch in the blocked kernel (1 or 2)
 // jacobi3d_tb.hip
 int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, float h2, float dt, int W, int zchunk,
+                      bool pre, hipStream_t s);
+// jacobi3d_tbk.hip: K = 2..4 sweeps per pass
+int jacobi3d_tbk_pass(int K, const float *in, float *out, const float *div, int nz, int ny, int nx,
+                      int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt, int zchunk,
                       bool pre, hipStream_t s);
 // red-black GS workspace (cfd_rbgs_workspace_bytes): flags[1] = iterations
 // done (the fused kernels' stop counter), float maxc[iterations] at byte 16

@@ -64,18 +64,23 @@ struct J3Config {
     int variant = 0;  // 0 auto, 1 LDS, 2 cache
     int waves = 0;    // rows per workgroup (0 = auto)
     int zchunk = 0;   // planes per workgroup (0 = auto)
-    int tb_steps = 0; // sweeps fused per pass: 0 auto (2), 1 off, 2 on
+    int tb_steps = 0; // sweeps fused per pass: 0 auto, 1 off, 2..4
     int tb_rows = 0;  // output rows per temporally blocked tile (0 = auto)
     int tb_zchunk = 0;
     int tb_prefetch = 0;  // 0 auto (2), 1, 2
 };
 static J3Config g_j3;
+// Jacobi sweeps per pass when tb_steps == 0 (r01 sweep at 1024^3: K=2 855,
+// K=3 1010-1030, K=4 1000 Gcell/s)
+constexpr int kDefaultLevels = 3;
 
 // defaults from the r01 tile sweep (1024^3): 13 output rows per tile, prefetch
 // 1 plane ahead; planes per tile chosen by jacobi3d_tb2_pass (0 = auto)
 int jacobi3d_tb_rows() { return g_j3.tb_rows ? g_j3.tb_rows : 13; }
 int jacobi3d_tb_zchunk() { return g_j3.tb_zchunk; }
 bool jacobi3d_tb_enabled() { return g_j3.tb_steps != 1; }
+bool jacobi3d_tb_rows_explicit() { return g_j3.tb_rows != 0; }
+int jacobi3d_tb_levels() { return g_j3.tb_steps >= 2 ? g_j3.tb_steps : kDefaultLevels; }
 bool rbgs3d_fused_ok(const float *phi, const float *phi_tmp, const float *div, const uint8_t *mask,
                      int nx) {
     return phi_tmp && jacobi3d_tb_enabled() && !mask && nx % 4 == 0 && aligned16(phi) &&
@@ -452,7 +457,7 @@ int cfd_set_jacobi3d_prefetch(int planes) {
 }
 
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
-    CFD_REQUIRE(steps >= 0 && steps <= 2, "blocking steps must be 0 (auto), 1 or 2");
+    CFD_REQUIRE(steps >= 0 && steps <= 4, "blocking steps must be 0 (auto), 1 (off) or 2..4");
     CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13, "blocking rows must be 0, 5, 13");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
     g_j3.tb_steps = steps;
@@ -460,6 +465,8 @@ int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
     g_j3.tb_zchunk = zchunk;
     return CFD_OK;
 }
+
+int cfd_get_jacobi3d_levels(void) { return jacobi3d_tb_levels(); }
 
 int cfd_set_jacobi3d_config(int variant, int waves, int zchunk) {
     CFD_REQUIRE(variant >= 0 && variant <= 2, "variant must be 0..2");
@@ -508,19 +515,23 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
     const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(src);
     if (jacobi3d_tb_enabled() && !mask && resid_every <= 0 && vec_ok && nz >= 3 && ny >= 3 &&
         iters >= 2) {
-        // temporally blocked: one single sweep if iters is odd, then fused pairs
+        // temporally blocked: passes of K sweeps, the remainder last
+        const int K = jacobi3d_tb_levels();
         int done = 0;
         while (done < iters) {
-            const bool single = (iters - done) & 1;
-            if (single)
+            const int k = iters - done < K ? iters - done : K;
+            if (k == 1)
                 rc = jacobi3d_sweep(a, b, src, mask, nz, ny, nx, 1, nz - 1, h2, dt, pre, nullptr, s);
-            else
+            else if (k == 2 && jacobi3d_tb_rows_explicit())  // the tuned 2-level kernel
                 rc = jacobi3d_tb2_pass(a, b, src, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt,
                                        jacobi3d_tb_rows(), jacobi3d_tb_zchunk(), pre, s);
+            else
+                rc = jacobi3d_tbk_pass(k, a, b, src, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt,
+                                       jacobi3d_tb_zchunk(), pre, s);
             if (rc) return rc;
             if (done == 0 && (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, 0, nz, 0, nz - 1, s)))
                 return rc;
-            done += single ? 1 : 2;
+            done += k;
             float *t = a;
             a = b;
             b = t;

@@ -1,9 +1,11 @@
 // slab.hip -- multi-GPU slab decomposition of the 3-D Jacobi sweep.
 //
 // One process per GPU.  The (nz, ny, nx) grid is cut on z; each rank's local
-// array is (nz_local + 2, ny, nx) with one ghost plane per side.  After every
-// sweep the two owned boundary planes go to the z-neighbours with RCCL
-// send/recv (point-to-point over xGMI: one direct link per neighbour pair).
+// array is (nz_local + 2G, ny, nx) with G ghost planes per side (G = 1..4).
+// A pass performs up to G sweeps (the K-level blocked kernels recompute the
+// inner ghost planes' intermediate levels); after every pass the G owned
+// boundary planes per side go to the z-neighbours with RCCL send/recv
+// (point-to-point over xGMI: one direct link per neighbour pair).
 // With overlap on, the boundary planes are swept first, their exchange runs on
 // a second HIP stream, and the interior planes sweep concurrently on the main
 // stream; the main stream waits on the exchange before the next sweep.  The
@@ -115,7 +117,7 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
                           void *comm_stream) {
     SlabComm *c = reinterpret_cast<SlabComm *>(comm);
     CFD_REQUIRE(c && div && phi && phi_tmp, "slab_jacobi3d: null pointer");
-    CFD_REQUIRE(ghost == 1 || ghost == 2, "slab_jacobi3d: ghost depth must be 1 or 2");
+    CFD_REQUIRE(ghost >= 1 && ghost <= 4, "slab_jacobi3d: ghost depth must be 1..4");
     CFD_REQUIRE(nz_local >= ghost && ny >= 1 && nx >= 1 && iters >= 0, "slab_jacobi3d: bad shape");
     const int G = ghost;
     CFD_REQUIRE(z_update_begin >= G && z_update_end <= nz_local + G &&
@@ -147,8 +149,9 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
     if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
     const int zb = z_update_begin, ze = z_update_end;
     const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(src);
-    // two sweeps per pass needs 2-deep ghosts (and no mask)
-    const bool tb = G == 2 && jacobi3d_tb_enabled() && !mask && vec_ok && ny >= 3;
+    // k sweeps per pass need k-deep ghosts (and no mask): k = min(G, configured levels)
+    const bool tb = G >= 2 && jacobi3d_tb_enabled() && !mask && vec_ok && ny >= 3;
+    const int K = tb ? (jacobi3d_tb_levels() < G ? jacobi3d_tb_levels() : G) : 1;
     const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
     // owned planes a neighbour needs after each pass: the G next to it
     const bool lo_b = lo_peer >= 0, hi_b = hi_peer >= 0;
@@ -157,12 +160,15 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
     const int tk = timing_begin(s);
     int done = 0;
     while (done < iters) {
-        const bool pair = tb && (iters - done) >= 2 && !((iters - done) & 1);
+        const int k = iters - done < K ? iters - done : K;
         auto run = [&](int z0, int z1) -> int {
             if (z1 <= z0) return CFD_OK;
-            if (pair)
-                return jacobi3d_tb2_pass(a, b, src, nzt, ny, nx, z0, z1, z0 == zb && fixed_lo,
-                                         z1 == ze && fixed_hi, h2, dt, jacobi3d_tb_rows(),
+            const int flo = z0 == zb && fixed_lo, fhi = z1 == ze && fixed_hi;
+            if (k == 2 && jacobi3d_tb_rows_explicit())
+                return jacobi3d_tb2_pass(a, b, src, nzt, ny, nx, z0, z1, flo, fhi, h2, dt,
+                                         jacobi3d_tb_rows(), jacobi3d_tb_zchunk(), pre, s);
+            if (k >= 2)
+                return jacobi3d_tbk_pass(k, a, b, src, nzt, ny, nx, z0, z1, flo, fhi, h2, dt,
                                          jacobi3d_tb_zchunk(), pre, s);
             return jacobi3d_sweep(a, b, src, mask, nzt, ny, nx, z0, z1, h2, dt, pre, nullptr, s);
         };
@@ -192,7 +198,7 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
         if (done == 0 &&
             (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
             return rc;
-        done += pair ? 2 : 1;
+        done += k;
         float *t = a;
         a = b;
         b = t;

@@ -5,9 +5,9 @@ The reference runs on one node's CPU threads (SURVEY.md section 2,
 rank holds its owned planes plus one ghost plane per side.  After every sweep
 the ranks swap boundary planes with their z-neighbours over RCCL send/recv
 (xGMI), and that swap overlaps the interior sweep on a second HIP stream.
-With 2-deep ghosts the sweeps run temporally blocked: two sweeps per pass and
-one 2-plane exchange per pass, half as many messages at the same bytes per
-sweep.  Jacobi updates reassociate nothing across planes, so the decomposed
+With G-deep ghosts (G = 2..4) the sweeps run temporally blocked: G sweeps per
+pass and one G-plane exchange per pass, 1/G as many messages at the same bytes
+per sweep.  Jacobi updates reassociate nothing across planes, so the decomposed
 result is bit-identical to the single-GPU one for every rank count.
 
 ``SlabPlan`` is pure host logic: ownership, peers, update range and the
@@ -31,7 +31,7 @@ UNIQUE_ID_BYTES = 128
 @dataclass(frozen=True)
 class SlabPlan:
     """Ownership and halo plan of one rank.  Local arrays hold the owned
-    planes plus ``ghost`` planes per side (2 for temporally blocked passes):
+    planes plus ``ghost`` planes per side (1..4; G-sweep blocked passes need G):
     local index k <-> global plane z_lo - ghost + k."""
     nz: int        # global planes
     nranks: int
@@ -41,8 +41,8 @@ class SlabPlan:
     def __post_init__(self):
         if not (0 <= self.rank < self.nranks):
             raise ValueError("rank out of range")
-        if self.ghost not in (1, 2):
-            raise ValueError("ghost depth must be 1 or 2")
+        if self.ghost not in (1, 2, 3, 4):
+            raise ValueError("ghost depth must be 1..4")
         if self.nz < self.nranks * self.ghost:
             raise ValueError(f"cannot split {self.nz} planes over {self.nranks} ranks "
                              f"with {self.ghost}-deep ghosts")
@@ -166,8 +166,8 @@ class RcclComm:
 
 class SlabJacobi3D:
     """Distributed 7-point Jacobi on this rank's slab (device tensors).  With
-    ``plan.ghost == 2`` the sweeps run temporally blocked (two per pass, one
-    2-plane halo exchange per pass)."""
+    ``plan.ghost == G >= 2`` the sweeps run temporally blocked (up to G per
+    pass, one G-plane halo exchange per pass)."""
 
     def __init__(self, plan: SlabPlan, ny: int, nx: int, h: float, dt, comm: RcclComm | None,
                  device=None, mask=None, rhs_workspace: bool = True):

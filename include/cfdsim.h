@@ -183,7 +183,8 @@ int cfd_comm_unique_id(void *out, size_t bytes); /* bytes >= 128 */
 int cfd_comm_init(const void *unique_id, int nranks, int rank, void **comm);
 int cfd_comm_destroy(void *comm);
 /* Exchange plan, computed and tested on the host (SlabPlan in the package):
- * ghost = ghost planes per side (1, or 2 for temporally blocked passes):
+ * ghost = ghost planes per side, 1..4: a pass runs min(ghost, levels) sweeps
+ * (cfd_set_jacobi3d_blocking), so ghost >= 2 enables the blocked kernels:
  * local array (nz_local + 2*ghost, ny, nx), owned planes ghost ..
  * ghost+nz_local-1.  lo_peer / hi_peer: neighbour ranks or -1.
  * z_update_begin/end: local indices of the owned planes that are updated
@@ -241,10 +242,14 @@ int cfd_rbgs_finish(void *ws, float *phi, const float *phi_tmp, size_t n, int *i
  * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */
 int cfd_set_jacobi3d_config(int variant, int waves, int zchunk);
 /* Temporal blocking of the 3-D Jacobi solve (cfd_jacobi3d_f32 without mask
- * or residual): steps = sweeps fused per HBM pass (0 = auto = 2, 1 = off);
- * rows = output rows per tile (0 auto, 5, 13); zchunk = planes per tile.
- * Fused or not, results are bit-identical. */
+ * or residual): steps = sweeps fused per HBM pass (0 = auto, 1 = off, 2..4;
+ * a remainder of iters % steps runs as a shorter pass); rows = output rows
+ * per tile of the 2-sweep kernel (0 auto, 5, 13); zchunk = planes per tile.
+ * Fused or not, results are bit-identical.  The red-black GS solves use the
+ * 2-level kernel whenever blocking is not off. */
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk);
+/* Jacobi sweeps per blocked pass currently in effect (2..4). */
+int cfd_get_jacobi3d_levels(void);
 /* Prefetch distance of the blocked kernel in planes (0 = auto = 1, 1, 2). */
 int cfd_set_jacobi3d_prefetch(int planes);
 

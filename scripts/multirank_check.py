@@ -44,7 +44,7 @@ def main():
     comm = S.RcclComm(rank, world)
     ok = True
     try:
-        for ghost in (1, 2):
+        for ghost in (1, 2, 3, 4):
             for overlap in (False, True):
                 for iters in (6, 7):
                     plan = S.SlabPlan(nz, world, rank, ghost=ghost)

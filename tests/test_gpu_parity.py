@@ -169,6 +169,28 @@ def test_jacobi3d_temporal_blocking_bitexact(shape, iters, rows, zchunk, prefetc
     assert np.array_equal(host(phi), ref)
 
 
+@pytest.mark.parametrize("levels", [3, 4])
+@pytest.mark.parametrize("shape,iters", [((9, 10, 12), 7), ((21, 30, 264), 8), ((40, 31, 520), 12),
+                                         ((5, 4, 8), 4), ((13, 40, 16), 9)])
+@pytest.mark.parametrize("zchunk", [0, 1, 5])
+@pytest.mark.parametrize("prefetch", [1, 2])
+def test_jacobi3d_k_levels_bitexact(shape, iters, levels, zchunk, prefetch):
+    """K = 3 / 4 sweeps per HBM pass (jacobi3d_tbk): bit-identical to the
+    oracle for tile-edge shapes, several x-segments, z-chunks of 1..5 planes
+    (march start/end clipping) and remainders (iters % K)."""
+    call("cfd_set_jacobi3d_blocking", levels, 0, zchunk)
+    call("cfd_set_jacobi3d_prefetch", prefetch)
+    rng = np.random.default_rng(31)
+    div = rng.standard_normal(shape).astype(np.float32)
+    phi0 = rng.standard_normal(shape).astype(np.float32)
+    ref = oracle.jacobi3d(div, phi0, h=0.06, dt=np.float32(3e-3), iters=iters)
+    phi = dev(phi0)
+    for rhs in (None, torch.empty_like(phi)):
+        phi.copy_(dev(phi0))
+        K.solve_pressure_jacobi3d(phi, dev(div), 0.06, np.float32(3e-3), None, iters, rhs_ws=rhs)
+        assert np.array_equal(host(phi), ref)
+
+
 def test_jacobi3d_residual_matches_oracle():
     rng = np.random.default_rng(8)
     div = rng.standard_normal((18, 20, 64)).astype(np.float32)
@@ -202,15 +224,19 @@ def test_jacobi3d_variants_agree_at_1024():
     g = torch.Generator(device=DEV).manual_seed(7)
     div = torch.randn((n, n, n), generator=g, device=DEV, dtype=torch.float32)
     outs = []
-    for cfgv, tb in [((1, 4, 0), 1), ((2, 4, 0), 1), ((1, 8, 64), 1), ((2, 16, 0), 1), ((0, 0, 0), 2),
-                     ((0, 0, 0), (2, 13, 0)), ((0, 0, 0), (2, 5, 40))]:
+    for cfgv, tb, *pf in [((1, 4, 0), 1), ((2, 4, 0), 1), ((1, 8, 64), 1), ((2, 16, 0), 1), ((0, 0, 0), 2),
+                     ((0, 0, 0), (2, 13, 0)), ((0, 0, 0), (2, 5, 40)), ((0, 0, 0), 3),
+                     ((0, 0, 0), 4), ((0, 0, 0), (3, 0, 70)), ((0, 0, 0), (3, 0, 0), 2),
+                     ((0, 0, 0), (4, 0, 0), 2)]:
         call("cfd_set_jacobi3d_config", *cfgv)
         call("cfd_set_jacobi3d_blocking", *(tb if isinstance(tb, tuple) else (tb, 0, 0)))
+        call("cfd_set_jacobi3d_prefetch", pf[0] if pf else 0)
         phi = torch.zeros_like(div)
         K.solve_pressure_jacobi3d(phi, div, 1.0 / (n - 1), np.float32(5e-5), None, 30)
-        outs.append(phi)
-    for o in outs[1:]:
-        assert torch.equal(o, outs[0])
+        if outs:
+            assert torch.equal(phi, outs[0]), (cfgv, tb, pf)
+        else:
+            outs.append(phi)
 
 
 # ------------------------------------------------------------- red-black GS
@@ -450,7 +476,7 @@ def test_slab_sweeps_emulated_on_one_gpu():
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("ghost", [1, 2])
+@pytest.mark.parametrize("ghost", [1, 2, 3, 4])
 @pytest.mark.parametrize("overlap", [False, True])
 def test_slab_rccl_single_rank(overlap, ghost):
     """The RCCL slab driver with a one-rank communicator equals the plain solve."""

@@ -65,16 +65,17 @@ def _worker(rank, world, port, nz, ny, nx, iters, ghost, out_dir):
 
         done = 0
         while done < iters:
-            if ghost == 2 and (iters - done) % 2 == 0:
-                # the fused pass: level 1 on [zb-1, ze+1) (inner ghosts too,
-                # unless they are global Dirichlet planes), level 2 on [zb, ze)
-                l1 = sweep(phi, zb - 1 + fixed_lo, ze + 1 - fixed_hi)
-                new = phi.copy()
-                new[zb:ze] = sweep(l1, zb, ze)[zb:ze]
-                done += 2
-            else:
-                new = sweep(phi, zb, ze)
-                done += 1
+            # a fused pass of k = min(ghost, remaining) levels (as
+            # cfd_slab_jacobi3d_f32): level j on the owned range widened by
+            # k - j inner ghost planes (never past a global Dirichlet plane)
+            k = min(ghost, iters - done)
+            lev = phi
+            for j in range(1, k + 1):
+                w = k - j
+                lev = sweep(lev, zb if fixed_lo else zb - w, ze if fixed_hi else ze + w)
+            new = phi.copy()
+            new[zb:ze] = lev[zb:ze]
+            done += k
             reqs, bufs = [], []
             for first, count, peer, _ in p.exchanges():
                 reqs.append(dist.isend(torch.from_numpy(new[first:first + count].copy()), dst=peer))
@@ -93,7 +94,8 @@ def _worker(rank, world, port, nz, ny, nx, iters, ghost, out_dir):
 
 
 @pytest.mark.parametrize("world,nz,ghost,iters", [(2, 17, 1, 5), (3, 20, 1, 5), (2, 17, 2, 6),
-                                                  (3, 21, 2, 7), (3, 8, 2, 4)])
+                                                  (3, 21, 2, 7), (3, 8, 2, 4), (2, 19, 3, 8),
+                                                  (3, 22, 4, 9), (3, 12, 4, 6)])
 def test_slab_decomposition_gloo_bitexact(tmp_path, world, nz, ghost, iters):
     import oracle
     ny, nx = 9, 12
@@ -218,7 +220,7 @@ def test_slab_rbgs_gloo_bitexact(tmp_path, world, nz, ghost, iters, tol):
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("ghost", [1, 2])
+@pytest.mark.parametrize("ghost", [1, 2, 3, 4])
 def test_slab_plan_partition(ghost):
     for nz in (7, 64, 1024):
         for R in (1, 2, 3, 4, 8):
