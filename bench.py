@@ -318,7 +318,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
                      "kernel": ("jacobi3d_tb2<MODE_RBGS>" if blocked else "rbgs3d_color x2") if gs
-                     else (("jacobi3d_tb2" if levels == 2 else f"jacobi3d_tbk<{levels}>") if blocked
+                     else (blocked_kernel_name(levels, ARGS.tb_rows) if blocked
                            else "jacobi3d_march") if len(shape) == 3
                      else ("jacobi2d_tb2" if blocked else "jacobi2d_march"),
                      "sweeps_per_launch": spl, "bytes_per_cell_update": bpc / spl,
@@ -345,6 +345,17 @@ def main():
         comm.close()
     if use_slab:
         dist.destroy_process_group()
+
+
+def blocked_kernel_name(levels, rows):
+    """The kernel cfd_jacobi3d_f32 dispatches for (levels, rows) -- mirrors
+    jacobi3d_blocked_pass in poisson3d.hip."""
+    if levels == 2:
+        return "jacobi3d_tb2" if rows in (5, 13) else "jacobi3d_tbk<2>"
+    if (levels, rows) in ((3, 11), (4, 9)):
+        return f"jacobi3d_tbk<{levels}>"
+    shape = {(3, 17): "7x3", (4, 16): "11x2"}.get((levels, rows), "11x2" if levels == 3 else "7x3")
+    return f"jacobi3d_tbr<{levels}, {shape}>"
 
 
 def verify_slabs(S, K, dist, comm, world, rank, dev):

@@ -14,7 +14,10 @@ int jacobi3d_tb_rows();      // configured rows per temporally blocked tile
 int jacobi3d_tb_zchunk();
 bool jacobi3d_tb_enabled();
 int jacobi3d_tb_levels();    // Jacobi sweeps per blocked pass (2..4)
-bool jacobi3d_tb_rows_explicit();  // rows set: 2-sweep passes use jacobi3d_tb2
+// one pass of k = 1..4 sweeps, kernel and tile chosen from the blocking config
+int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, int nz, int ny,
+                          int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt,
+                          bool pre, hipStream_t s);
 int jacobi3d_tb_prefetch();  // planes of prefetch in the blocked kernel (1 or 2)
 // jacobi3d_tb.hip
 int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
@@ -24,6 +27,10 @@ int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int
 int jacobi3d_tbk_pass(int K, const float *in, float *out, const float *div, int nz, int ny, int nx,
                       int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt, int zchunk,
                       bool pre, hipStream_t s);
+// jacobi3d_tbr.hip: K = 3, 4 with several rows per wave (tall tiles)
+int jacobi3d_tbr_pass(int K, int shape, const float *in, float *out, const float *div, int nz,
+                      int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
+                      float dt, int zchunk, bool pre, hipStream_t s);
 // red-black GS workspace (cfd_rbgs_workspace_bytes): flags[1] = iterations
 // done (the fused kernels' stop counter), float maxc[iterations] at byte 16
 struct RbgsWs {

@@ -1,0 +1,368 @@
+// jacobi3d_tbr.hip -- K Jacobi sweeps per HBM pass with TALL tiles: several
+// rows per wave and single-buffered LDS level tiles (two barriers per step).
+//
+// jacobi3d_tbk (one row per wave, double-buffered tiles) is limited to 16
+// waves = W + 2K - 1, so a tile of W output rows re-reads 2K halo rows of its
+// neighbours (W = 11 rows for K = 3: 17 rows of phi and 15 of rhs are fetched
+// per 11 output rows, mostly from HBM).  Here a row wave owns RPW rows (its
+// register queues are RPW times as large; 8-12 waves per workgroup leave
+// 168-256 VGPRs per wave), and the level tiles are single-buffered so that
+// the taller tile still fits in LDS:
+//
+//    phase W: level 0 of plane z, and the level-l values computed in the
+//             previous step (plane z-l), into the tiles T_0 .. T_(K-1);
+//    barrier;
+//    phase R: level l of plane z-l+1 for l = 1..K, reading T_(l-1) (y) and
+//             the register queues (z); level K goes to HBM;
+//    barrier.
+//
+// Shapes (K, row waves, rows per wave) -> output rows W = NWR*RPW + 2 - 2K:
+// (3, 11, 2) W = 18; (4, 7, 3) W = 15; (3, 7, 3) W = 17.  Everything else --
+// the halo wave, the z-march bounds, Dirichlet copies, erosion of garbage --
+// is as in jacobi3d_tbk.hip, and the result is bit-identical to K single
+// sweeps (tests/test_gpu_parity.py).
+#include "internal.hpp"
+
+namespace cfd {
+
+namespace {
+
+__device__ inline float4 ldg4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ inline void stg4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+__device__ inline float4 lds4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+
+struct TbrArgs {
+    const float *in;
+    float *out;
+    const float *div;  // div, or the precomputed rhs (PRE)
+    int nz, ny, nx, nseg, ntile_y, zb, ze, zchunk, fixed_lo, fixed_hi;
+    float h2, dt;
+};
+
+template <bool PRE>
+__device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S, float4 U,
+                                float4 D, float4 d, int x, int nx, bool upd, float h2, float dt) {
+    if (!upd) return c;
+    const float cv[4] = {c.x, c.y, c.z, c.w};
+    const float nv[4] = {N.x, N.y, N.z, N.w};
+    const float sv[4] = {S.x, S.y, S.z, S.w};
+    const float uv[4] = {U.x, U.y, U.z, U.w};
+    const float dv[4] = {D.x, D.y, D.z, D.w};
+    const float rv[4] = {d.x, d.y, d.z, d.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float E = k < 3 ? cv[k + 1] : er;
+        const float Wv = k > 0 ? cv[k - 1] : wl;
+        float s = E + Wv;
+        s = s + nv[k];
+        s = s + sv[k];
+        s = s + uv[k];
+        s = s + dv[k];
+        const float rhs = PRE ? rv[k] : (h2 * rv[k]) / dt;
+        const int xk = x + k;
+        o[k] = (xk != 0 && xk != nx - 1) ? (1.0f / 6.0f) * (s - rhs) : cv[k];
+    }
+    return make_float4(o[0], o[1], o[2], o[3]);
+}
+
+}  // namespace
+
+// (A double-buffered, one-barrier-per-step version of the (3, 11, 2) shape --
+// 139 KB of LDS -- was measured at 1007 against 1131 Gcell/s for this one.)
+template <int K, int NWR, int RPW, bool PRE, int PD>
+__global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
+    constexpr int NR = NWR * RPW + 2;  // level-0 rows per tile
+    constexpr int W = NR - 2 * K;      // output rows
+    constexpr int RS = 264;            // LDS row: 4 halo | 256 | 4 halo floats
+    static_assert(K >= 2 && K <= 4 && W >= 1, "bad shape");
+    static_assert(2 * NR <= 64, "halo wave: one lane per (row, side)");
+    constexpr int TOTAL = [] {
+        int t = 0;
+        for (int l = 0; l < K; ++l) t += (NR - 2 * l) * RS;
+        return t;
+    }();
+    __shared__ __attribute__((aligned(16))) float smem[TOTAL];
+    // level l keeps rows [l, NR - l)
+    auto T = [&](int l, int r) -> float * {
+        int base = 0;
+#pragma unroll
+        for (int m = 0; m < K; ++m)
+            if (m < l) base += (NR - 2 * m) * RS;
+        return smem + base + (r - l) * RS;
+    };
+
+    const int nz = a.nz, ny = a.ny, nx = a.nx;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int t = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int seg = t % a.nseg;
+    const int ty = (t / a.nseg) % a.ntile_y;
+    const int zc = t / (a.nseg * a.ntile_y);
+    const int z0 = a.zb + zc * a.zchunk;
+    if (z0 >= a.ze) return;  // workgroup-uniform
+    const int z1 = min(z0 + a.zchunk, a.ze);
+    const int y0 = 1 + ty * W;
+    const int xs = seg * 256;
+    const int x = xs + 4 * lane;
+    const bool xin = x < nx;
+    const size_t plane = (size_t)ny * nx;
+    const int zs = z0 - K + 1;  // first front plane
+    const int zl = z1 + K - 2;  // last front plane
+    const float h2 = a.h2, dt = a.dt;
+    auto P = [&](int p) { return a.in + (size_t)p * plane; };
+    auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    if (wv < NWR) {
+        // ------------------------------------------------------------ row wave
+        int rr[RPW];
+        size_t ofs[RPW];
+        bool ld[RPW], irow[RPW], orow[RPW];
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            rr[j] = 1 + wv + j * NWR;
+            const int y = y0 - K + rr[j];
+            const bool rowin = y >= 0 && y <= ny - 1;
+            ld[j] = xin && rowin;
+            irow[j] = y >= 1 && y <= ny - 2;
+            orow[j] = rr[j] >= K && rr[j] < NR - K && y <= ny - 2 && xin;
+            ofs[j] = (size_t)(rowin ? y : 0) * nx + (xin ? x : 0);
+        }
+        auto ldp = [&](int j, int p) {
+            return (ld[j] && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ofs[j]) : z4;
+        };
+        auto ldr = [&](int j, int p) {
+            return (ld[j] && p >= 0 && p <= nz - 1) ? ldg4(a.div + (size_t)p * plane + ofs[j]) : z4;
+        };
+        float4 Q[RPW][K][3];  // Q[j][l][i] = level l of plane (z - l) - 1 + i, row j
+        float4 Rq[RPW][K];    // Rq[j][i] = rhs of plane z - i
+        float4 Cq[RPW][PD], Rn[RPW][PD];
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+#pragma unroll
+            for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = z4;
+            Q[j][0][0] = ldp(j, zs - 1);
+            Q[j][0][1] = ldp(j, zs);
+            Q[j][0][2] = ldp(j, zs + 1);
+#pragma unroll
+            for (int i = 0; i < K; ++i) Rq[j][i] = ldr(j, zs - i);
+#pragma unroll
+            for (int i = 0; i + 1 < PD; ++i) {
+                Cq[j][i] = ldp(j, zs + 2 + i);
+                Rn[j][i] = ldr(j, zs + 1 + i);
+            }
+        }
+        for (int z = zs; z <= zl; ++z) {
+#pragma unroll
+            for (int j = 0; j < RPW; ++j) {
+                Cq[j][PD - 1] = ldp(j, z + 1 + PD);
+                Rn[j][PD - 1] = ldr(j, z + PD);
+            }
+            // phase W
+#pragma unroll
+            for (int j = 0; j < RPW; ++j) {
+                if (ld[j]) sts4(T(0, rr[j]) + 4 + 4 * lane, Q[j][0][1]);
+#pragma unroll
+                for (int l = 1; l < K; ++l)
+                    if (xin && rr[j] >= l && rr[j] < NR - l) sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][2]);
+            }
+            __syncthreads();
+            // phase R
+#pragma unroll
+            for (int l = 1; l <= K; ++l) {
+                const int p = z - l + 1;
+                const bool fx = fixedp(p);
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) {
+                    const int r = rr[j];
+                    if (r >= l && r < NR - l) {
+                        const float4 c = Q[j][l - 1][1];
+                        float wl = __shfl_up(c.w, 1, 64);
+                        float er = __shfl_down(c.x, 1, 64);
+                        const float *row = T(l - 1, r);
+                        const float wl_l = row[3], er_l = row[260];
+                        if (lane == 0) wl = wl_l;
+                        if (lane == 63) er = er_l;
+                        float4 v = c;
+                        if (xin) {
+                            const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
+                            const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
+                            v = level4<PRE>(c, wl, er, N, S, Q[j][l - 1][2], Q[j][l - 1][0], Rq[j][l - 1],
+                                            x, nx, irow[j] && !fx, h2, dt);
+                        }
+                        if (l < K) {
+                            Q[j][l][0] = Q[j][l][1];
+                            Q[j][l][1] = Q[j][l][2];
+                            Q[j][l][2] = v;
+                        } else if (orow[j] && p >= z0 && p < z1) {
+                            stg4(a.out + (size_t)p * plane + ofs[j], v);
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < RPW; ++j) {
+                Q[j][0][0] = Q[j][0][1];
+                Q[j][0][1] = Q[j][0][2];
+                Q[j][0][2] = Cq[j][0];
+#pragma unroll
+                for (int i = K - 1; i > 0; --i) Rq[j][i] = Rq[j][i - 1];
+                Rq[j][0] = Rn[j][0];
+#pragma unroll
+                for (int i = 0; i + 1 < PD; ++i) {
+                    Cq[j][i] = Cq[j][i + 1];
+                    Rn[j][i] = Rn[j][i + 1];
+                }
+            }
+        }
+    } else {
+        // ------------------------------------------------------------ halo wave
+        const int ylo = y0 - K, yhi = y0 - K + NR - 1;
+        const bool elo = xin && ylo >= 0 && ylo <= ny - 1;
+        const bool ehi = xin && yhi >= 0 && yhi <= ny - 1;
+        const size_t olo = (size_t)(elo ? ylo : 0) * nx + (xin ? x : 0);
+        const size_t ohi = (size_t)(ehi ? yhi : 0) * nx + (xin ? x : 0);
+        const int hr = lane >> 1, side = lane & 1;
+        const int yr = y0 - K + hr;
+        const bool hact = lane < 2 * NR;
+        const bool hon = hact && yr >= 0 && yr <= ny - 1 && (side ? xs + 256 < nx : xs > 0);
+        const bool hint = hon && yr >= 1 && yr <= ny - 2;
+        const int hx = side ? xs + 256 : xs - 4;
+        const size_t hofs = (size_t)(hon ? yr : 0) * nx + (hon ? hx : 0);
+        const int col = side ? 260 : 0;
+        auto ldh = [&](const float *base, int p) {
+            return (hon && p >= 0 && p <= nz - 1) ? ldg4(base + (size_t)p * plane + hofs) : z4;
+        };
+        auto ldlo = [&](int p) { return (elo && p >= 0 && p <= nz - 1) ? ldg4(P(p) + olo) : z4; };
+        auto ldhi = [&](int p) { return (ehi && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ohi) : z4; };
+        float4 lo = ldlo(zs), hi = ldhi(zs);
+        float4 H[K][3];
+        float4 Hr[K];
+#pragma unroll
+        for (int l = 0; l < K; ++l) H[l][0] = H[l][1] = H[l][2] = z4;
+        H[0][0] = ldh(a.in, zs - 1);
+        H[0][1] = ldh(a.in, zs);
+        H[0][2] = ldh(a.in, zs + 1);
+#pragma unroll
+        for (int i = 0; i < K; ++i) Hr[i] = ldh(a.div, zs - i);
+        float4 Lq[PD], Uq[PD], Hq[PD], Rn[PD];
+#pragma unroll
+        for (int i = 0; i + 1 < PD; ++i) {
+            Lq[i] = ldlo(zs + 1 + i);
+            Uq[i] = ldhi(zs + 1 + i);
+            Hq[i] = ldh(a.in, zs + 2 + i);
+            Rn[i] = ldh(a.div, zs + 1 + i);
+        }
+        for (int z = zs; z <= zl; ++z) {
+            Lq[PD - 1] = ldlo(z + PD);
+            Uq[PD - 1] = ldhi(z + PD);
+            Hq[PD - 1] = ldh(a.in, z + 1 + PD);
+            Rn[PD - 1] = ldh(a.div, z + PD);
+            // phase W
+            if (elo) sts4(T(0, 0) + 4 + 4 * lane, lo);
+            if (ehi) sts4(T(0, NR - 1) + 4 + 4 * lane, hi);
+            if (hon) {
+                sts4(T(0, hr) + col, H[0][1]);
+#pragma unroll
+                for (int l = 1; l < K; ++l)
+                    if (hr >= l && hr < NR - l) sts4(T(l, hr) + col, H[l][2]);
+            }
+            __syncthreads();
+            // phase R: levels 1..K-1 of the halo chunks
+#pragma unroll
+            for (int l = 1; l < K; ++l) {
+                const int p = z - l + 1;
+                if (hact && hr >= l && hr < NR - l) {
+                    const float4 c = H[l - 1][1];
+                    const float inner = T(l - 1, hr)[side ? 259 : 4];
+                    float4 v = c;
+                    if (hon) {
+                        const float4 N = lds4(T(l - 1, hr + 1) + col);
+                        const float4 S = lds4(T(l - 1, hr - 1) + col);
+                        v = level4<PRE>(c, side ? inner : 0.f, side ? 0.f : inner, N, S, H[l - 1][2],
+                                        H[l - 1][0], Hr[l - 1], hx, nx, hint && !fixedp(p), h2, dt);
+                    }
+                    H[l][0] = H[l][1];
+                    H[l][1] = H[l][2];
+                    H[l][2] = v;
+                }
+            }
+            __syncthreads();
+            lo = Lq[0];
+            hi = Uq[0];
+            H[0][0] = H[0][1];
+            H[0][1] = H[0][2];
+            H[0][2] = Hq[0];
+#pragma unroll
+            for (int i = K - 1; i > 0; --i) Hr[i] = Hr[i - 1];
+            Hr[0] = Rn[0];
+#pragma unroll
+            for (int i = 0; i + 1 < PD; ++i) {
+                Lq[i] = Lq[i + 1];
+                Uq[i] = Uq[i + 1];
+                Hq[i] = Hq[i + 1];
+                Rn[i] = Rn[i + 1];
+            }
+        }
+    }
+}
+
+// Output rows per tile of the tall-tile shape for K levels.
+int jacobi3d_tbr_pass(int K, int shape, const float *in, float *out, const float *div, int nz,
+                      int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
+                      float dt, int zchunk, bool pre, hipStream_t s) {
+    if (ze <= zb || ny < 3) return CFD_OK;
+    TbrArgs a{};
+    a.in = in; a.out = out; a.div = div;
+    a.nz = nz; a.ny = ny; a.nx = nx; a.zb = zb; a.ze = ze;
+    a.fixed_lo = fixed_lo; a.fixed_hi = fixed_hi; a.h2 = h2; a.dt = dt;
+    const int pd = jacobi3d_tb_prefetch();
+    // shapes: 0 = (K=3: 11 row waves x 2 rows | K=4: 7 x 3), 1 = (K=3: 7 x 3 | K=4: 11 x 2)
+    int nwr, rpw;
+    if (K == 3 && shape == 1) { nwr = 7; rpw = 3; }
+    else if (K == 3) { nwr = 11; rpw = 2; }
+    else if (K == 4 && shape == 1) { nwr = 11; rpw = 2; }
+    else if (K == 4) { nwr = 7; rpw = 3; }
+    else {
+        set_error("jacobi3d_tbr: unsupported levels per pass %d (3, 4)", K);
+        return CFD_E_INVALID;
+    }
+    const int W = nwr * rpw + 2 - 2 * K;
+    a.nseg = ceil_div(nx, 256);
+    a.ntile_y = ceil_div(ny - 2, W);
+    const int L = ze - zb;
+    if (zchunk <= 0) {
+        const long tiles = (long)a.nseg * a.ntile_y;
+        int nzc = (int)((1024 + tiles - 1) / tiles);
+        if (nzc < 1) nzc = 1;
+        zchunk = ceil_div(L, nzc);
+        if (zchunk > 256) zchunk = 256;
+        if (zchunk < 16) zchunk = 16;
+    }
+    if (zchunk > L) zchunk = L;
+    a.zchunk = zchunk;
+    const int blocks = a.nseg * a.ntile_y * ceil_div(L, zchunk);
+#define CFD_TBR_L(KV, NW, RP, PR, PDV) \
+    hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, PR, PDV>), dim3(blocks), dim3((NW + 1) * 64), 0, s, a)
+#define CFD_TBR(KV, NW, RP)                                                              \
+    do {                                                                                 \
+        if (pd == 2) {                                                                   \
+            if (pre) CFD_TBR_L(KV, NW, RP, true, 2); else CFD_TBR_L(KV, NW, RP, false, 2); \
+        } else {                                                                         \
+            if (pre) CFD_TBR_L(KV, NW, RP, true, 1); else CFD_TBR_L(KV, NW, RP, false, 1); \
+        }                                                                                \
+    } while (0)
+    if (K == 3 && rpw == 2) CFD_TBR(3, 11, 2);
+    else if (K == 3) CFD_TBR(3, 7, 3);
+    else if (rpw == 2) CFD_TBR(4, 11, 2);
+    else CFD_TBR(4, 7, 3);
+#undef CFD_TBR
+#undef CFD_TBR_L
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+}  // namespace cfd

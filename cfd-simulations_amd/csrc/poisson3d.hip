@@ -79,7 +79,6 @@ constexpr int kDefaultLevels = 3;
 int jacobi3d_tb_rows() { return g_j3.tb_rows ? g_j3.tb_rows : 13; }
 int jacobi3d_tb_zchunk() { return g_j3.tb_zchunk; }
 bool jacobi3d_tb_enabled() { return g_j3.tb_steps != 1; }
-bool jacobi3d_tb_rows_explicit() { return g_j3.tb_rows != 0; }
 int jacobi3d_tb_levels() { return g_j3.tb_steps >= 2 ? g_j3.tb_steps : kDefaultLevels; }
 bool rbgs3d_fused_ok(const float *phi, const float *phi_tmp, const float *div, const uint8_t *mask,
                      int nx) {
@@ -444,6 +443,31 @@ RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double toler
     return k;
 }
 
+// One pass of k Jacobi sweeps over planes [zb, ze) (k = 1..4), with the tile
+// shape cfd_set_jacobi3d_blocking selected: rows 5 / 13 -> jacobi3d_tb2 for
+// k = 2; rows 11 (k = 3) / 9 (k = 4) -> jacobi3d_tbk; otherwise the tall-tile
+// jacobi3d_tbr for k >= 3 (17 or 18 rows for k = 3, 15 for k = 4) and
+// jacobi3d_tbk for k = 2.
+int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, int nz, int ny,
+                          int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt,
+                          bool pre, hipStream_t s) {
+    const int rows = g_j3.tb_rows, zc = g_j3.tb_zchunk;
+    if (k == 1) return jacobi3d_sweep(in, out, src, nullptr, nz, ny, nx, zb, ze, h2, dt, pre, nullptr, s);
+    if (k == 2) {
+        if (rows == 5 || rows == 13)
+            return jacobi3d_tb2_pass(in, out, src, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, h2, dt, rows,
+                                     zc, pre, s);
+        return jacobi3d_tbk_pass(2, in, out, src, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, h2, dt, zc,
+                                 pre, s);
+    }
+    if ((k == 3 && rows == 11) || (k == 4 && rows == 9))
+        return jacobi3d_tbk_pass(k, in, out, src, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, h2, dt, zc,
+                                 pre, s);
+    return jacobi3d_tbr_pass(k, (k == 3 && rows == 17) || (k == 4 && rows == 16) ? 1 : 0, in, out, src,
+                             nz, ny, nx, zb, ze,
+                             fixed_lo, fixed_hi, h2, dt, zc, pre, s);
+}
+
 }  // namespace cfd
 
 using namespace cfd;
@@ -458,7 +482,9 @@ int cfd_set_jacobi3d_prefetch(int planes) {
 
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
     CFD_REQUIRE(steps >= 0 && steps <= 4, "blocking steps must be 0 (auto), 1 (off) or 2..4");
-    CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13, "blocking rows must be 0, 5, 13");
+    CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13 || rows == 9 || rows == 11 || rows == 15 ||
+                    rows == 16 || rows == 17 || rows == 18,
+                "blocking rows must be 0 (auto), 5, 13 (2 levels), 11, 17, 18 (3), 9, 15, 16 (4)");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
     g_j3.tb_steps = steps;
     g_j3.tb_rows = rows;
@@ -520,14 +546,7 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
         int done = 0;
         while (done < iters) {
             const int k = iters - done < K ? iters - done : K;
-            if (k == 1)
-                rc = jacobi3d_sweep(a, b, src, mask, nz, ny, nx, 1, nz - 1, h2, dt, pre, nullptr, s);
-            else if (k == 2 && jacobi3d_tb_rows_explicit())  // the tuned 2-level kernel
-                rc = jacobi3d_tb2_pass(a, b, src, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt,
-                                       jacobi3d_tb_rows(), jacobi3d_tb_zchunk(), pre, s);
-            else
-                rc = jacobi3d_tbk_pass(k, a, b, src, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt,
-                                       jacobi3d_tb_zchunk(), pre, s);
+            rc = jacobi3d_blocked_pass(k, a, b, src, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt, pre, s);
             if (rc) return rc;
             if (done == 0 && (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, 0, nz, 0, nz - 1, s)))
                 return rc;

@@ -163,14 +163,10 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
         const int k = iters - done < K ? iters - done : K;
         auto run = [&](int z0, int z1) -> int {
             if (z1 <= z0) return CFD_OK;
-            const int flo = z0 == zb && fixed_lo, fhi = z1 == ze && fixed_hi;
-            if (k == 2 && jacobi3d_tb_rows_explicit())
-                return jacobi3d_tb2_pass(a, b, src, nzt, ny, nx, z0, z1, flo, fhi, h2, dt,
-                                         jacobi3d_tb_rows(), jacobi3d_tb_zchunk(), pre, s);
-            if (k >= 2)
-                return jacobi3d_tbk_pass(k, a, b, src, nzt, ny, nx, z0, z1, flo, fhi, h2, dt,
-                                         jacobi3d_tb_zchunk(), pre, s);
-            return jacobi3d_sweep(a, b, src, mask, nzt, ny, nx, z0, z1, h2, dt, pre, nullptr, s);
+            if (k == 1)
+                return jacobi3d_sweep(a, b, src, mask, nzt, ny, nx, z0, z1, h2, dt, pre, nullptr, s);
+            return jacobi3d_blocked_pass(k, a, b, src, nzt, ny, nx, z0, z1, z0 == zb && fixed_lo,
+                                         z1 == ze && fixed_hi, h2, dt, pre, s);
         };
         if (!can_overlap) {
             if ((rc = run(zb, ze))) return rc;

@@ -169,16 +169,17 @@ def test_jacobi3d_temporal_blocking_bitexact(shape, iters, rows, zchunk, prefetc
     assert np.array_equal(host(phi), ref)
 
 
-@pytest.mark.parametrize("levels", [3, 4])
+@pytest.mark.parametrize("levels,rows", [(3, 11), (3, 17), (3, 18), (4, 9), (4, 15), (4, 16), (2, 0)])
 @pytest.mark.parametrize("shape,iters", [((9, 10, 12), 7), ((21, 30, 264), 8), ((40, 31, 520), 12),
-                                         ((5, 4, 8), 4), ((13, 40, 16), 9)])
+                                         ((5, 4, 8), 4), ((13, 40, 16), 9), ((12, 47, 264), 8)])
 @pytest.mark.parametrize("zchunk", [0, 1, 5])
 @pytest.mark.parametrize("prefetch", [1, 2])
-def test_jacobi3d_k_levels_bitexact(shape, iters, levels, zchunk, prefetch):
-    """K = 3 / 4 sweeps per HBM pass (jacobi3d_tbk): bit-identical to the
-    oracle for tile-edge shapes, several x-segments, z-chunks of 1..5 planes
-    (march start/end clipping) and remainders (iters % K)."""
-    call("cfd_set_jacobi3d_blocking", levels, 0, zchunk)
+def test_jacobi3d_k_levels_bitexact(shape, iters, levels, rows, zchunk, prefetch):
+    """K = 2..4 sweeps per HBM pass (jacobi3d_tbk: one row per wave;
+    jacobi3d_tbr: tall tiles, several rows per wave): bit-identical to the
+    oracle for tile-edge shapes, several x-segments and y-tiles, z-chunks of
+    1..5 planes (march start/end clipping) and remainders (iters % K)."""
+    call("cfd_set_jacobi3d_blocking", levels, rows, zchunk)
     call("cfd_set_jacobi3d_prefetch", prefetch)
     rng = np.random.default_rng(31)
     div = rng.standard_normal(shape).astype(np.float32)
@@ -227,7 +228,8 @@ def test_jacobi3d_variants_agree_at_1024():
     for cfgv, tb, *pf in [((1, 4, 0), 1), ((2, 4, 0), 1), ((1, 8, 64), 1), ((2, 16, 0), 1), ((0, 0, 0), 2),
                      ((0, 0, 0), (2, 13, 0)), ((0, 0, 0), (2, 5, 40)), ((0, 0, 0), 3),
                      ((0, 0, 0), 4), ((0, 0, 0), (3, 0, 70)), ((0, 0, 0), (3, 0, 0), 2),
-                     ((0, 0, 0), (4, 0, 0), 2)]:
+                     ((0, 0, 0), (4, 0, 0), 2), ((0, 0, 0), (3, 11, 0)), ((0, 0, 0), (3, 17, 0)),
+                     ((0, 0, 0), (4, 9, 0)), ((0, 0, 0), (4, 15, 0), 1)]:
         call("cfd_set_jacobi3d_config", *cfgv)
         call("cfd_set_jacobi3d_blocking", *(tb if isinstance(tb, tuple) else (tb, 0, 0)))
         call("cfd_set_jacobi3d_prefetch", pf[0] if pf else 0)
