@@ -28,7 +28,7 @@ int jacobi3d_tbk_pass(int K, const float *in, float *out, const float *div, int 
                       int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt, int zchunk,
                       bool pre, hipStream_t s);
 // jacobi3d_tbr.hip: K = 3, 4 with several rows per wave (tall tiles)
-int jacobi3d_tbr_pass(int K, int shape, const float *in, float *out, const float *div, int nz,
+int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float *div, int nz,
                       int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
                       float dt, int zchunk, bool pre, hipStream_t s);
 // red-black GS workspace (cfd_rbgs_workspace_bytes): flags[1] = iterations

@@ -311,7 +311,36 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
 }
 
 // Output rows per tile of the tall-tile shape for K levels.
-int jacobi3d_tbr_pass(int K, int shape, const float *in, float *out, const float *div, int nz,
+namespace {
+struct TbrShape {
+    int K, nwr, rpw;
+    bool autopick;  // candidate for rows == 0
+    int rows() const { return nwr * rpw + 2 - 2 * K; }
+};
+// (4, 11, 2) spills 9 VGPRs at 168 and runs slower than (4, 7, 3): explicit only
+constexpr TbrShape kShapes[] = {{3, 11, 2, true}, {3, 10, 2, true}, {3, 7, 3, false},
+                                {4, 7, 3, true}, {4, 11, 2, false}};
+
+int num_cus() {
+    static int n = 0;
+    if (n <= 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+}  // namespace
+
+// rows = output rows per tile (0: pick the shape and z-chunk by a cost model).
+// One workgroup fills a CU (LDS / VGPRs), so workgroups run in rounds of
+// #CUs.  Model: rounds x (steps per workgroup + ~8 steps of pipeline fill) x
+// rows loaded per step (a saturated chip gives each CU an equal byte rate).
+// Calibrated on 1024^3, K = 3: 16-row tiles in one round of 256 workgroups
+// (2.48 ms per pass) beat 18-row tiles in 9 rounds of 103 planes (2.62 ms)
+// and in 5 rounds of 205 planes (2.79 ms); the model orders them the same.
+int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float *div, int nz,
                       int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
                       float dt, int zchunk, bool pre, hipStream_t s) {
     if (ze <= zb || ny < 3) return CFD_OK;
@@ -320,31 +349,39 @@ int jacobi3d_tbr_pass(int K, int shape, const float *in, float *out, const float
     a.nz = nz; a.ny = ny; a.nx = nx; a.zb = zb; a.ze = ze;
     a.fixed_lo = fixed_lo; a.fixed_hi = fixed_hi; a.h2 = h2; a.dt = dt;
     const int pd = jacobi3d_tb_prefetch();
-    // shapes: 0 = (K=3: 11 row waves x 2 rows | K=4: 7 x 3), 1 = (K=3: 7 x 3 | K=4: 11 x 2)
-    int nwr, rpw;
-    if (K == 3 && shape == 1) { nwr = 7; rpw = 3; }
-    else if (K == 3) { nwr = 11; rpw = 2; }
-    else if (K == 4 && shape == 1) { nwr = 11; rpw = 2; }
-    else if (K == 4) { nwr = 7; rpw = 3; }
-    else {
-        set_error("jacobi3d_tbr: unsupported levels per pass %d (3, 4)", K);
+    const int L = ze - zb;
+    const int nseg = ceil_div(nx, 256);
+    const int ncu = num_cus();
+    const TbrShape *best = nullptr;
+    int best_zlen = 0;
+    double best_cost = 0.0;
+    for (const TbrShape &sh : kShapes) {
+        if (sh.K != K || (rows ? sh.rows() != rows : !sh.autopick)) continue;
+        const int W = sh.rows(), NR = W + 2 * K;
+        const long tiles = (long)nseg * ceil_div(ny - 2, W);
+        for (int nzc = 1; nzc <= 64; ++nzc) {
+            int zlen = zchunk > 0 ? zchunk : ceil_div(L, nzc);
+            if (zlen > L) zlen = L;
+            if (zchunk <= 0 && zlen < 8 && L >= 8) break;
+            const long wgs = tiles * ceil_div(L, zlen);
+            const double cost = (double)ceil_div(wgs, ncu) * (zlen + 2 * K - 2 + 8) * NR;
+            if (!best || cost < best_cost) {
+                best = &sh;
+                best_cost = cost;
+                best_zlen = zlen;
+            }
+            if (zchunk > 0) break;
+        }
+    }
+    if (!best) {
+        set_error("jacobi3d_tbr: no tile shape with %d rows for %d levels per pass", rows, K);
         return CFD_E_INVALID;
     }
-    const int W = nwr * rpw + 2 - 2 * K;
-    a.nseg = ceil_div(nx, 256);
+    const int W = best->rows();
+    a.nseg = nseg;
     a.ntile_y = ceil_div(ny - 2, W);
-    const int L = ze - zb;
-    if (zchunk <= 0) {
-        const long tiles = (long)a.nseg * a.ntile_y;
-        int nzc = (int)((1024 + tiles - 1) / tiles);
-        if (nzc < 1) nzc = 1;
-        zchunk = ceil_div(L, nzc);
-        if (zchunk > 256) zchunk = 256;
-        if (zchunk < 16) zchunk = 16;
-    }
-    if (zchunk > L) zchunk = L;
-    a.zchunk = zchunk;
-    const int blocks = a.nseg * a.ntile_y * ceil_div(L, zchunk);
+    a.zchunk = best_zlen;
+    const int blocks = a.nseg * a.ntile_y * ceil_div(L, best_zlen);
 #define CFD_TBR_L(KV, NW, RP, PR, PDV) \
     hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, PR, PDV>), dim3(blocks), dim3((NW + 1) * 64), 0, s, a)
 #define CFD_TBR(KV, NW, RP)                                                              \
@@ -355,10 +392,14 @@ int jacobi3d_tbr_pass(int K, int shape, const float *in, float *out, const float
             if (pre) CFD_TBR_L(KV, NW, RP, true, 1); else CFD_TBR_L(KV, NW, RP, false, 1); \
         }                                                                                \
     } while (0)
-    if (K == 3 && rpw == 2) CFD_TBR(3, 11, 2);
-    else if (K == 3) CFD_TBR(3, 7, 3);
-    else if (rpw == 2) CFD_TBR(4, 11, 2);
-    else CFD_TBR(4, 7, 3);
+    const int code = best->K * 100 + best->nwr * 10 + best->rpw;
+    switch (code) {
+        case 3 * 100 + 11 * 10 + 2: CFD_TBR(3, 11, 2); break;
+        case 3 * 100 + 10 * 10 + 2: CFD_TBR(3, 10, 2); break;
+        case 3 * 100 + 7 * 10 + 3: CFD_TBR(3, 7, 3); break;
+        case 4 * 100 + 7 * 10 + 3: CFD_TBR(4, 7, 3); break;
+        default: CFD_TBR(4, 11, 2); break;
+    }
 #undef CFD_TBR
 #undef CFD_TBR_L
     CFD_LAUNCH_CHECK();

@@ -446,12 +446,14 @@ RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double toler
 // One pass of k Jacobi sweeps over planes [zb, ze) (k = 1..4), with the tile
 // shape cfd_set_jacobi3d_blocking selected: rows 5 / 13 -> jacobi3d_tb2 for
 // k = 2; rows 11 (k = 3) / 9 (k = 4) -> jacobi3d_tbk; otherwise the tall-tile
-// jacobi3d_tbr for k >= 3 (17 or 18 rows for k = 3, 15 for k = 4) and
-// jacobi3d_tbk for k = 2.
+// jacobi3d_tbr for k >= 3 (16, 17 or 18 rows for k = 3, 15 or 16 for k = 4;
+// 0 = chosen by its cost model) and jacobi3d_tbk for k = 2.
 int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, int nz, int ny,
                           int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt,
                           bool pre, hipStream_t s) {
-    const int rows = g_j3.tb_rows, zc = g_j3.tb_zchunk;
+    // the configured rows apply to passes of the configured depth; a shorter
+    // remainder pass picks its own tile
+    const int rows = k == jacobi3d_tb_levels() ? g_j3.tb_rows : 0, zc = g_j3.tb_zchunk;
     if (k == 1) return jacobi3d_sweep(in, out, src, nullptr, nz, ny, nx, zb, ze, h2, dt, pre, nullptr, s);
     if (k == 2) {
         if (rows == 5 || rows == 13)
@@ -463,8 +465,7 @@ int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, 
     if ((k == 3 && rows == 11) || (k == 4 && rows == 9))
         return jacobi3d_tbk_pass(k, in, out, src, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, h2, dt, zc,
                                  pre, s);
-    return jacobi3d_tbr_pass(k, (k == 3 && rows == 17) || (k == 4 && rows == 16) ? 1 : 0, in, out, src,
-                             nz, ny, nx, zb, ze,
+    return jacobi3d_tbr_pass(k, rows, in, out, src, nz, ny, nx, zb, ze,
                              fixed_lo, fixed_hi, h2, dt, zc, pre, s);
 }
 
@@ -484,7 +485,7 @@ int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
     CFD_REQUIRE(steps >= 0 && steps <= 4, "blocking steps must be 0 (auto), 1 (off) or 2..4");
     CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13 || rows == 9 || rows == 11 || rows == 15 ||
                     rows == 16 || rows == 17 || rows == 18,
-                "blocking rows must be 0 (auto), 5, 13 (2 levels), 11, 17, 18 (3), 9, 15, 16 (4)");
+                "blocking rows must be 0 (auto), 5, 13 (2 levels), 11, 16, 17, 18 (3), 9, 15, 16 (4)");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
     g_j3.tb_steps = steps;
     g_j3.tb_rows = rows;

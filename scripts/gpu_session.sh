@@ -39,7 +39,7 @@ for s in "$@"; do
     slab1) step slab1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --force-slab --steps 3 --warmup 1 ;;
     benchch) step benchch 600 python bench.py --workload jacobi3d_channel --no-cpu-baseline ;;
     testsk) step pytest_k 900 python -m pytest tests -m gpu -q -k "k_levels or variants_agree or temporal or full_size" ;;
-    ksweep) step ksweep 900 bash -c 'for cfg in ${KSWEEP:-"3 18 1 0" "4 16 1 0" "4 16 1 128" "4 15 1 128" "4 15 1 256"}; do set -- $cfg; echo "K=$1 rows=$2 PD=$3 zchunk=$4"; python bench.py --no-cpu-baseline --steps 5 --tb $1 --tb-rows $2 --tb-prefetch $3 --tb-zchunk $4 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
+    ksweep) step ksweep 900 bash -c 'for cfg in ${KSWEEP:-"3 0 1 0" "3 16 2 0" "3 16 1 256" "4 0 1 0" "2 0 1 0"}; do set -- $cfg; echo "K=$1 rows=$2 PD=$3 zchunk=$4"; python bench.py --no-cpu-baseline --steps 5 --tb $1 --tb-rows $2 --tb-prefetch $3 --tb-zchunk $4 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
     testsgs) step pytest_gs 900 python -m pytest tests -m gpu -q -k "rbgs or slab" ;;
     benchgs) step benchgs 600 python bench.py --workload rbgs3d_1024 ;;
     benchgs_inplace) step benchgs_inplace 600 python bench.py --workload rbgs3d_1024 --tb 1 --no-cpu-baseline --steps 3 ;;

@@ -169,7 +169,8 @@ def test_jacobi3d_temporal_blocking_bitexact(shape, iters, rows, zchunk, prefetc
     assert np.array_equal(host(phi), ref)
 
 
-@pytest.mark.parametrize("levels,rows", [(3, 11), (3, 17), (3, 18), (4, 9), (4, 15), (4, 16), (2, 0)])
+@pytest.mark.parametrize("levels,rows", [(3, 11), (3, 16), (3, 17), (3, 18), (3, 0), (4, 9), (4, 15), (4, 16),
+                                         (2, 0)])
 @pytest.mark.parametrize("shape,iters", [((9, 10, 12), 7), ((21, 30, 264), 8), ((40, 31, 520), 12),
                                          ((5, 4, 8), 4), ((13, 40, 16), 9), ((12, 47, 264), 8)])
 @pytest.mark.parametrize("zchunk", [0, 1, 5])
