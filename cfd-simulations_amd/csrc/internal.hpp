@@ -31,18 +31,30 @@ int jacobi3d_tbk_pass(int K, const float *in, float *out, const float *div, int 
 int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float *div, int nz,
                       int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
                       float dt, int zchunk, bool pre, hipStream_t s);
-// red-black GS workspace (cfd_rbgs_workspace_bytes): flags[1] = iterations
-// done (the fused kernels' stop counter), float maxc[iterations] at byte 16
+// red-black GS workspace (declared below) passes on tall tiles
+struct RbgsWs;
+struct RbgsConsts;
+int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
+                    int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
+                    int iters, RbgsWs *ws, int rollback, int npairs, int rows, hipStream_t s);
+// red-black GS workspace (cfd_rbgs_workspace_bytes): flags[0] = iterations,
+// flags[1] = iterations done, flags[2] = tolerance (float bits), float
+// maxc[iterations] at byte 16
 struct RbgsWs {
     int flags[4];
     float maxc[1];
 };
 // poisson2d.hip
-int launch_rbgs_init(RbgsWs *ws, int iterations, int *iters_done, hipStream_t s);
+int launch_rbgs_init(RbgsWs *ws, int iterations, float tol, int *iters_done, hipStream_t s);
+// iterations done (flags[1], *iters_done) from the per-iteration maxima
+int launch_rbgs_count(RbgsWs *ws, int *iters_done, hipStream_t s);
+// phi <- phi_tmp when ceil(done / per_pass) is odd (phi_tmp NULL: nothing)
+int launch_rbgs_copy(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n, int per_pass,
+                     hipStream_t s);
 // after fused (out-of-place) iterations: phi <- phi_tmp when an odd number
 // ran, and *iters_done <- the count (both read on device: no host sync)
-int launch_rbgs_finish(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n,
-                       int *iters_done, hipStream_t s);
+int launch_rbgs_finish(RbgsWs *ws, float *phi, const float *phi_tmp, size_t n,
+                       int *iters_done, hipStream_t s);  // count + copy, one iteration per pass
 
 // 3-D red-black GS (poisson3d.hip / jacobi3d_tb.hip)
 struct RbgsConsts {
@@ -56,6 +68,10 @@ bool rbgs3d_fused_ok(const float *phi, const float *phi_tmp, const float *div, c
 int rbgs3d_colour_pass(int colour, float *phi, const float *div, const uint8_t *mask, int ny,
                        int nx, int z0, int z1, int zoff, const RbgsConsts &k, RbgsWs *ws, int it,
                        hipStream_t s);
+int rbgs3d_iters_per_pass();  // 1, or 2 (blocking depth 4)
+int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
+                      int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
+                      int iters, RbgsWs *ws, hipStream_t s);
 // one fused iteration (both colours) of planes [zb, ze) of `out` from `in`;
 // max|change| into ws->maxc[it], stop counter ws->flags[1]
 int rbgs3d_tb_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,

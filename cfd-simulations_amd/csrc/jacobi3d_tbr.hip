@@ -32,18 +32,59 @@ __device__ inline void stg4(float *p, float4 v) { *reinterpret_cast<float4 *>(p)
 __device__ inline float4 lds4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
+enum { kJacobi = 0, kRbgs = 1 };
+
 struct TbrArgs {
     const float *in;
     float *out;
     const float *div;  // div, or the precomputed rhs (PRE)
     int nz, ny, nx, nseg, ntile_y, zb, ze, zchunk, fixed_lo, fixed_hi;
-    float h2, dt;
+    float h2, dt;                      // Jacobi
+    float cx, cy, cz, cd, dt_inv, tol; // red-black GS
+    int zoff;        // global z of local plane 0 (colour parity)
+    int it;          // first GS iteration of this pass
+    float *maxc;     // per-iteration max|change| (device), NULL: not accumulated
+    int rollback;    // GS: the conditional re-run of one iteration (see rbgs3d_rollback)
+    int npairs;      // GS rollback: pair passes the solve scheduled
+    const int *count;  // GS rollback: iterations done (device)
 };
 
-template <bool PRE>
+// One level on the float4 of cells x .. x+3.  Jacobi: every interior cell.
+// Red-black GS: the cells of colour `par` parity (v5.py:213-219 generalised:
+// (((cx(E+W) + cy(N+S)) + cz(U+D)) - rhs) * cd with rhs = -div * dt_inv, the
+// in-place kernel's operation order); `chg` folds max|change| of own cells.
+template <int MODE, bool PRE>
 __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S, float4 U,
-                                float4 D, float4 d, int x, int nx, bool upd, float h2, float dt) {
+                                float4 D, float4 d, int x, int nx, bool upd, const TbrArgs &a,
+                                int par, bool own, float &chg) {
     if (!upd) return c;
+    if (MODE == kRbgs) {
+        const float cv[4] = {c.x, c.y, c.z, c.w};
+        const float nv[4] = {N.x, N.y, N.z, N.w};
+        const float sv[4] = {S.x, S.y, S.z, S.w};
+        const float uv[4] = {U.x, U.y, U.z, U.w};
+        const float dv[4] = {D.x, D.y, D.z, D.w};
+        const float rv[4] = {d.x, d.y, d.z, d.w};
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float E = k < 3 ? cv[k + 1] : er;
+            const float Wv = k > 0 ? cv[k - 1] : wl;
+            const int xk = x + k;
+            o[k] = cv[k];
+            if (xk != 0 && xk != nx - 1 && ((par + xk) & 1) == 0) {
+                const float rhs = -rv[k] * a.dt_inv;
+                const float p = a.cx * (E + Wv);
+                const float q = a.cy * (nv[k] + sv[k]);
+                const float r = a.cz * (uv[k] + dv[k]);
+                o[k] = (((p + q) + r) - rhs) * a.cd;
+                const float ch = fabsf(o[k] - cv[k]);
+                if (own && ch > chg) chg = ch;
+            }
+        }
+        return make_float4(o[0], o[1], o[2], o[3]);
+    }
+    const float h2 = a.h2, dt = a.dt;
     const float cv[4] = {c.x, c.y, c.z, c.w};
     const float nv[4] = {N.x, N.y, N.z, N.w};
     const float sv[4] = {S.x, S.y, S.z, S.w};
@@ -71,7 +112,9 @@ __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S
 
 // (A double-buffered, one-barrier-per-step version of the (3, 11, 2) shape --
 // 139 KB of LDS -- was measured at 1007 against 1131 Gcell/s for this one.)
-template <int K, int NWR, int RPW, bool PRE, int PD>
+// MODE kRbgs: K/2 red-black iterations per pass (level l = colour (l-1)&1);
+// see rbgs3d_tbr_pass for the stop rule and the rollback.
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE>
 __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     constexpr int NR = NWR * RPW + 2;  // level-0 rows per tile
     constexpr int W = NR - 2 * K;      // output rows
@@ -93,6 +136,23 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         return smem + base + (r - l) * RS;
     };
 
+    static_assert(MODE == kJacobi || (K % 2 == 0 && !PRE), "GS: whole iterations, raw div");
+    constexpr int NIT = MODE == kRbgs ? K / 2 : 1;  // GS iterations per pass
+    if (MODE == kRbgs) {
+        if (a.rollback) {
+            // re-run iteration 2m' alone when the stop fell after the first
+            // iteration of pair pass m' (whose output holds one too many)
+            const int c = *a.count;
+            if (!((c & 1) && (c - 1) / 2 < a.npairs)) return;
+            if (((c - 1) / 2) & 1) {
+                float *t_ = const_cast<float *>(a.in);
+                a.in = a.out;
+                a.out = t_;
+            }
+        } else if ((a.it >= 1 && a.maxc[a.it - 1] < a.tol) || (a.it >= 2 && a.maxc[a.it - 2] < a.tol)) {
+            return;  // an earlier iteration met the tolerance (v5.py:224-225)
+        }
+    }
     const int nz = a.nz, ny = a.ny, nx = a.nx;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -110,10 +170,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     const size_t plane = (size_t)ny * nx;
     const int zs = z0 - K + 1;  // first front plane
     const int zl = z1 + K - 2;  // last front plane
-    const float h2 = a.h2, dt = a.dt;
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float chg[NIT];  // GS: max|change| of own cells per iteration
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) chg[i] = 0.f;
 
     if (wv < NWR) {
         // ------------------------------------------------------------ row wave
@@ -189,8 +251,11 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                         if (xin) {
                             const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
                             const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
-                            v = level4<PRE>(c, wl, er, N, S, Q[j][l - 1][2], Q[j][l - 1][0], Rq[j][l - 1],
-                                            x, nx, irow[j] && !fx, h2, dt);
+                            const int y = y0 - K + r;
+                            v = level4<MODE, PRE>(c, wl, er, N, S, Q[j][l - 1][2], Q[j][l - 1][0],
+                                                  Rq[j][l - 1], x, nx, irow[j] && !fx, a,
+                                                  (a.zoff + p + y + 1 + ((l - 1) & 1)) & 1,
+                                                  orow[j] && p >= z0 && p < z1, chg[(l - 1) / 2]);
                         }
                         if (l < K) {
                             Q[j][l][0] = Q[j][l][1];
@@ -282,8 +347,11 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     if (hon) {
                         const float4 N = lds4(T(l - 1, hr + 1) + col);
                         const float4 S = lds4(T(l - 1, hr - 1) + col);
-                        v = level4<PRE>(c, side ? inner : 0.f, side ? 0.f : inner, N, S, H[l - 1][2],
-                                        H[l - 1][0], Hr[l - 1], hx, nx, hint && !fixedp(p), h2, dt);
+                        float dummy = 0.f;
+                        v = level4<MODE, PRE>(c, side ? inner : 0.f, side ? 0.f : inner, N, S,
+                                              H[l - 1][2], H[l - 1][0], Hr[l - 1], hx, nx,
+                                              hint && !fixedp(p), a,
+                                              (a.zoff + p + yr + 1 + ((l - 1) & 1)) & 1, false, dummy);
                     }
                     H[l][0] = H[l][1];
                     H[l][1] = H[l][2];
@@ -308,6 +376,11 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             }
         }
     }
+    if (MODE == kRbgs && a.maxc) {
+        __shared__ float red[NIT][NWR + 1];
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) block_reduce_max_store(chg[i], a.maxc + a.it + i, red[i]);
+    }
 }
 
 // Output rows per tile of the tall-tile shape for K levels.
@@ -317,9 +390,12 @@ struct TbrShape {
     bool autopick;  // candidate for rows == 0
     int rows() const { return nwr * rpw + 2 - 2 * K; }
 };
-// (4, 11, 2) spills 9 VGPRs at 168 and runs slower than (4, 7, 3): explicit only
+// (4, 11, 2) spills 9 VGPRs at 168 and runs slower than (4, 7, 3): explicit only.
+// K = 2 shapes serve the red-black GS passes (one iteration per pass); r01 at
+// 1024^3: 20 rows 2.48 ms, 18 rows 2.51 ms, 28 rows 2.60 ms per iteration.
 constexpr TbrShape kShapes[] = {{3, 11, 2, true}, {3, 10, 2, true}, {3, 7, 3, false},
-                                {4, 7, 3, true}, {4, 11, 2, false}};
+                                {4, 7, 3, true}, {4, 11, 2, false}, {2, 11, 2, true},
+                                {2, 10, 2, false}, {2, 10, 3, false}};
 
 int num_cus() {
     static int n = 0;
@@ -340,17 +416,12 @@ int num_cus() {
 // Calibrated on 1024^3, K = 3: 16-row tiles in one round of 256 workgroups
 // (2.48 ms per pass) beat 18-row tiles in 9 rounds of 103 planes (2.62 ms)
 // and in 5 rounds of 205 planes (2.79 ms); the model orders them the same.
-int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float *div, int nz,
-                      int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
-                      float dt, int zchunk, bool pre, hipStream_t s) {
-    if (ze <= zb || ny < 3) return CFD_OK;
-    TbrArgs a{};
-    a.in = in; a.out = out; a.div = div;
-    a.nz = nz; a.ny = ny; a.nx = nx; a.zb = zb; a.ze = ze;
-    a.fixed_lo = fixed_lo; a.fixed_hi = fixed_hi; a.h2 = h2; a.dt = dt;
+// Pick the shape and z-chunk (see above) and launch.
+template <int MODE>
+static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStream_t s) {
     const int pd = jacobi3d_tb_prefetch();
-    const int L = ze - zb;
-    const int nseg = ceil_div(nx, 256);
+    const int L = a.ze - a.zb;
+    const int nseg = ceil_div(a.nx, 256);
     const int ncu = num_cus();
     const TbrShape *best = nullptr;
     int best_zlen = 0;
@@ -358,7 +429,7 @@ int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float 
     for (const TbrShape &sh : kShapes) {
         if (sh.K != K || (rows ? sh.rows() != rows : !sh.autopick)) continue;
         const int W = sh.rows(), NR = W + 2 * K;
-        const long tiles = (long)nseg * ceil_div(ny - 2, W);
+        const long tiles = (long)nseg * ceil_div(a.ny - 2, W);
         for (int nzc = 1; nzc <= 64; ++nzc) {
             int zlen = zchunk > 0 ? zchunk : ceil_div(L, nzc);
             if (zlen > L) zlen = L;
@@ -377,33 +448,71 @@ int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float 
         set_error("jacobi3d_tbr: no tile shape with %d rows for %d levels per pass", rows, K);
         return CFD_E_INVALID;
     }
-    const int W = best->rows();
     a.nseg = nseg;
-    a.ntile_y = ceil_div(ny - 2, W);
+    a.ntile_y = ceil_div(a.ny - 2, best->rows());
     a.zchunk = best_zlen;
     const int blocks = a.nseg * a.ntile_y * ceil_div(L, best_zlen);
 #define CFD_TBR_L(KV, NW, RP, PR, PDV) \
-    hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, PR, PDV>), dim3(blocks), dim3((NW + 1) * 64), 0, s, a)
-#define CFD_TBR(KV, NW, RP)                                                              \
-    do {                                                                                 \
-        if (pd == 2) {                                                                   \
-            if (pre) CFD_TBR_L(KV, NW, RP, true, 2); else CFD_TBR_L(KV, NW, RP, false, 2); \
-        } else {                                                                         \
-            if (pre) CFD_TBR_L(KV, NW, RP, true, 1); else CFD_TBR_L(KV, NW, RP, false, 1); \
-        }                                                                                \
+    hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, PR, PDV, MODE>), dim3(blocks), dim3((NW + 1) * 64), 0, s, a)
+#define CFD_TBR(KV, NW, RP)                                                                   \
+    do {                                                                                      \
+        if constexpr (MODE == kRbgs) {                                                        \
+            if (pd == 2) CFD_TBR_L(KV, NW, RP, false, 2); else CFD_TBR_L(KV, NW, RP, false, 1); \
+        } else if (pd == 2) {                                                                 \
+            if (pre) CFD_TBR_L(KV, NW, RP, true, 2); else CFD_TBR_L(KV, NW, RP, false, 2);      \
+        } else {                                                                              \
+            if (pre) CFD_TBR_L(KV, NW, RP, true, 1); else CFD_TBR_L(KV, NW, RP, false, 1);      \
+        }                                                                                     \
     } while (0)
     const int code = best->K * 100 + best->nwr * 10 + best->rpw;
     switch (code) {
-        case 3 * 100 + 11 * 10 + 2: CFD_TBR(3, 11, 2); break;
-        case 3 * 100 + 10 * 10 + 2: CFD_TBR(3, 10, 2); break;
-        case 3 * 100 + 7 * 10 + 3: CFD_TBR(3, 7, 3); break;
+        case 3 * 100 + 11 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBR(3, 11, 2); break;
+        case 3 * 100 + 10 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBR(3, 10, 2); break;
+        case 3 * 100 + 7 * 10 + 3: if constexpr (MODE == kJacobi) CFD_TBR(3, 7, 3); break;
         case 4 * 100 + 7 * 10 + 3: CFD_TBR(4, 7, 3); break;
-        default: CFD_TBR(4, 11, 2); break;
+        case 4 * 100 + 11 * 10 + 2: CFD_TBR(4, 11, 2); break;
+        case 2 * 100 + 11 * 10 + 2: CFD_TBR(2, 11, 2); break;
+        case 2 * 100 + 10 * 10 + 2: CFD_TBR(2, 10, 2); break;
+        default: CFD_TBR(2, 10, 3); break;
     }
 #undef CFD_TBR
 #undef CFD_TBR_L
     CFD_LAUNCH_CHECK();
     return CFD_OK;
+}
+
+int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float *div, int nz,
+                      int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
+                      float dt, int zchunk, bool pre, hipStream_t s) {
+    if (ze <= zb || ny < 3) return CFD_OK;
+    TbrArgs a{};
+    a.in = in; a.out = out; a.div = div;
+    a.nz = nz; a.ny = ny; a.nx = nx; a.zb = zb; a.ze = ze;
+    a.fixed_lo = fixed_lo; a.fixed_hi = fixed_hi; a.h2 = h2; a.dt = dt;
+    return tbr_launch<kJacobi>(a, K, rows, zchunk, pre, s);
+}
+
+// Red-black GS passes on tall tiles: `iters` (1 or 2) iterations from `it` on,
+// planes [zb, ze) of `out` from `in`.  A pass is skipped on the device when
+// iteration it-1 or it-2 met the tolerance; max|change| of each iteration goes
+// to ws->maxc.  rollback != 0: the conditional re-run after a stop inside a
+// pair pass (in = phi, out = phi_tmp as passed to the solve; the kernel picks
+// the direction from the count in ws->flags[1], see rbgs_count).
+int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
+                    int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
+                    int iters, RbgsWs *ws, int rollback, int npairs, int rows, hipStream_t s) {
+    if (ze <= zb || ny < 3) return CFD_OK;
+    TbrArgs a{};
+    a.in = in; a.out = out; a.div = div;
+    a.nz = nz; a.ny = ny; a.nx = nx; a.zb = zb; a.ze = ze;
+    a.fixed_lo = fixed_lo; a.fixed_hi = fixed_hi;
+    a.cx = k.cx; a.cy = k.cy; a.cz = k.cz; a.cd = k.cd; a.dt_inv = k.dt_inv; a.tol = k.tol;
+    a.zoff = zoff; a.it = it;
+    a.maxc = rollback ? nullptr : ws->maxc;
+    a.rollback = rollback;
+    a.npairs = npairs;
+    a.count = &ws->flags[1];
+    return tbr_launch<kRbgs>(a, 2 * iters, rows, jacobi3d_tb_zchunk(), false, s);
 }
 
 }  // namespace cfd

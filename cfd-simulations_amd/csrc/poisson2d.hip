@@ -423,26 +423,61 @@ __device__ inline bool rbgs_stopped(const RbgsWs *ws, int it, float tol) {
     return it > 0 && ws->maxc[it - 1] < tol;
 }
 
-__global__ void rbgs_init(RbgsWs *ws, int iterations, int *iters_done) {
+__global__ void rbgs_init(RbgsWs *ws, int iterations, float tol, int *iters_done) {
     for (int k = threadIdx.x; k < iterations; k += blockDim.x) ws->maxc[k] = 0.0f;
-    if (threadIdx.x < 4) ws->flags[threadIdx.x] = threadIdx.x == 1 ? iterations : 0;
-    if (threadIdx.x == 0 && iters_done) *iters_done = iterations;
+    if (threadIdx.x == 0) {
+        ws->flags[0] = iterations;
+        ws->flags[1] = iterations;
+        ws->flags[2] = __float_as_int(tol);
+        ws->flags[3] = 0;
+        if (iters_done) *iters_done = iterations;
+    }
 }
 
-int launch_rbgs_init(RbgsWs *ws, int iterations, int *iters_done, hipStream_t s) {
-    hipLaunchKernelGGL(rbgs_init, dim3(1), dim3(1024), 0, s, ws, iterations, iters_done);
+int launch_rbgs_init(RbgsWs *ws, int iterations, float tol, int *iters_done, hipStream_t s) {
+    hipLaunchKernelGGL(rbgs_init, dim3(1), dim3(1024), 0, s, ws, iterations, tol, iters_done);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }
 
-// The fused path ping-pongs phi / phi_tmp, one buffer per iteration; where the
+// Iterations done = 1 + the first iteration whose max|change| < tol (the
+// reference's break, v5.py:224-225), else all: iterations after a stop never
+// write maxc, which stays 0 (< tol whenever a stop is possible at all).  One
+// wave scans maxc; the count goes to flags[1] and *iters_done.
+__global__ void rbgs_count(RbgsWs *__restrict__ ws, int *iters_done) {
+    const int n = ws->flags[0];
+    const float tol = __int_as_float(ws->flags[2]);
+    int first = n;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + (int)threadIdx.x;
+        const bool hit = i < n && ws->maxc[i] < tol;
+        const unsigned long long m = __ballot(hit);
+        if (m) {
+            first = base + __ffsll((long long)m) - 1;
+            break;
+        }
+    }
+    if (threadIdx.x == 0) {
+        const int c = first < n ? first + 1 : n;
+        ws->flags[1] = c;
+        if (iters_done) *iters_done = c;
+    }
+}
+
+int launch_rbgs_count(RbgsWs *ws, int *iters_done, hipStream_t s) {
+    hipLaunchKernelGGL(rbgs_count, dim3(1), dim3(64), 0, s, ws, iters_done);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// The fused paths ping-pong phi / phi_tmp, one buffer per pass; where the
 // last iteration landed depends on the device-side stop, so the copy-back is
-// decided on device too (no host sync in the solve).
-__global__ void rbgs_finish(const RbgsWs *__restrict__ ws, float *__restrict__ phi,
-                            const float *__restrict__ tmp, size_t n, int *iters_done) {
-    const int done = ws->flags[1];
-    if (blockIdx.x == 0 && threadIdx.x == 0 && iters_done) *iters_done = done;
-    if (!tmp || !(done & 1)) return;
+// decided on device too (no host sync in the solve): after c iterations at
+// `per_pass` iterations per pass the result is in buffer ceil(c / per_pass) & 1.
+__global__ void rbgs_copy(const RbgsWs *__restrict__ ws, float *__restrict__ phi,
+                          const float *__restrict__ tmp, size_t n, int per_pass) {
+    const int c = ws->flags[1];
+    if (!(((c + per_pass - 1) / per_pass) & 1)) return;
     const size_t n4 = n / 4;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -451,14 +486,21 @@ __global__ void rbgs_finish(const RbgsWs *__restrict__ ws, float *__restrict__ p
     for (size_t k = 4 * n4 + t0; k < n; k += stride) phi[k] = tmp[k];
 }
 
-int launch_rbgs_finish(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n,
-                       int *iters_done, hipStream_t s) {
+int launch_rbgs_copy(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n, int per_pass,
+                     hipStream_t s) {
+    if (!phi_tmp) return CFD_OK;
     long blocks = (long)((n / 4 + 255) / 256);
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(rbgs_finish, dim3(blocks), dim3(256), 0, s, ws, phi, phi_tmp, n, iters_done);
+    hipLaunchKernelGGL(rbgs_copy, dim3(blocks), dim3(256), 0, s, ws, phi, phi_tmp, n, per_pass);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
+}
+
+int launch_rbgs_finish(RbgsWs *ws, float *phi, const float *phi_tmp, size_t n, int *iters_done,
+                       hipStream_t s) {
+    int rc = launch_rbgs_count(ws, iters_done, s);
+    return rc ? rc : launch_rbgs_copy(ws, phi, phi_tmp, n, 1, s);
 }
 
 // Fused red-black iteration, 2-D: the overlapped-segment row march of
@@ -712,7 +754,7 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
     const float dt_inv = 1.0f / dt;  // 1.0 / np.float32 -> float32
     const float tol = (float)tolerance;
     RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
-    int rc = launch_rbgs_init(w, iterations, iters_done, s);
+    int rc = launch_rbgs_init(w, iterations, tol, iters_done, s);
     if (rc) return rc;
     if (ny < 3 || nx < 3 || iterations == 0) return CFD_OK;
     const bool vec_ok = (nx % 4 == 0) && aligned16(phi) && aligned16(div);

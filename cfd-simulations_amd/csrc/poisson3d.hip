@@ -171,7 +171,7 @@ __global__ __launch_bounds__(W * 64) void jacobi3d_march(
             d = ld4(div + (size_t)z * plane + rofs);
             if (MASK) m = *reinterpret_cast<const uchar4 *>(mask + (size_t)z * plane + rofs);
         }
-        if (USE_LDS) {
+        if constexpr (USE_LDS) {
             const int buf = z & 1;
             lds[buf][w + 1][lane] = cur;
             if (w == 0) lds[buf][0][lane] = hlo;
@@ -443,6 +443,23 @@ RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double toler
     return k;
 }
 
+// Red-black GS iterations per fused pass: 2 when the blocking depth is set to
+// 4 levels (then a stop inside a pair is rolled back after the loop), else 1.
+int rbgs3d_iters_per_pass() { return g_j3.tb_steps == 4 ? 2 : 1; }
+
+// One fused GS pass of `iters` (1, 2) iterations: the tuned 2-level kernel
+// when its rows are set explicitly (5, 13), the tall-tile kernel otherwise.
+int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
+                      int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
+                      int iters, RbgsWs *ws, hipStream_t s) {
+    if (iters == 1 && (g_j3.tb_rows == 5 || g_j3.tb_rows == 13))
+        return rbgs3d_tb_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, ws, s);
+    const int r = g_j3.tb_rows;
+    const bool shape_ok = iters == 1 ? (r == 18 || r == 20 || r == 28) : (r == 15 || r == 16);
+    return rbgs3d_tbr_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, iters,
+                           ws, 0, 0, shape_ok ? r : 0, s);
+}
+
 // One pass of k Jacobi sweeps over planes [zb, ze) (k = 1..4), with the tile
 // shape cfd_set_jacobi3d_blocking selected: rows 5 / 13 -> jacobi3d_tb2 for
 // k = 2; rows 11 (k = 3) / 9 (k = 4) -> jacobi3d_tbk; otherwise the tall-tile
@@ -484,8 +501,9 @@ int cfd_set_jacobi3d_prefetch(int planes) {
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
     CFD_REQUIRE(steps >= 0 && steps <= 4, "blocking steps must be 0 (auto), 1 (off) or 2..4");
     CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13 || rows == 9 || rows == 11 || rows == 15 ||
-                    rows == 16 || rows == 17 || rows == 18,
-                "blocking rows must be 0 (auto), 5, 13 (2 levels), 11, 16, 17, 18 (3), 9, 15, 16 (4)");
+                    rows == 16 || rows == 17 || rows == 18 || rows == 20 || rows == 28,
+                "blocking rows must be 0 (auto), 5, 13, 18, 20, 28 (2 levels), 11, 16, 17, 18 (3), "
+                "9, 15, 16 (4)");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
     g_j3.tb_steps = steps;
     g_j3.tb_rows = rows;
@@ -587,21 +605,33 @@ int cfd_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask, int nz, in
     hipStream_t s = as_stream(stream);
     const RbgsConsts k = rbgs3d_consts(dx, dy, dz, dt, tolerance);
     RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
-    int rc = launch_rbgs_init(w, iterations, iters_done, s);
+    int rc = launch_rbgs_init(w, iterations, k.tol, iters_done, s);
     if (rc) return rc;
     if (nz < 3 || ny < 3 || nx < 3 || iterations == 0) return CFD_OK;
     const size_t n = (size_t)nz * ny * nx;
     const int tk = timing_begin(s);
     if (rbgs3d_fused_ok(phi, phi_tmp, div, mask, nx)) {
-        // fused: one out-of-place pass per iteration (both colours), ping-pong
+        // fused: out-of-place passes of pp iterations (both colours each),
+        // ping-pong; the result's buffer and a stop inside a pair pass are
+        // resolved on the device after the loop
         if ((rc = launch_fix_faces3d(phi, phi_tmp, nullptr, ny, nx, 0, nz, 0, nz - 1, s))) return rc;
+        const int pp = rbgs3d_iters_per_pass();
+        const int npairs = pp == 2 ? iterations / 2 : 0;
         float *a = phi, *b = phi_tmp;
-        for (int it = 0; it < iterations; ++it) {
-            if ((rc = rbgs3d_tb_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, it, w, s))) return rc;
+        for (int it = 0; it < iterations;) {
+            const int m = iterations - it >= pp ? pp : 1;
+            if ((rc = rbgs3d_fused_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, it, m, w, s)))
+                return rc;
+            it += m;
             float *t = a; a = b; b = t;
         }
         timing_end(tk, s, iterations);
-        return launch_rbgs_finish(w, phi, phi_tmp, n, iters_done, s);
+        if ((rc = launch_rbgs_count(w, iters_done, s))) return rc;
+        if (pp == 2 &&
+            (rc = rbgs3d_tbr_pass(phi, phi_tmp, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, 0, 1, w, 1,
+                                  npairs, 0, s)))
+            return rc;
+        return launch_rbgs_copy(w, phi, phi_tmp, n, pp, s);
     }
     for (int it = 0; it < iterations; ++it) {
         if ((rc = rbgs3d_colour_pass(0, phi, div, mask, ny, nx, 1, nz - 1, 0, k, w, it, s))) return rc;
@@ -625,20 +655,21 @@ int cfd_rbgs3d_pass_f32(const float *in, float *out, const float *div, int nz, i
                 "rbgs3d_pass: planes [%d,%d) need 1 (fixed) or 2 readable planes on each side (nz %d)",
                 z_begin, z_end, nz);
     const RbgsConsts k = rbgs3d_consts(dx, dy, dz, dt, tolerance);
-    return rbgs3d_tb_pass(in, out, div, nz, ny, nx, z_begin, z_end, fixed_lo, fixed_hi,
-                          z_global_offset, k, iteration, reinterpret_cast<RbgsWs *>(ws),
-                          as_stream(stream));
+    return rbgs3d_fused_pass(in, out, div, nz, ny, nx, z_begin, z_end, fixed_lo, fixed_hi,
+                             z_global_offset, k, iteration, 1, reinterpret_cast<RbgsWs *>(ws),
+                             as_stream(stream));
 }
 
-int cfd_rbgs_init(void *ws, int iterations, int *iters_done, void *stream) {
+int cfd_rbgs_init(void *ws, int iterations, double tolerance, int *iters_done, void *stream) {
     CFD_REQUIRE(ws && iterations >= 0, "rbgs_init: bad arguments");
-    return launch_rbgs_init(reinterpret_cast<RbgsWs *>(ws), iterations, iters_done, as_stream(stream));
+    return launch_rbgs_init(reinterpret_cast<RbgsWs *>(ws), iterations, (float)tolerance, iters_done,
+                            as_stream(stream));
 }
 
 int cfd_rbgs_finish(void *ws, float *phi, const float *phi_tmp, size_t n, int *iters_done,
                     void *stream) {
     CFD_REQUIRE(ws && phi, "rbgs_finish: null pointer");
-    return launch_rbgs_finish(reinterpret_cast<const RbgsWs *>(ws), phi, phi_tmp, n, iters_done,
+    return launch_rbgs_finish(reinterpret_cast<RbgsWs *>(ws), phi, phi_tmp, n, iters_done,
                               as_stream(stream));
 }
 

@@ -211,8 +211,9 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
 // (bit-identical for every rank count).  The stop rule needs the GLOBAL
 // max|change| of each iteration: one ncclAllReduce(max) of 4 bytes per
 // iteration (skipped when tolerance <= 0, which can never stop).
-//  * fused (ghost 2, no mask): one out-of-place pass per iteration; its two
-//    owned boundary planes per side go out while the interior runs.
+//  * fused (ghost >= 2, no mask): one out-of-place pass per iteration (two per
+//    pass with ghost 4 and blocking depth 4); its G owned boundary planes per
+//    side go out while the interior runs.
 //  * otherwise: in-place colour passes, a G-plane exchange after each colour.
 int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
                         const uint8_t *mask, int nz_local, int ghost, int ny, int nx, int lo_peer,
@@ -222,7 +223,7 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
                         void *comm_stream) {
     SlabComm *c = reinterpret_cast<SlabComm *>(comm);
     CFD_REQUIRE(c && div && phi && ws, "slab_rbgs3d: null pointer");
-    CFD_REQUIRE(ghost == 1 || ghost == 2, "slab_rbgs3d: ghost depth must be 1 or 2");
+    CFD_REQUIRE(ghost >= 1 && ghost <= 4, "slab_rbgs3d: ghost depth must be 1..4");
     CFD_REQUIRE(nz_local >= ghost && ny >= 1 && nx >= 1 && iterations >= 0, "slab_rbgs3d: bad shape");
     const int G = ghost;
     CFD_REQUIRE(z_update_begin >= G && z_update_end <= nz_local + G &&
@@ -234,22 +235,22 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     hipStream_t cs = comm_stream ? as_stream(comm_stream) : s;
     RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
     const RbgsConsts k = rbgs3d_consts(dx, dy, dz, dt, tolerance);
-    int rc = launch_rbgs_init(w, iterations, iters_done, s);
+    int rc = launch_rbgs_init(w, iterations, k.tol, iters_done, s);
     if (rc || iterations == 0 || ny < 3 || nx < 3) return rc;
     const int nzt = nz_local + 2 * G;
     const size_t plane = (size_t)ny * nx;
     const int zb = z_update_begin, ze = z_update_end, zoff = z_global_offset;
     const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
     const bool reduce = c->nranks > 1 && k.tol > 0.0f;
-    auto allreduce = [&](int it, hipStream_t st) -> int {
+    auto allreduce = [&](int it, int cnt, hipStream_t st) -> int {
         if (reduce)
-            CFD_CHECK_NCCL(ncclAllReduce(w->maxc + it, w->maxc + it, 1, ncclFloat32, ncclMax, c->comm, st));
+            CFD_CHECK_NCCL(ncclAllReduce(w->maxc + it, w->maxc + it, cnt, ncclFloat32, ncclMax, c->comm, st));
         return CFD_OK;
     };
     // ghosts of the initial guess
     if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
     const int tk = timing_begin(s);
-    const bool fused = G == 2 && rbgs3d_fused_ok(phi, phi_tmp, div, mask, nx);
+    const bool fused = G >= 2 && rbgs3d_fused_ok(phi, phi_tmp, div, mask, nx);
     if (!fused) {
         for (int it = 0; it < iterations; ++it) {
             for (int colour = 0; colour < 2; ++colour) {
@@ -257,11 +258,15 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
                     return rc;
                 if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
             }
-            if ((rc = allreduce(it, s))) return rc;
+            if ((rc = allreduce(it, 1, s))) return rc;
         }
         timing_end(tk, s, iterations);
         return launch_rbgs_finish(w, phi, nullptr, plane * nzt, iters_done, s);
     }
+    // pp iterations per pass need 2*pp-deep ghosts (the pass recomputes the
+    // inner ghost planes' intermediate colours)
+    const int pp = rbgs3d_iters_per_pass() == 2 && G >= 4 ? 2 : 1;
+    const int npairs = pp == 2 ? iterations / 2 : 0;
     // owned faces the passes never write, in both buffers
     const int full_lo = fixed_lo ? G : -1;
     const int full_hi = fixed_hi ? nz_local + G - 1 : -1;
@@ -269,16 +274,17 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
         return rc;
     const bool can_overlap = overlap && c->nranks > 1 && (ze - zb) >= 2 * G + 1;
     float *a = phi, *b = phi_tmp;
-    for (int it = 0; it < iterations; ++it) {
+    for (int it = 0; it < iterations;) {
+        const int m = iterations - it >= pp ? pp : 1;
         auto run = [&](int z0, int z1) -> int {
             if (z1 <= z0) return CFD_OK;
-            return rbgs3d_tb_pass(a, b, div, nzt, ny, nx, z0, z1, z0 == zb && fixed_lo,
-                                  z1 == ze && fixed_hi, zoff, k, it, w, s);
+            return rbgs3d_fused_pass(a, b, div, nzt, ny, nx, z0, z1, z0 == zb && fixed_lo,
+                                     z1 == ze && fixed_hi, zoff, k, it, m, w, s);
         };
         if (!can_overlap) {
             if ((rc = run(zb, ze))) return rc;
             if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
-            if ((rc = allreduce(it, s))) return rc;
+            if ((rc = allreduce(it, m, s))) return rc;
         } else {
             int ib = zb, ie = ze;
             if (lo_peer >= 0) {
@@ -297,17 +303,25 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
                 // the global max needs the interior's contribution too
                 CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
                 CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
-                if ((rc = allreduce(it, cs))) return rc;
+                if ((rc = allreduce(it, m, cs))) return rc;
             }
             CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
             CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
         }
+        it += m;
         float *t = a;
         a = b;
         b = t;
     }
     timing_end(tk, s, iterations);
-    return launch_rbgs_finish(w, phi, phi_tmp, plane * nzt, iters_done, s);
+    // count (same on every rank: the maxima are global), re-run a pair
+    // pass's first iteration if the stop fell inside it, pick the buffer
+    if ((rc = launch_rbgs_count(w, iters_done, s))) return rc;
+    if (pp == 2 &&
+        (rc = rbgs3d_tbr_pass(phi, phi_tmp, div, nzt, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, 0, 1,
+                              w, 1, npairs, 0, s)))
+        return rc;
+    return launch_rbgs_copy(w, phi, phi_tmp, plane * nzt, pp, s);
 }
 
 }  // extern "C"

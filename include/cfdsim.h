@@ -225,14 +225,15 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
  * global plane z_global_offset).  fixed_lo/hi: plane z_begin-1 / z_end is a
  * Dirichlet plane (else it is recomputed from the plane beyond it).  Skipped
  * when ws's max|change| of iteration-1 < tolerance.  nx % 4 == 0, 16-byte
- * aligned.  ws is prepared by cfd_rbgs_init and read out by cfd_rbgs_finish
- * (phi <- phi_tmp when an odd number of iterations ran; phi_tmp may be NULL
- * for in-place solves; n = elements). */
+ * aligned.  ws is prepared by cfd_rbgs_init and read out by cfd_rbgs_finish:
+ * iterations done = 1 + the first iteration whose max|change| < tolerance
+ * (else all), into *iters_done; phi <- phi_tmp when that count is odd
+ * (phi_tmp may be NULL for in-place solves; n = elements). */
 int cfd_rbgs3d_pass_f32(const float *in, float *out, const float *div, int nz, int ny, int nx,
                         int z_begin, int z_end, int fixed_lo, int fixed_hi, int z_global_offset,
                         double dx, double dy, double dz, float dt, double tolerance, int iteration,
                         void *ws, void *stream);
-int cfd_rbgs_init(void *ws, int iterations, int *iters_done, void *stream);
+int cfd_rbgs_init(void *ws, int iterations, double tolerance, int *iters_done, void *stream);
 int cfd_rbgs_finish(void *ws, float *phi, const float *phi_tmp, size_t n, int *iters_done,
                     void *stream);
 

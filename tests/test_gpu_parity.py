@@ -321,26 +321,38 @@ def test_rbgs3d_random_bitexact(shape, masked, fused):
     assert int(host(done)[0]) == n_ref
 
 
-@pytest.mark.parametrize("rows,zchunk", [(5, 0), (13, 0), (13, 3), (5, 1)])
+# (blocking steps, rows): tuned 2-level kernel (rows 5 / 13), tall tiles with
+# one iteration per pass (steps 0 / 2 / 3), tall tiles with two (steps 4)
+GS_FUSED = [(2, 5), (2, 13), (0, 0), (3, 0), (4, 0)]
+
+
+@pytest.mark.parametrize("steps,rows", GS_FUSED)
+@pytest.mark.parametrize("zchunk", [0, 3, 1])
 @pytest.mark.parametrize("prefetch", [1, 2])
-def test_rbgs3d_fused_tiles_bitexact(rows, zchunk, prefetch):
-    """Tile shapes of the fused pass: 5/13 rows, 1..3 planes per march, both
-    prefetch depths; odd iteration count (result copied back from phi_tmp)."""
-    call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
+@pytest.mark.parametrize("iters", [7, 8])
+def test_rbgs3d_fused_tiles_bitexact(steps, rows, zchunk, prefetch, iters):
+    """Tile shapes of the fused passes: both kernels, 1..3 planes per march,
+    both prefetch depths, odd / even iteration counts (the result is copied
+    back from phi_tmp on the device when it ends there)."""
+    call("cfd_set_jacobi3d_blocking", steps, rows, zchunk)
     call("cfd_set_jacobi3d_prefetch", prefetch)
     rng = np.random.default_rng(8)
-    div = rng.standard_normal((19, 29, 264)).astype(np.float32)
-    ref, n_ref = oracle.rbgs3d(div, dx=0.1, dy=0.1, dz=0.1, dt=np.float32(1e-2), iters=7, tol=0.0)
+    div = rng.standard_normal((19, 45, 264)).astype(np.float32)
+    ref, n_ref = oracle.rbgs3d(div, dx=0.1, dy=0.1, dz=0.1, dt=np.float32(1e-2), iters=iters, tol=0.0)
     phi = torch.zeros_like(dev(div))
     done = torch.zeros(1, dtype=torch.int32, device=DEV)
-    K.solve_pressure_gauss_seidel3d(phi, dev(div), 0.1, 0.1, 0.1, np.float32(1e-2), None, 7, 0.0,
+    K.solve_pressure_gauss_seidel3d(phi, dev(div), 0.1, 0.1, 0.1, np.float32(1e-2), None, iters, 0.0,
                                     iters_done=done)
-    assert n_ref == 7 and int(host(done)[0]) == 7
+    assert n_ref == iters and int(host(done)[0]) == iters
     assert np.array_equal(host(phi), ref)
 
 
-@pytest.mark.parametrize("tol", [2e-5, 1.5e-5])  # stops after 6 / 7 iterations
-def test_rbgs3d_early_exit_fused(tol):
+@pytest.mark.parametrize("steps,rows", GS_FUSED)
+@pytest.mark.parametrize("tol", [2e-5, 1.5e-5, 1e-5])  # stops after 6 / 7 / 11 iterations
+def test_rbgs3d_early_exit_fused(steps, rows, tol):
+    """The stop inside a pair pass (odd count at two iterations per pass) is
+    rolled back on the device; the count and field match the oracle."""
+    call("cfd_set_jacobi3d_blocking", steps, rows, 0)
     rng = np.random.default_rng(13)
     div = rng.standard_normal((24, 26, 40)).astype(np.float32) * np.float32(1e-3)
     ref, n_ref = oracle.rbgs3d(div, dx=0.05, dy=0.05, dz=0.05, dt=np.float32(1e-2), iters=300, tol=tol)
@@ -360,15 +372,15 @@ def test_rbgs3d_fused_matches_colour_passes_at_512():
     g = torch.Generator(device=DEV).manual_seed(3)
     div = torch.randn((n, n, n), device=DEV, generator=g)
     outs = []
-    for fused in (False, True):
-        _gs_fused(fused)
+    for steps in (1, 0, 4):
+        call("cfd_set_jacobi3d_blocking", steps, 0, 0)
         phi = torch.zeros_like(div)
         done = torch.zeros(1, dtype=torch.int32, device=DEV)
         h = 1.0 / (n - 1)
         K.solve_pressure_gauss_seidel3d(phi, div, h, h, h, np.float32(5e-5), None, 6, 0.0, iters_done=done)
         outs.append((phi, int(host(done)[0])))
-    assert outs[0][1] == outs[1][1] == 6
-    assert torch.equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1] == outs[2][1] == 6
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][0], outs[2][0])
 
 
 # ------------------------------------------------------------- predictor & co
@@ -518,7 +530,7 @@ def test_slab_rbgs_passes_emulated_on_one_gpu(tol, iters):
     done = [torch.zeros(1, dtype=torch.int32, device=DEV) for _ in plans]
     s = stream_handle()
     for w, dn in zip(W, done):
-        call("cfd_rbgs_init", ptr(w), iters, ptr(dn), s)
+        call("cfd_rbgs_init", ptr(w), iters, tol, ptr(dn), s)
     for it in range(iters):
         for p, a, b, d_, w in zip(plans, A, B, D, W):
             call("cfd_rbgs3d_pass_f32", ptr(a), ptr(b), ptr(d_), p.nz_total, ny, nx, p.z_update_begin,
@@ -548,11 +560,13 @@ def test_slab_rbgs_passes_emulated_on_one_gpu(tol, iters):
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("ghost", [1, 2])
+@pytest.mark.parametrize("ghost,steps", [(1, 0), (2, 0), (2, 2), (4, 4), (3, 0)])
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("tol", [0.0, 2e-5])
-def test_slab_rbgs_rccl_single_rank(overlap, ghost, tol):
-    """cfd_slab_rbgs3d_f32 with a one-rank communicator equals the oracle."""
+def test_slab_rbgs_rccl_single_rank(overlap, ghost, steps, tol):
+    """cfd_slab_rbgs3d_f32 with a one-rank communicator equals the oracle
+    (one or two iterations per fused pass, early stop included)."""
+    call("cfd_set_jacobi3d_blocking", steps, 13 if steps == 2 else 0, 0)
     nz, ny, nx, iters = 30, 26, 40, 300 if tol > 0 else 9
     rng = np.random.default_rng(11)
     div = rng.standard_normal((nz, ny, nx)).astype(np.float32) * np.float32(1e-3)
