@@ -63,8 +63,7 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="3-D kernel: 0 auto, 1 LDS, 2 cache")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--zchunk", type=int, default=0)
-    ap.add_argument("--tb", type=int, default=0,
-                    help="sweeps fused per HBM pass: 0 auto, 1 off, 2..4 (3-D), 2 (2-D)")
+    ap.add_argument("--tb", type=int, default=0, help="sweeps fused per HBM pass: 0 auto, 1 off, 2..4")
     ap.add_argument("--tb-rows", type=int, default=0)
     ap.add_argument("--tb-zchunk", type=int, default=0)
     ap.add_argument("--tb-prefetch", type=int, default=0, help="planes of prefetch in the blocked kernel")
@@ -167,9 +166,11 @@ def main():
     shape, dt_name, iters_default, bpc = WORKLOADS[ARGS.workload]
     iters = ARGS.iters or iters_default
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
-    call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
-    call("cfd_set_jacobi3d_prefetch", ARGS.tb_prefetch)
-    call("cfd_set_jacobi2d_blocking", min(ARGS.tb, 2))
+    if len(shape) == 3:
+        call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
+        call("cfd_set_jacobi3d_prefetch", ARGS.tb_prefetch)
+    else:
+        call("cfd_set_jacobi2d_blocking", ARGS.tb)
     dt = np.float32(5e-5)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 
@@ -287,7 +288,7 @@ def main():
     # (jacobi3d_tb2) performs 2 sweeps in one HBM pass: 12 B of algorithmic
     # traffic per cell per launch = 6 B per cell-update.
     blocked = ARGS.tb != 1 and (iters >= 2 or gs)
-    levels = int(lib().cfd_get_jacobi3d_levels()) if len(shape) == 3 else 2
+    levels = int(lib().cfd_get_jacobi3d_levels() if len(shape) == 3 else lib().cfd_get_jacobi2d_levels())
     # sweeps per launch: K Jacobi sweeps per blocked pass; the GS timing
     # counts iterations, and a fused GS pass is one (two with --tb 4)
     spl = levels if blocked and not gs else (2 if gs and blocked and ARGS.tb == 4 else 1)
@@ -322,7 +323,7 @@ def main():
                                  f"jacobi3d_tbr<{2 * spl}, MODE_RBGS>") if blocked else "rbgs3d_color x2") if gs
                      else (blocked_kernel_name(levels, ARGS.tb_rows) if blocked
                            else "jacobi3d_march") if len(shape) == 3
-                     else ("jacobi2d_tb2" if blocked else "jacobi2d_march"),
+                     else (f"jacobi2d_tbk<{levels}>" if blocked else "jacobi2d_march"),
                      "sweeps_per_launch": spl, "bytes_per_cell_update": bpc / spl,
                      "cells_per_launch": cells_rank, "algorithmic_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": round(launch_ms, 4),

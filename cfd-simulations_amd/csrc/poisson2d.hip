@@ -204,14 +204,19 @@ static int jacobi2d_sweep(const T *in, T *out, const T *div, const uint8_t *mask
 }
 
 // ---------------------------------------------------------------------------
-// Temporally blocked 2-D Jacobi: TWO sweeps per pass (12 B per two f32
-// cell-updates, 24 B per two f64 updates).  A wave owns 64 lanes x VEC cells
-// but its x-segments OVERLAP by VEC cells on each side: it writes only the
-// inner 64*VEC - 2*VEC cells, so every lane runs the same code and the
-// intermediate level phi^(k+1) it needs one cell beyond its output is
-// computed in-wave (lane 0 / lane 63's chunks), never exchanged.  Rows march
-// with register queues: phi^k rows r-1..r+1 (+ r+2 prefetched) and
-// phi^(k+1) rows r-2..r.  Bit-identical to two single sweeps.
+// Temporally blocked 2-D Jacobi: K sweeps per pass (K = 2..6, 8): one pass reads
+// phi^k and the rhs once and writes phi^(k+K), 12 B (f32) / 24 B (f64) per
+// cell for K cell-updates.  A wave owns 64 lanes x VEC cells, but its
+// x-segments OVERLAP by HL = ceil(K / VEC) lanes on each side: it writes only
+// the inner (64 - 2 HL) * VEC cells, so every lane runs the same code, and the
+// intermediate levels it needs near the segment edge are computed in-wave
+// (erosion: level l is exact HL*VEC - l cells deep into the halo lanes), never
+// exchanged.  Rows march with register queues, the 2-D analogue of
+// jacobi3d_tbk: at front row r, level l is computed for row r - l + 1 from
+// the level-(l-1) queue (rows p-1, p, p+1) and lane shuffles.  Every level
+// uses the single sweep's operation order and mask rule (masked cells -> 0,
+// edges included; Dirichlet rows/columns copied), so the result is
+// bit-identical to K single sweeps.
 template <typename T>
 __device__ inline T jac5(T E, T W, T N, T S, T d, T dx2, T dtv, bool pre) {
     T s = E + W;
@@ -221,14 +226,14 @@ __device__ inline T jac5(T E, T W, T N, T S, T d, T dx2, T dtv, bool pre) {
     return T(0.25) * (s - rhs);
 }
 
-template <typename T, int VEC, bool PRE, bool MASK>
-__global__ __launch_bounds__(256) void jacobi2d_tb2(const T *__restrict__ in, T *__restrict__ out,
+template <typename T, int VEC, int K, bool PRE, bool MASK>
+__global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T *__restrict__ out,
                                                     const T *__restrict__ div,
                                                     const uint8_t *__restrict__ mask, int ny,
                                                     int nx, int nseg, int rows_per_chunk, T dx2,
                                                     T dtv) {
-    static_assert(VEC >= 2, "the overlapped segment needs 2+ cells per lane");
-    constexpr int SOUT = 64 * VEC - 2 * VEC;  // cells written per wave
+    constexpr int HL = (K + VEC - 1) / VEC;    // halo lanes per side
+    constexpr int SOUT = (64 - 2 * HL) * VEC;  // cells written per wave
     const int lane = threadIdx.x & 63;
     const int wpb = blockDim.x / 64;
     const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -238,110 +243,146 @@ __global__ __launch_bounds__(256) void jacobi2d_tb2(const T *__restrict__ in, T 
     const int y0 = 1 + chunk * rows_per_chunk;
     if (y0 >= ny - 1) return;  // wave-uniform
     const int y1 = min(y0 + rows_per_chunk, ny - 1);
-    const int xs = seg * SOUT;
-    const int x0 = xs - VEC + lane * VEC;  // this lane's first cell
+    const int x0 = seg * SOUT - HL * VEC + lane * VEC;  // this lane's first cell
     const bool valid = x0 >= 0 && x0 < nx;
-    const bool writer = lane >= 1 && lane <= 62 && valid;
-    T am[VEC], ac[VEC], ap[VEC], app[VEC];    // phi^k rows r-1, r, r+1, r+2
-    T bm[VEC], bc[VEC], bp[VEC];              // phi^(k+1) rows r-2, r-1, r
-    T dm[VEC], dc[VEC], dn[VEC];              // rhs/div rows r-1, r, r+1
-    uint8_t mm[VEC], mc[VEC], mn[VEC];
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        am[k] = ac[k] = ap[k] = app[k] = bm[k] = bc[k] = bp[k] = dm[k] = dc[k] = dn[k] = T(0);
-        mm[k] = mc[k] = mn[k] = 0;
-    }
-    const int rs = y0 - 1;  // first front row
+    const bool writer = lane >= HL && lane < 64 - HL && valid;
     auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
-    if (valid) {
-        if (rs - 1 >= 0) ld<T, VEC>(in + row(rs - 1), am);
-        ld<T, VEC>(in + row(rs), ac);
-        ld<T, VEC>(in + row(rs + 1), ap);  // rs + 1 = y0 <= ny - 2
-        ld<T, VEC>(div + row(rs), dc);
-        ld<T, VEC>(div + row(rs + 1), dn);
-        if (MASK) {
+    auto inrow = [&](int y) { return valid && y >= 0 && y <= ny - 1; };
+    T Q[K][3][VEC];  // Q[l][i][k]: level l of row (r - l) - 1 + i
+    T R[K][VEC];     // R[j]: rhs of row r - j
+    uint8_t M[K][VEC];
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) { mc[k] = mask[row(rs) + k]; mn[k] = mask[row(rs + 1) + k]; }
-        }
-    }
-    for (int r = rs; r <= y1; ++r) {
-        // prefetch phi^k row r+2 (needed as the N neighbour next step)
-        if (valid && r + 1 <= y1 && r + 2 <= ny - 1) ld<T, VEC>(in + row(r + 2), app);
-        // phi^(k+1) of row r
-        const bool fixed = r == 0 || r == ny - 1;
-        T wl = __shfl_up(ac[VEC - 1], 1, 64);
-        T er = __shfl_down(ac[0], 1, 64);
-        T l1[VEC];
+    for (int l = 0; l < K; ++l)
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            const T E = (k + 1 < VEC) ? ac[k + 1] : er;
-            const T W = (k > 0) ? ac[k - 1] : wl;
-            const int x = x0 + k;
-            T v = (fixed || x == 0 || x >= nx - 1) ? ac[k] : jac5<T>(E, W, ap[k], am[k], dc[k], dx2, dtv, PRE);
-            if (MASK && mc[k]) v = T(0);
-            l1[k] = v;
+            Q[l][0][k] = Q[l][1][k] = Q[l][2][k] = R[l][k] = T(0);
+            M[l][k] = 0;
         }
-        // phi^(k+2) of row r-1
-        T wl1 = __shfl_up(bc[VEC - 1], 1, 64);
-        T er1 = __shfl_down(bc[0], 1, 64);
-        if (r >= y0 + 1 && writer) {
-            T o[VEC];
+    const int rs = y0 - K + 1;  // first front row
+    const int rl = y1 + K - 2;  // last front row
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const T E = (k + 1 < VEC) ? bc[k + 1] : er1;
-                const T W = (k > 0) ? bc[k - 1] : wl1;
-                const int x = x0 + k;
-                T v = (x == 0 || x >= nx - 1) ? bc[k] : jac5<T>(E, W, l1[k], bm[k], dm[k], dx2, dtv, PRE);
-                if (MASK && mm[k]) v = T(0);
-                o[k] = v;
-            }
-            st<T, VEC>(out + row(r - 1), o);
-        }
-        // rotate (rhs/mask for row r+2 loaded here: used two steps on)
+    for (int i = 0; i < 3; ++i)
+        if (inrow(rs - 1 + i)) ld<T, VEC>(in + row(rs - 1 + i), Q[0][i]);
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            am[k] = ac[k]; ac[k] = ap[k]; ap[k] = app[k];
-            bm[k] = bc[k]; bc[k] = l1[k];
-            dm[k] = dc[k]; dc[k] = dn[k];
-            if (MASK) { mm[k] = mc[k]; mc[k] = mn[k]; }
-        }
-        if (valid && r + 2 <= y1 + 0 && r + 2 <= ny - 1) {
-            ld<T, VEC>(div + row(r + 2), dn);
+    for (int j = 0; j < K; ++j) {
+        if (inrow(rs - j)) {
+            ld<T, VEC>(div + row(rs - j), R[j]);
             if (MASK) {
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) mn[k] = mask[row(r + 2) + k];
+                for (int k = 0; k < VEC; ++k) M[j][k] = mask[row(rs - j) + k];
             }
+        }
+    }
+    for (int r = rs; r <= rl; ++r) {
+        // prefetch: level 0 of row r+2, rhs / mask of row r+1 (next step's)
+        T nq[VEC], nd[VEC];
+        uint8_t nm[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) { nq[k] = nd[k] = T(0); nm[k] = 0; }
+        if (inrow(r + 2)) ld<T, VEC>(in + row(r + 2), nq);
+        if (inrow(r + 1)) {
+            ld<T, VEC>(div + row(r + 1), nd);
+            if (MASK) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) nm[k] = mask[row(r + 1) + k];
+            }
+        }
+#pragma unroll
+        for (int l = 1; l <= K; ++l) {
+            const int p = r - l + 1;
+            const bool fixed = p == 0 || p == ny - 1;
+            const T wl = __shfl_up(Q[l - 1][1][VEC - 1], 1, 64);
+            const T er = __shfl_down(Q[l - 1][1][0], 1, 64);
+            T v[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const T E = (k + 1 < VEC) ? Q[l - 1][1][k + 1] : er;
+                const T W = (k > 0) ? Q[l - 1][1][k - 1] : wl;
+                const int x = x0 + k;
+                T val = (fixed || x <= 0 || x >= nx - 1)
+                            ? Q[l - 1][1][k]
+                            : jac5<T>(E, W, Q[l - 1][2][k], Q[l - 1][0][k], R[l - 1][k], dx2, dtv, PRE);
+                if (MASK && M[l - 1][k]) val = T(0);
+                v[k] = val;
+            }
+            if (l < K) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    Q[l][0][k] = Q[l][1][k];
+                    Q[l][1][k] = Q[l][2][k];
+                    Q[l][2][k] = v[k];
+                }
+            } else if (writer && p >= y0 && p < y1) {
+                st<T, VEC>(out + row(p), v);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            Q[0][0][k] = Q[0][1][k];
+            Q[0][1][k] = Q[0][2][k];
+            Q[0][2][k] = nq[k];
+        }
+#pragma unroll
+        for (int j = K - 1; j > 0; --j)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                R[j][k] = R[j - 1][k];
+                M[j][k] = M[j - 1][k];
+            }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            R[0][k] = nd[k];
+            M[0][k] = nm[k];
         }
     }
 }
 
 template <typename T, int VEC>
-static int jacobi2d_tb2_pass(const T *in, T *out, const T *div, const uint8_t *mask, int ny, int nx,
-                             T dx2, T dtv, bool pre, hipStream_t s) {
-    constexpr int SOUT = 64 * VEC - 2 * VEC;
+static int jacobi2d_tbk_pass(int K, const T *in, T *out, const T *div, const uint8_t *mask, int ny,
+                             int nx, T dx2, T dtv, bool pre, hipStream_t s) {
+    const int HL = (K + VEC - 1) / VEC;
+    const int SOUT = (64 - 2 * HL) * VEC;
     const int nseg = ceil_div(nx, SOUT);
     const int rows = ny - 2;
     if (rows <= 0) return CFD_OK;
+    // ~8192 waves (32 per CU) when the grid allows; chunks long enough that
+    // the 2K-2 re-marched rows stay a small fraction
     int rpc = ceil_div((long)rows * nseg, 8192);
-    if (rpc < 8) rpc = 8;
-    if (rpc > 64) rpc = 64;
+    const int rmin = 16 * (K - 1);
+    if (rpc < rmin) rpc = rmin;
+    if (rpc > 256) rpc = 256;
     const int nchunk = ceil_div(rows, rpc);
     const int wpb = 4;
     const int blocks = ceil_div((long)nseg * nchunk, wpb);
-#define CFD_J2TB(PR, M)                                                                          \
-    hipLaunchKernelGGL((jacobi2d_tb2<T, VEC, PR, M>), dim3(blocks), dim3(wpb * 64), 0, s, in, out, \
-                       div, mask, ny, nx, nseg, rpc, dx2, dtv)
-    if (mask) {
-        if (pre) CFD_J2TB(true, true); else CFD_J2TB(false, true);
-    } else {
-        if (pre) CFD_J2TB(true, false); else CFD_J2TB(false, false);
+#define CFD_J2K(KV, PR, M)                                                                        \
+    hipLaunchKernelGGL((jacobi2d_tbk<T, VEC, KV, PR, M>), dim3(blocks), dim3(wpb * 64), 0, s, in, \
+                       out, div, mask, ny, nx, nseg, rpc, dx2, dtv)
+#define CFD_J2KK(KV)                                                              \
+    do {                                                                          \
+        if (mask) {                                                               \
+            if (pre) CFD_J2K(KV, true, true); else CFD_J2K(KV, false, true);      \
+        } else {                                                                  \
+            if (pre) CFD_J2K(KV, true, false); else CFD_J2K(KV, false, false);    \
+        }                                                                         \
+    } while (0)
+    switch (K) {
+        case 2: CFD_J2KK(2); break;
+        case 3: CFD_J2KK(3); break;
+        case 4: CFD_J2KK(4); break;
+        case 5: CFD_J2KK(5); break;
+        case 6: CFD_J2KK(6); break;
+        default: CFD_J2KK(8); break;
     }
-#undef CFD_J2TB
+#undef CFD_J2KK
+#undef CFD_J2K
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }
 
-static int g_j2_blocking = 0;  // 0 auto (on), 1 off
+static int g_j2_blocking = 0;  // sweeps per pass: 0 auto, 1 off, 2..6, 8
+// r01 at 8192^2 f64 (Gcell/s): K=2 368, 3 554, 4 752, 5 876, 6 1051, 8 1232,
+// 10 1228, 12 1155 (the pass turns latency-bound past 8 levels)
+constexpr int kDefaultLevels2d = 8;
 
 template <typename T>
 __global__ void k_rhs2d(const T *__restrict__ div, T *__restrict__ rhs, size_t n, T dx2, T dtv) {
@@ -380,15 +421,17 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
     T *a = phi, *b = tmp;
     const int tk = timing_begin(s);
     if (g_j2_blocking != 1 && vec_ok && resid_every <= 0 && iters >= 2 && ny >= 3) {
-        // temporally blocked: one single sweep if iters is odd, then fused pairs
+        // temporally blocked: passes of K sweeps, the remainder last
+        const int K = g_j2_blocking >= 2 ? g_j2_blocking : kDefaultLevels2d;
         int done = 0;
         while (done < iters) {
-            const bool single = (iters - done) & 1;
-            rc = single ? jacobi2d_sweep<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, nullptr, s)
-                        : jacobi2d_tb2_pass<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, s);
+            int k = iters - done < K ? iters - done : K;
+            if (k == 7) k = 6;  // instantiated depths: 2..6, 8
+            rc = k == 1 ? jacobi2d_sweep<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, nullptr, s)
+                        : jacobi2d_tbk_pass<T, V>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, s);
             if (rc) return rc;
             if (done == 0 && (rc = fix_edge_rows<T>(tmp, phi, nullptr, ny, nx, s))) return rc;
-            done += single ? 1 : 2;
+            done += k;
             T *t = a; a = b; b = t;
         }
         timing_end(tk, s, iters);
@@ -731,8 +774,11 @@ int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rh
                                   iters, resid_every, resid_out, as_stream(stream));
 }
 
+int cfd_get_jacobi2d_levels(void) { return g_j2_blocking >= 2 ? g_j2_blocking : kDefaultLevels2d; }
+
 int cfd_set_jacobi2d_blocking(int steps) {
-    CFD_REQUIRE(steps >= 0 && steps <= 2, "blocking steps must be 0 (auto), 1 or 2");
+    CFD_REQUIRE((steps >= 0 && steps <= 6) || steps == 8,
+                "blocking steps must be 0 (auto), 1 (off), 2..6 or 8");
     g_j2_blocking = steps;
     return CFD_OK;
 }

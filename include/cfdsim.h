@@ -69,10 +69,14 @@ int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, float *resid_out, void *stream);
 /* fp64 fields (memory_efficient=False, v5.py:287); dt promotes exactly. */
-/* Both 2-D solves fuse two sweeps per HBM pass (temporal blocking, same bits)
- * unless disabled: steps = 0 auto (on), 1 off, 2 on.  Residual requests and
- * unaligned / nx % (16/sizeof(T)) != 0 arrays always run single sweeps. */
+/* Both 2-D solves fuse `steps` sweeps per HBM pass (temporal blocking, same
+ * bits; a remainder iters % steps runs as a shorter pass): 0 auto (8), 1 off,
+ * 2..6, 8.  Residual requests and unaligned / nx % (16/sizeof(T)) != 0 arrays
+ * always run single sweeps.  (The 2-D red-black GS fuses its two colours per
+ * pass unless steps == 1.) */
 int cfd_set_jacobi2d_blocking(int steps);
+/* 2-D Jacobi sweeps per blocked pass currently in effect. */
+int cfd_get_jacobi2d_levels(void);
 int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, double *resid_out, void *stream);

@@ -62,11 +62,11 @@ def test_jacobi2d_golden_bitexact(golden, name):
     assert np.array_equal(out, d["phi"])
 
 
-@pytest.mark.parametrize("blocking", [1, 2])
+@pytest.mark.parametrize("blocking", [1, 2, 3, 4, 5, 6, 8])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("shape,iters", [((37, 53), 17), ((3, 3), 4), ((130, 260), 31),
                                          ((66, 516), 8), ((2, 9), 3), ((200, 248), 10), ((9, 124), 6),
-                                         ((71, 1000), 12)])
+                                         ((71, 1000), 12), ((300, 124), 9), ((517, 40), 7)])
 def test_jacobi2d_random_bitexact(dtype, shape, iters, blocking):
     call("cfd_set_jacobi2d_blocking", blocking)
     rng = np.random.default_rng(11)
@@ -119,9 +119,10 @@ def test_jacobi2d_residual():
         assert got[k - 1] == np.abs(a - b).max()
 
 
-def test_jacobi2d_8192_f64_full_size():
+@pytest.mark.parametrize("iters", [3, 8])
+def test_jacobi2d_8192_f64_full_size(iters):
     """Config 2 at full size (8192^2 fp64): a few sweeps, bit-exact."""
-    n, iters = 8192, 3
+    n = 8192
     rng = np.random.default_rng(1234)
     div = rng.standard_normal((n, n))
     ref = oracle.jacobi2d(div, dx=1.0 / (n - 1), dt=np.float32(5e-5), iters=iters)
