@@ -11,9 +11,10 @@ fixed, each rank owns 1024/N planes).
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  `value` = all ranks' interior cell-updates / the
-max-over-ranks wall time of the K timed steps.  `roofline` prices the
-dominant kernel (the sweep) at 12 algorithmic bytes per fp32 cell-update
-(read phi, read div, write phi') using HIP events recorded on the sweep's own
+max-over-ranks wall time of the K timed steps.  `roofline` prices one launch
+of the dominant kernel -- a temporally blocked pass that fuses several sweeps
+-- at the 12 algorithmic bytes per fp32 cell (24 per fp64) the pass moves
+(read phi, read rhs, write phi'), using HIP events recorded on the solve's own
 stream around its launches.  `cpu_baseline` times the NumPy restatement of the
 reference's Jacobi branch (oracle/, bit-exact to v5.py:336-346) on a bounded
 sample of the same grid, on this host, at N=1 only.
@@ -357,8 +358,9 @@ def blocked_kernel_name(levels, rows):
         return "jacobi3d_tb2" if rows in (5, 13) else "jacobi3d_tbk<2>"
     if (levels, rows) in ((3, 11), (4, 9)):
         return f"jacobi3d_tbk<{levels}>"
-    shape = {(3, 17): "7x3", (4, 16): "11x2"}.get((levels, rows), "11x2" if levels == 3 else "7x3")
-    return f"jacobi3d_tbr<{levels}, {shape}>"
+    if rows == 0:
+        return f"jacobi3d_tbr<{levels}> (tile shape by the launcher's cost model)"
+    return f"jacobi3d_tbr<{levels}> ({rows}-row tiles)"
 
 
 def verify_slabs(S, K, dist, comm, world, rank, dev):

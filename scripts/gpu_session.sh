@@ -29,8 +29,8 @@ for s in "$@"; do
     bench2d) step bench2d 600 python bench.py --workload jacobi2d_8192_f64 ;;
     tiles) step tiles 900 python bench.py --steps 2 --warmup 1 --sweep-tiles --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-    pmc_fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
-    pmc_write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    pmc_fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 30 --no-cpu-baseline ;;
+    pmc_write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 30 --no-cpu-baseline ;;
     sq_tb) step sq_tb 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES -d gpurun_out/sq_tb -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
     sq_march) step sq_march 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES -d gpurun_out/sq_march -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --tb 1 --no-cpu-baseline ;;
     pmc_fetch_tb) step pmc_fetch_tb 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_tb -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
@@ -47,6 +47,9 @@ for s in "$@"; do
     gssweep) step gssweep 900 bash -c 'for cfg in "0 0" "2 13" "4 0" "4 16" "2 18" "2 20" "2 28"; do set -- $cfg; echo "tb=$1 rows=$2"; python bench.py --workload rbgs3d_1024 --no-cpu-baseline --steps 3 --tb $1 --tb-rows $2 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*\|iterations_done_last_step\": [0-9]*" | tr "\n" " "; echo; done' ;;
     benchgs_inplace) step benchgs_inplace 600 python bench.py --workload rbgs3d_1024 --tb 1 --no-cpu-baseline --steps 3 ;;
     slab1gs) step slab1gs 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29542 bench.py --gpus 1 --force-slab --workload rbgs3d_1024 --steps 3 --warmup 1 ;;
+    prof2d) step prof2d 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof2d -o run --output-format csv -- python3 bench.py --workload jacobi2d_8192_f64 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_fetch_2d) step pmc_fetch_2d 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_2d -o run --output-format csv -- python3 bench.py --workload jacobi2d_8192_f64 --steps 1 --warmup 0 --iters 80 --no-cpu-baseline ;;
+    pmc_write_2d) step pmc_write_2d 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_2d -o run --output-format csv -- python3 bench.py --workload jacobi2d_8192_f64 --steps 1 --warmup 0 --iters 80 --no-cpu-baseline ;;
     prof_gs) step prof_gs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_fetch_gs) step pmc_fetch_gs 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
     pmc_write_gs) step pmc_write_gs 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
