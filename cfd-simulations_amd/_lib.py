@@ -60,6 +60,7 @@ PROTOTYPES = {
     "cfd_comm_unique_id": (c_int, [P, c_size_t]),
     "cfd_comm_init": (c_int, [P, c_int, c_int, ctypes.POINTER(c_void_p)]),
     "cfd_comm_destroy": (c_int, [P]),
+    "cfd_comm_init_local": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "cfd_slab_jacobi3d_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                       c_int, c_double, c_float, c_int, c_int, P, P]),
     "cfd_jacobi3d_sweep_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_double,

@@ -14,17 +14,148 @@
 //
 // The exchange plan (peers, which planes are updated) is computed on the host
 // (SlabPlan in the Python package) and tested there on CPU with gloo.
+//
+// Transport: RCCL (cfd_comm_init), or -- for tests and rehearsals on a single
+// GPU, where RCCL refuses several ranks per device -- an in-process group of N
+// ranks driven by N host threads (cfd_comm_init_local): the same drivers, the
+// same pass / exchange / reduce sequence, with the send/recv pairs replaced by
+// device copies ordered by HIP events and host barriers.
 #include <rccl/rccl.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <vector>
 
 #include "internal.hpp"
 
 namespace cfd {
 
+struct LocalGroup {
+    struct Slot {
+        float *buf[2] = {nullptr, nullptr};
+        float *maxc = nullptr;
+        int nzl = 0, G = 0;
+        size_t plane = 0;
+        hipEvent_t ready = nullptr, done = nullptr;
+    };
+    explicit LocalGroup(int n_) : n(n_), slot(n_) {}
+    // all ranks meet; false if a rank did not arrive within the timeout (it
+    // failed): the group is then broken and every later call fails fast
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) return false;
+        const long gen = generation;
+        if (++arrived == n) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+            return true;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen || broken; })) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return !broken;
+    }
+    int n;
+    std::vector<Slot> slot;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    long generation = 0;
+    bool broken = false;
+};
+
 struct SlabComm {
     ncclComm_t comm = nullptr;
+    std::shared_ptr<LocalGroup> grp;  // in-process transport instead of RCCL
     int rank = 0, nranks = 1;
     hipEvent_t ev_boundary = nullptr, ev_comm = nullptr;
 };
+
+#define CFD_GROUP_BARRIER(g)                                                       \
+    do {                                                                           \
+        if (!(g)->barrier()) {                                                     \
+            ::cfd::set_error("local slab group: a rank did not reach the barrier"); \
+            return CFD_E_COMM;                                                     \
+        }                                                                          \
+    } while (0)
+
+// each rank of a local group publishes its two field buffers and maxima
+static int register_local(SlabComm *c, float *phi, float *phi_tmp, RbgsWs *ws, int nzl, int G,
+                          size_t plane) {
+    LocalGroup::Slot &me = c->grp->slot[c->rank];
+    me.buf[0] = phi;
+    me.buf[1] = phi_tmp;
+    me.maxc = ws ? ws->maxc : nullptr;
+    me.nzl = nzl;
+    me.G = G;
+    me.plane = plane;
+    CFD_GROUP_BARRIER(c->grp);
+    return CFD_OK;
+}
+
+// send/recv of G planes with each neighbour, as device copies: wait until the
+// neighbour's pass has produced its planes (and stopped reading its ghosts),
+// copy ours into its ghosts, and let it wait for our copies in turn
+static int exchange_local(SlabComm *c, float *a, int nzl, int G, size_t plane, int lo, int hi,
+                          hipStream_t s) {
+    LocalGroup *g = c->grp.get();
+    LocalGroup::Slot &me = g->slot[c->rank];
+    const int bi = a == me.buf[0] ? 0 : a == me.buf[1] ? 1 : -1;
+    CFD_REQUIRE(bi >= 0, "local slab group: exchange of an unregistered buffer");
+    CFD_CHECK_HIP(hipEventRecord(me.ready, s));
+    CFD_GROUP_BARRIER(g);
+    const size_t n = (size_t)G * plane * sizeof(float);
+    for (int peer : {lo, hi}) {
+        if (peer < 0) continue;
+        const LocalGroup::Slot &p = g->slot[peer];
+        CFD_REQUIRE(p.G == G && p.plane == plane, "local slab group: ranks disagree on the layout");
+        CFD_CHECK_HIP(hipStreamWaitEvent(s, p.ready, 0));
+        const float *src = peer == lo ? a + (size_t)G * plane : a + (size_t)nzl * plane;
+        float *dst = peer == lo ? p.buf[bi] + (size_t)(p.nzl + G) * plane : p.buf[bi];
+        CFD_CHECK_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s));
+    }
+    CFD_CHECK_HIP(hipEventRecord(me.done, s));
+    CFD_GROUP_BARRIER(g);
+    for (int peer : {lo, hi})
+        if (peer >= 0) CFD_CHECK_HIP(hipStreamWaitEvent(s, g->slot[peer].done, 0));
+    return CFD_OK;
+}
+
+struct MaxcPtrs {
+    const float *p[16];
+};
+__global__ void k_group_max(MaxcPtrs ptrs, int n, int off, int cnt, float *dst) {
+    const int i = threadIdx.x;
+    if (i >= cnt) return;
+    float m = 0.f;
+    for (int r = 0; r < n; ++r) m = fmaxf(m, ptrs.p[r][off + i]);
+    dst[off + i] = m;
+}
+
+// allreduce(max) of maxc[off .. off+cnt) over the group (idempotent: a rank
+// may read a peer's entry before or after the peer overwrote it with the max)
+static int allreduce_local(SlabComm *c, int off, int cnt, hipStream_t s) {
+    LocalGroup *g = c->grp.get();
+    CFD_REQUIRE(g->n <= 16, "local slab group: at most 16 ranks");
+    LocalGroup::Slot &me = g->slot[c->rank];
+    CFD_CHECK_HIP(hipEventRecord(me.ready, s));
+    CFD_GROUP_BARRIER(g);
+    MaxcPtrs ptrs{};
+    for (int r = 0; r < g->n; ++r) {
+        CFD_CHECK_HIP(hipStreamWaitEvent(s, g->slot[r].ready, 0));
+        ptrs.p[r] = g->slot[r].maxc;
+    }
+    hipLaunchKernelGGL(k_group_max, dim3(1), dim3(64), 0, s, ptrs, g->n, off, cnt, me.maxc);
+    CFD_LAUNCH_CHECK();
+    // no rank reuses its ready event before every rank has enqueued its waits
+    CFD_GROUP_BARRIER(g);
+    return CFD_OK;
+}
 
 #define CFD_CHECK_NCCL(expr)                                                              \
     do {                                                                                  \
@@ -41,6 +172,7 @@ struct SlabComm {
 // planes; each direction is one contiguous message of G planes.
 static int exchange(SlabComm *c, float *a, int nzl, int G, size_t plane, int lo, int hi,
                     hipStream_t s) {
+    if (c->grp) return exchange_local(c, a, nzl, G, plane, lo, hi, s);
     if (lo < 0 && hi < 0) return CFD_OK;
     const size_t n = (size_t)G * plane;
     CFD_CHECK_NCCL(ncclGroupStart());
@@ -96,11 +228,37 @@ int cfd_comm_init(const void *unique_id, int nranks, int rank, void **comm) {
     return CFD_OK;
 }
 
+int cfd_comm_init_local(int nranks, void **comms) {
+    CFD_REQUIRE(comms && nranks >= 1 && nranks <= 16, "comm_init_local: 1..16 ranks");
+    auto g = std::make_shared<LocalGroup>(nranks);
+    for (int r = 0; r < nranks; ++r) {
+        SlabComm *c = new SlabComm();
+        c->grp = g;
+        c->rank = r;
+        c->nranks = nranks;
+        if (hipEventCreateWithFlags(&c->ev_boundary, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->slot[r].ready, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->slot[r].done, hipEventDisableTiming) != hipSuccess) {
+            set_error("comm_init_local: hipEventCreate failed");
+            return CFD_E_HIP;
+        }
+        comms[r] = c;
+    }
+    return CFD_OK;
+}
+
 int cfd_comm_destroy(void *comm) {
     if (!comm) return CFD_OK;
     SlabComm *c = reinterpret_cast<SlabComm *>(comm);
     if (c->ev_boundary) (void)hipEventDestroy(c->ev_boundary);
     if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
+    if (c->grp) {
+        LocalGroup::Slot &me = c->grp->slot[c->rank];
+        if (me.ready) (void)hipEventDestroy(me.ready);
+        if (me.done) (void)hipEventDestroy(me.done);
+        me.ready = me.done = nullptr;
+    }
     ncclResult_t r = c->comm ? ncclCommDestroy(c->comm) : ncclSuccess;
     delete c;
     if (r != ncclSuccess) {
@@ -145,6 +303,7 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
         if ((rc = launch_rhs_f32(div, rhs_ws, plane * nzt, h2, dt, s))) return rc;
         src = rhs_ws;
     }
+    if (c->grp && (rc = register_local(c, phi, phi_tmp, nullptr, nz_local, G, plane))) return rc;
     // ghosts of the initial guess
     if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
     const int zb = z_update_begin, ze = z_update_end;
@@ -243,10 +402,12 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
     const bool reduce = c->nranks > 1 && k.tol > 0.0f;
     auto allreduce = [&](int it, int cnt, hipStream_t st) -> int {
+        if (reduce && c->grp) return allreduce_local(c, it, cnt, st);
         if (reduce)
             CFD_CHECK_NCCL(ncclAllReduce(w->maxc + it, w->maxc + it, cnt, ncclFloat32, ncclMax, c->comm, st));
         return CFD_OK;
     };
+    if (c->grp && (rc = register_local(c, phi, phi_tmp, w, nz_local, G, plane))) return rc;
     // ghosts of the initial guess
     if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
     const int tk = timing_begin(s);

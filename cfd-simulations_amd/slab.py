@@ -164,6 +164,33 @@ class RcclComm:
             pass
 
 
+class LocalComm:
+    """One rank of an in-process slab group (cfd_comm_init_local): N ranks
+    driven by N host threads on one GPU, for tests and rehearsals where RCCL
+    cannot put several ranks on one device.  Same interface as RcclComm."""
+
+    def __init__(self, handle, rank: int, nranks: int):
+        self.handle, self.rank, self.nranks = handle, rank, nranks
+
+    @staticmethod
+    def group(nranks: int):
+        import ctypes
+        arr = (ctypes.c_void_p * nranks)()
+        call("cfd_comm_init_local", int(nranks), arr)
+        return [LocalComm(ctypes.c_void_p(arr[r]), r, nranks) for r in range(nranks)]
+
+    def close(self):
+        if self.handle:
+            call("cfd_comm_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class SlabJacobi3D:
     """Distributed 7-point Jacobi on this rank's slab (device tensors).  With
     ``plan.ghost == G >= 2`` the sweeps run temporally blocked (up to G per
@@ -250,4 +277,4 @@ def sweep_range(phi_in, phi_out, div, mask, z_begin, z_end, h, dt, resid=None):
          float(np.float32(dt)), ptr(resid), stream_handle())
 
 
-__all__ = ["SlabPlan", "RcclComm", "SlabJacobi3D", "SlabRBGS3D", "sweep_range", "comm_unique_id", "lib"]
+__all__ = ["SlabPlan", "RcclComm", "LocalComm", "SlabJacobi3D", "SlabRBGS3D", "sweep_range", "comm_unique_id", "lib"]

@@ -186,6 +186,13 @@ int cfd_nonfinite_count_f32(const float *a, const float *b, size_t n, int *out, 
 int cfd_comm_unique_id(void *out, size_t bytes); /* bytes >= 128 */
 int cfd_comm_init(const void *unique_id, int nranks, int rank, void **comm);
 int cfd_comm_destroy(void *comm);
+/* An in-process group of nranks (<= 16) communicators for ONE process driving
+ * the ranks from nranks host threads on one GPU (RCCL refuses several ranks per
+ * device): the slab drivers below run unchanged, with each send/recv pair
+ * replaced by a device copy ordered by HIP events and host barriers, and the
+ * max-allreduce by a kernel over all ranks' maxima.  For tests and
+ * rehearsals; comms[r] is released with cfd_comm_destroy. */
+int cfd_comm_init_local(int nranks, void **comms);
 /* Exchange plan, computed and tested on the host (SlabPlan in the package):
  * ghost = ghost planes per side, 1..4: a pass runs min(ghost, levels) sweeps
  * (cfd_set_jacobi3d_blocking), so ghost >= 2 enables the blocked kernels:

@@ -42,6 +42,7 @@ for s in "$@"; do
     ksweep) step ksweep 900 bash -c 'for cfg in ${KSWEEP:-"3 0 1 0" "3 16 2 0" "3 16 1 256" "4 0 1 0" "2 0 1 0"}; do set -- $cfg; echo "K=$1 rows=$2 PD=$3 zchunk=$4"; python bench.py --no-cpu-baseline --steps 5 --tb $1 --tb-rows $2 --tb-prefetch $3 --tb-zchunk $4 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
     tests2d) step pytest_2d 900 python -m pytest tests -m gpu -q -k "jacobi2d or rbgs2d or time_step or golden" ;;
     sweep2d) step sweep2d 900 bash -c 'for K in ${K2D:-8 10 12}; do echo "K=$K"; python bench.py --workload jacobi2d_8192_f64 --no-cpu-baseline --steps 3 --tb $K | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
+    testslocal) step pytest_local 900 python -m pytest tests -m gpu -q -x -k "local_group" ;;
     testsgs) step pytest_gs 900 python -m pytest tests -m gpu -q -k "rbgs or slab" ;;
     benchgs) step benchgs 600 python bench.py --workload rbgs3d_1024 ;;
     gssweep) step gssweep 900 bash -c 'for cfg in "0 0" "2 13" "4 0" "4 16" "2 18" "2 20" "2 28"; do set -- $cfg; echo "tb=$1 rows=$2"; python bench.py --workload rbgs3d_1024 --no-cpu-baseline --steps 3 --tb $1 --tb-rows $2 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*\|iterations_done_last_step\": [0-9]*" | tr "\n" " "; echo; done' ;;

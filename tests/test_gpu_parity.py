@@ -582,3 +582,86 @@ def test_slab_rbgs_rccl_single_rank(overlap, ghost, steps, tol):
         assert np.array_equal(host(sg.owned()), ref)
     finally:
         comm.close()
+
+
+# ------------------------------------------------- multi-rank, one GPU (threads)
+def _run_local_group(R, make, run):
+    """R ranks of an in-process slab group (cfd_comm_init_local), one host
+    thread and one stream per rank, running the real slab drivers."""
+    import threading
+    comms = S.LocalComm.group(R)
+    solvers = [make(r, comms[r]) for r in range(R)]
+    streams = [torch.cuda.Stream() for _ in range(R)]
+    torch.cuda.synchronize()
+    errs = [None] * R
+
+    def work(r):
+        try:
+            with torch.cuda.stream(streams[r]):
+                run(solvers[r])
+            streams[r].synchronize()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs[r] = e
+
+    threads = [threading.Thread(target=work, args=(r,)) for r in range(R)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=600)
+    torch.cuda.synchronize()
+    for c in comms:
+        c.close()
+    assert not any(t.is_alive() for t in threads), "a rank hung"
+    assert errs == [None] * R, errs
+    return solvers
+
+
+@pytest.mark.parametrize("R", [2, 3, 4])
+@pytest.mark.parametrize("ghost", [1, 2, 3, 4])
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("iters", [7, 12])
+def test_slab_jacobi_local_group_multirank(R, ghost, overlap, iters):
+    """cfd_slab_jacobi3d_f32 with R real ranks (threads on one GPU, device
+    copies for the send/recv pairs): the owned planes, gathered, equal the
+    single-domain oracle bit for bit -- K-level passes, boundary-first overlap,
+    remainders."""
+    nz, ny, nx = 41, 30, 72
+    rng = np.random.default_rng(40 + R)
+    div = rng.standard_normal((nz, ny, nx)).astype(np.float32)
+    ref = oracle.jacobi3d(div, h=0.05, dt=np.float32(1e-3), iters=iters)
+
+    def make(r, comm):
+        plan = S.SlabPlan(nz, R, r, ghost=ghost)
+        sj = S.SlabJacobi3D(plan, ny, nx, 0.05, np.float32(1e-3), comm)
+        sj.div.copy_(dev(plan.scatter(div)))
+        return sj
+
+    sols = _run_local_group(R, make, lambda sj: sj.solve(iters, overlap=overlap))
+    got = np.concatenate([host(sj.owned()) for sj in sols])
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("R", [2, 3])
+@pytest.mark.parametrize("ghost,steps", [(1, 0), (2, 0), (2, 2), (4, 4)])
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("tol,iters", [(0.0, 9), (2e-5, 300), (1.5e-5, 300)])
+def test_slab_rbgs_local_group_multirank(R, ghost, steps, overlap, tol, iters):
+    """cfd_slab_rbgs3d_f32 with R real ranks on one GPU: global colours, the
+    global stop rule through the max-allreduce, the rollback of a stop inside
+    a pair pass -- bit-identical to the oracle, same count on every rank."""
+    call("cfd_set_jacobi3d_blocking", steps, 13 if steps == 2 else 0, 0)
+    nz, ny, nx = 30, 26, 40
+    rng = np.random.default_rng(11)
+    div = rng.standard_normal((nz, ny, nx)).astype(np.float32) * np.float32(1e-3)
+    ref, n_ref = oracle.rbgs3d(div, dx=0.05, dy=0.05, dz=0.05, dt=np.float32(1e-2), iters=iters, tol=tol)
+
+    def make(r, comm):
+        plan = S.SlabPlan(nz, R, r, ghost=ghost)
+        sg = S.SlabRBGS3D(plan, ny, nx, 0.05, 0.05, 0.05, np.float32(1e-2), comm)
+        sg.div.copy_(dev(plan.scatter(div)))
+        return sg
+
+    sols = _run_local_group(R, make, lambda sg: sg.solve(iters, tolerance=tol, overlap=overlap))
+    assert [int(host(sg.iters_done)[0]) for sg in sols] == [n_ref] * R
+    got = np.concatenate([host(sg.owned()) for sg in sols])
+    assert np.array_equal(got, ref)
