@@ -22,7 +22,7 @@ step() {
 for s in "$@"; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -x ;;
+    tests) step pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread ;;
     testsq) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
     bench) step bench 600 python bench.py ;;
     bench512) step bench512 600 python bench.py --workload jacobi3d_512 --no-cpu-baseline ;;
