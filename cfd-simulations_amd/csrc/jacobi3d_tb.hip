@@ -34,8 +34,25 @@
 
 namespace cfd {
 
-__device__ inline float4 ldg4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-__device__ inline void stg4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+// explicit global address space (never flat_load / flat_store)
+typedef float gv4f __attribute__((ext_vector_type(4)));
+__device__ inline float4 ldg4(const float *p) {
+    const gv4f r = *(const __attribute__((address_space(1))) gv4f *)p;
+    return make_float4(r.x, r.y, r.z, r.w);
+}
+__device__ inline void stg4(float *p, float4 v) {
+    const gv4f r = {v.x, v.y, v.z, v.w};
+    *(__attribute__((address_space(1))) gv4f *)p = r;
+}
+
+// Zero unless c.  A `c ? ldg4(p) : zero` with the zero vector captured by
+// reference (an addressable local) was folded into a load from a select of
+// addresses, i.e. a flat_load from scratch or HBM.
+__device__ inline float4 ldg4_if(bool c, const float *p) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c) v = ldg4(p);
+    return v;
+}
 __device__ inline float4 lds4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
@@ -154,7 +171,7 @@ __global__ __launch_bounds__((W + 3) * 64) void jacobi3d_tb2(Tb2Args a) {
         for (int z = zs; z <= z1; ++z) {
             const int zp = z + PD - 1;  // this step fetches what step zp+1 needs
             if (ld_ok && zp + 1 <= z1) {
-                const float4 nc = (zp + 2 <= nz - 1) ? ldg4(P(zp + 2) + rofs) : z4;
+                const float4 nc = ldg4_if(zp + 2 <= nz - 1, P(zp + 2) + rofs);
                 const float4 nd = ldg4(R(zp + 1) + rofs);
                 if constexpr (PD == 2) { c3 = nc; d2 = nd; } else { cpp = nc; dnext = nd; }
             }
@@ -276,9 +293,9 @@ __global__ __launch_bounds__((W + 3) * 64) void jacobi3d_tb2(Tb2Args a) {
         for (int z = zs; z <= z1; ++z) {
             const int zp = z + PD - 1;
             if (zp + 1 <= z1) {
-                const float4 nlo = elo ? ldg4(P(zp + 1) + olo) : z4;
-                const float4 nhi = ehi ? ldg4(P(zp + 1) + ohi) : z4;
-                const float4 nh = (hon && zp + 2 <= nz - 1) ? ldg4(P(zp + 2) + hofs) : z4;
+                const float4 nlo = ldg4_if(elo, P(zp + 1) + olo);
+                const float4 nhi = ldg4_if(ehi, P(zp + 1) + ohi);
+                const float4 nh = ldg4_if(hon && zp + 2 <= nz - 1, P(zp + 2) + hofs);
                 const float nr = (hon && l1row) ? R(zp + 1)[rhofs] : 0.f;
                 if constexpr (PD == 2) { lo2 = nlo; hi2 = nhi; h3 = nh; rh2 = nr; }
                 else { lon = nlo; hin = nhi; hpp = nh; rhn = nr; }

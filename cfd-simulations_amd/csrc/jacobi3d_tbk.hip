@@ -32,8 +32,25 @@ namespace cfd {
 
 namespace {
 
-__device__ inline float4 ldg4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-__device__ inline void stg4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+// explicit global address space (never flat_load / flat_store)
+typedef float gv4f __attribute__((ext_vector_type(4)));
+__device__ inline float4 ldg4(const float *p) {
+    const gv4f r = *(const __attribute__((address_space(1))) gv4f *)p;
+    return make_float4(r.x, r.y, r.z, r.w);
+}
+__device__ inline void stg4(float *p, float4 v) {
+    const gv4f r = {v.x, v.y, v.z, v.w};
+    *(__attribute__((address_space(1))) gv4f *)p = r;
+}
+
+// Zero unless c.  A `c ? ldg4(p) : zero` with the zero vector captured by
+// reference (an addressable local) was folded into a load from a select of
+// addresses, i.e. a flat_load from scratch or HBM.
+__device__ inline float4 ldg4_if(bool c, const float *p) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c) v = ldg4(p);
+    return v;
+}
 __device__ inline float4 lds4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
@@ -137,8 +154,8 @@ __global__ __launch_bounds__((W + 2 * K - 1) * 64) void jacobi3d_tbk(TbkArgs a) 
         const bool int_row = y >= 1 && y <= ny - 2;
         const bool out_row = r >= K && r < NR - K && y <= ny - 2;
         const size_t rofs = (size_t)(rowin ? y : 0) * nx + (xin ? x : 0);
-        auto ldp = [&](int p) { return (ld && p >= 0 && p <= nz - 1) ? ldg4(P(p) + rofs) : z4; };
-        auto ldr = [&](int p) { return (ld && p >= 0 && p <= nz - 1) ? ldg4(R(p) + rofs) : z4; };
+        auto ldp = [&](int p) { return ldg4_if(ld && p >= 0 && p <= nz - 1, P(p) + rofs); };
+        auto ldr = [&](int p) { return ldg4_if(ld && p >= 0 && p <= nz - 1, R(p) + rofs); };
         float4 Q[K][3];   // Q[l][j] = level l of plane (z - l) - 1 + j, for the level-(l+1) update
         float4 Rq[K];     // Rq[j] = rhs of plane z - j
 #pragma unroll
@@ -218,10 +235,10 @@ __global__ __launch_bounds__((W + 2 * K - 1) * 64) void jacobi3d_tbk(TbkArgs a) 
         const size_t hofs = (size_t)(hon ? yr : 0) * nx + (hon ? hx : 0);
         const int col = side ? 260 : 0;  // chunk position in an LDS row
         auto ldh = [&](const float *base, int p) {
-            return (hon && p >= 0 && p <= nz - 1) ? ldg4(base + (size_t)p * plane + hofs) : z4;
+            return ldg4_if(hon && p >= 0 && p <= nz - 1, base + (size_t)p * plane + hofs);
         };
-        auto ldlo = [&](int p) { return (elo && p >= 0 && p <= nz - 1) ? ldg4(P(p) + olo) : z4; };
-        auto ldhi = [&](int p) { return (ehi && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ohi) : z4; };
+        auto ldlo = [&](int p) { return ldg4_if(elo && p >= 0 && p <= nz - 1, P(p) + olo); };
+        auto ldhi = [&](int p) { return ldg4_if(ehi && p >= 0 && p <= nz - 1, P(p) + ohi); };
         float4 lo = ldlo(zs), hi = ldhi(zs);
         float4 H[K][3];
         float4 Hr[K];

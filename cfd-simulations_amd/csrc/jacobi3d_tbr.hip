@@ -21,6 +21,8 @@
 // the halo wave, the z-march bounds, Dirichlet copies, erosion of garbage --
 // is as in jacobi3d_tbk.hip, and the result is bit-identical to K single
 // sweeps (tests/test_gpu_parity.py).
+#include <type_traits>
+
 #include "internal.hpp"
 
 namespace cfd {
@@ -31,6 +33,70 @@ __device__ inline float4 ldg4(const float *p) { return *reinterpret_cast<const f
 __device__ inline void stg4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 __device__ inline float4 lds4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+
+// Plane rows through buffer resources: one resource per (array, plane) in
+// SGPRs with num_records = the plane's bytes (0 for a plane outside the
+// array); a lane outside the grid passes kOob and reads 0, with no branch.
+constexpr uint32_t kOob = 0x80000000u;
+typedef float gv4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ inline __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, int p, int nz, size_t plane) {
+    const bool in = p >= 0 && p <= nz - 1;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(in ? base + (size_t)p * plane : base),
+                                             (short)0, in ? (int)(plane * sizeof(float)) : 0, 0x00020000);
+}
+__device__ inline float4 ldb4(__amdgpu_buffer_rsrc_t r, uint32_t byte_ofs) {
+    const gv4f v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_ofs, 0, 0);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+// LDS-DMA of one 1 KiB row (64 lanes x 16 B) into lds_row[0..255]: the data
+// lands in LDS without passing through VGPRs (buffer_load_dwordx4 ... lds,
+// destination M0 + 16 * lane).  Issued as inline asm on purpose: for a DMA the
+// compiler can see, the waitcnt pass cannot tell the level tiles from the
+// staging buffers and drains every DMA (vmcnt(0)) before each tile access.
+// Consumers wait with wait_vmcnt<> themselves; the compiler's own vmcnt
+// counts only grow stricter with the extra in-flight operations.
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+__device__ inline v4i32 plane_rsrc4(const float *base, int p, int nz, size_t plane) {
+    const bool in = p >= 0 && p <= nz - 1;
+    const unsigned long long b = (unsigned long long)(in ? base + (size_t)p * plane : base);
+    v4i32 r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    r.y = __builtin_amdgcn_readfirstlane((int)((unsigned)(b >> 32) & 0xffffu));  // stride 0
+    r.z = __builtin_amdgcn_readfirstlane(in ? (int)(plane * sizeof(float)) : 0);
+    r.w = 0x00020000;
+    return r;
+}
+__device__ inline void dma_row(v4i32 rs, uint32_t byte_ofs, float *lds_row) {
+    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float *)lds_row;
+    int saved;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "s"(__builtin_amdgcn_readfirstlane(la)), "v"(byte_ofs), "s"(rs)
+        : "memory");
+}
+// s_waitcnt vmcnt(N) (expcnt, lgkmcnt: no wait)
+template <int N>
+__device__ inline void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+// LDS barrier that leaves LDS-DMA in flight (__syncthreads' fence would wait
+// vmcnt(0)); the memory clobber keeps the compiler's LDS accesses in place
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// x-neighbours across lanes by DPP (wave_shr:1 / wave_shl:1) instead of
+// ds_bpermute: lane i gets lane i-1's (from_lower) or lane i+1's (from_upper)
+// value; lane 0 / 63 get 0 and are overwritten from LDS by the caller
+__device__ inline float dpp_from_lower(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ inline float dpp_from_upper(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
 
 enum { kJacobi = 0, kRbgs = 1 };
 
@@ -110,6 +176,122 @@ __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S
 
 }  // namespace
 
+// The halo wave of jacobi3d_tbr (see there): loads the two outermost level-0
+// rows and the 4-float x-halo chunks of every row, and computes levels
+// 1..K-1 of the chunks, in lock step (two barriers per step) with the row waves.
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE>
+__device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0, int z1, int y0, int xs) {
+    constexpr int NR = NWR * RPW + 2;
+    constexpr int RS = 264;
+    auto T = [&](int l, int r) -> float * {
+        int base = 0;
+#pragma unroll
+        for (int m = 0; m < K; ++m)
+            if (m < l) base += (NR - 2 * m) * RS;
+        return smem + base + (r - l) * RS;
+    };
+    const int nz = a.nz, ny = a.ny, nx = a.nx;
+    const int lane = threadIdx.x & 63;
+    const int x = xs + 4 * lane;
+    const bool xin = x < nx;
+    const size_t plane = (size_t)ny * nx;
+    const int zs = z0 - K + 1, zl = z1 + K - 2;
+    auto P = [&](int p) { return a.in + (size_t)p * plane; };
+    auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    // ------------------------------------------------------------ halo wave
+    const int ylo = y0 - K, yhi = y0 - K + NR - 1;
+    const bool elo = xin && ylo >= 0 && ylo <= ny - 1;
+    const bool ehi = xin && yhi >= 0 && yhi <= ny - 1;
+    const size_t olo = (size_t)(elo ? ylo : 0) * nx + (xin ? x : 0);
+    const size_t ohi = (size_t)(ehi ? yhi : 0) * nx + (xin ? x : 0);
+    const int hr = lane >> 1, side = lane & 1;
+    const int yr = y0 - K + hr;
+    const bool hact = lane < 2 * NR;
+    const bool hon = hact && yr >= 0 && yr <= ny - 1 && (side ? xs + 256 < nx : xs > 0);
+    const bool hint = hon && yr >= 1 && yr <= ny - 2;
+    const int hx = side ? xs + 256 : xs - 4;
+    const size_t hofs = (size_t)(hon ? yr : 0) * nx + (hon ? hx : 0);
+    const int col = side ? 260 : 0;
+    auto ldh = [&](const float *base, int p) {
+        return (hon && p >= 0 && p <= nz - 1) ? ldg4(base + (size_t)p * plane + hofs) : z4;
+    };
+    auto ldlo = [&](int p) { return (elo && p >= 0 && p <= nz - 1) ? ldg4(P(p) + olo) : z4; };
+    auto ldhi = [&](int p) { return (ehi && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ohi) : z4; };
+    float4 lo = ldlo(zs), hi = ldhi(zs);
+    float4 H[K][3];
+    float4 Hr[K];
+#pragma unroll
+    for (int l = 0; l < K; ++l) H[l][0] = H[l][1] = H[l][2] = z4;
+    H[0][0] = ldh(a.in, zs - 1);
+    H[0][1] = ldh(a.in, zs);
+    H[0][2] = ldh(a.in, zs + 1);
+#pragma unroll
+    for (int i = 0; i < K; ++i) Hr[i] = ldh(a.div, zs - i);
+    float4 Lq[PD], Uq[PD], Hq[PD], Rn[PD];
+#pragma unroll
+    for (int i = 0; i + 1 < PD; ++i) {
+        Lq[i] = ldlo(zs + 1 + i);
+        Uq[i] = ldhi(zs + 1 + i);
+        Hq[i] = ldh(a.in, zs + 2 + i);
+        Rn[i] = ldh(a.div, zs + 1 + i);
+    }
+    for (int z = zs; z <= zl; ++z) {
+        Lq[PD - 1] = ldlo(z + PD);
+        Uq[PD - 1] = ldhi(z + PD);
+        Hq[PD - 1] = ldh(a.in, z + 1 + PD);
+        Rn[PD - 1] = ldh(a.div, z + PD);
+        // phase W
+        if (elo) sts4(T(0, 0) + 4 + 4 * lane, lo);
+        if (ehi) sts4(T(0, NR - 1) + 4 + 4 * lane, hi);
+        if (hon) {
+            sts4(T(0, hr) + col, H[0][1]);
+#pragma unroll
+            for (int l = 1; l < K; ++l)
+                if (hr >= l && hr < NR - l) sts4(T(l, hr) + col, H[l][2]);
+        }
+        __syncthreads();
+        // phase R: levels 1..K-1 of the halo chunks
+#pragma unroll
+        for (int l = 1; l < K; ++l) {
+            const int p = z - l + 1;
+            if (hact && hr >= l && hr < NR - l) {
+                const float4 c = H[l - 1][1];
+                const float inner = T(l - 1, hr)[side ? 259 : 4];
+                float4 v = c;
+                if (hon) {
+                    const float4 N = lds4(T(l - 1, hr + 1) + col);
+                    const float4 S = lds4(T(l - 1, hr - 1) + col);
+                    float dummy = 0.f;
+                    v = level4<MODE, PRE>(c, side ? inner : 0.f, side ? 0.f : inner, N, S,
+                                          H[l - 1][2], H[l - 1][0], Hr[l - 1], hx, nx,
+                                          hint && !fixedp(p), a,
+                                          (a.zoff + p + yr + 1 + ((l - 1) & 1)) & 1, false, dummy);
+                }
+                H[l][0] = H[l][1];
+                H[l][1] = H[l][2];
+                H[l][2] = v;
+            }
+        }
+        __syncthreads();
+        lo = Lq[0];
+        hi = Uq[0];
+        H[0][0] = H[0][1];
+        H[0][1] = H[0][2];
+        H[0][2] = Hq[0];
+#pragma unroll
+        for (int i = K - 1; i > 0; --i) Hr[i] = Hr[i - 1];
+        Hr[0] = Rn[0];
+#pragma unroll
+        for (int i = 0; i + 1 < PD; ++i) {
+            Lq[i] = Lq[i + 1];
+            Uq[i] = Uq[i + 1];
+            Hq[i] = Hq[i + 1];
+            Rn[i] = Rn[i + 1];
+        }
+    }
+}
+
 // (A double-buffered, one-barrier-per-step version of the (3, 11, 2) shape --
 // 139 KB of LDS -- was measured at 1007 against 1131 Gcell/s for this one.)
 // MODE kRbgs: K/2 red-black iterations per pass (level l = colour (l-1)&1);
@@ -127,6 +309,16 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         return t;
     }();
     __shared__ __attribute__((aligned(16))) float smem[TOTAL];
+    // DMA staging (row waves, when it fits in LDS with the level tiles): the
+    // level-0 row of plane z + 2 and the rhs row of plane z + 1 are fetched by
+    // LDS-DMA at the start of step z into the even/odd buffers and read at
+    // step z + 1, so a fetch has a whole step in flight and holds no VGPRs.
+    // Separate arrays per parity let the compiler see that step z's reads do
+    // not alias step z's DMA (no vmcnt(0) before them).
+    constexpr int SR_ = NR - 2;  // rows 1 .. NR-2 (the row waves' rows)
+    constexpr bool DMA = PD == 1 && (TOTAL + 4 * SR_ * 256) * 4 <= 160 * 1024;
+    constexpr int SST = DMA ? SR_ * 256 : 4;
+    __shared__ __attribute__((aligned(16))) float st_p0[SST], st_p1[SST], st_r0[SST], st_r1[SST];
     // level l keeps rows [l, NR - l)
     auto T = [&](int l, int r) -> float * {
         int base = 0;
@@ -178,203 +370,244 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     for (int i = 0; i < NIT; ++i) chg[i] = 0.f;
 
     if (wv < NWR) {
-        // ------------------------------------------------------------ row wave
-        int rr[RPW];
-        size_t ofs[RPW];
-        bool ld[RPW], irow[RPW], orow[RPW];
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            rr[j] = 1 + wv + j * NWR;
-            const int y = y0 - K + rr[j];
-            const bool rowin = y >= 0 && y <= ny - 1;
-            ld[j] = xin && rowin;
-            irow[j] = y >= 1 && y <= ny - 2;
-            orow[j] = rr[j] >= K && rr[j] < NR - K && y <= ny - 2 && xin;
-            ofs[j] = (size_t)(rowin ? y : 0) * nx + (xin ? x : 0);
-        }
-        auto ldp = [&](int j, int p) {
-            return (ld[j] && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ofs[j]) : z4;
-        };
-        auto ldr = [&](int j, int p) {
-            return (ld[j] && p >= 0 && p <= nz - 1) ? ldg4(a.div + (size_t)p * plane + ofs[j]) : z4;
-        };
-        float4 Q[RPW][K][3];  // Q[j][l][i] = level l of plane (z - l) - 1 + i, row j
-        float4 Rq[RPW][K];    // Rq[j][i] = rhs of plane z - i
-        float4 Cq[RPW][PD], Rn[RPW][PD];
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-#pragma unroll
-            for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = z4;
-            Q[j][0][0] = ldp(j, zs - 1);
-            Q[j][0][1] = ldp(j, zs);
-            Q[j][0][2] = ldp(j, zs + 1);
-#pragma unroll
-            for (int i = 0; i < K; ++i) Rq[j][i] = ldr(j, zs - i);
-#pragma unroll
-            for (int i = 0; i + 1 < PD; ++i) {
-                Cq[j][i] = ldp(j, zs + 2 + i);
-                Rn[j][i] = ldr(j, zs + 1 + i);
-            }
-        }
-        for (int z = zs; z <= zl; ++z) {
+        if constexpr (DMA) {
+            // --------------------------------------------- row wave, DMA-staged
+            int rr[RPW];
+            uint32_t bo[RPW], so[RPW];  // load / store byte offsets in a plane, kOob outside
+            bool irow[RPW], orow[RPW];
 #pragma unroll
             for (int j = 0; j < RPW; ++j) {
-                Cq[j][PD - 1] = ldp(j, z + 1 + PD);
-                Rn[j][PD - 1] = ldr(j, z + PD);
+                rr[j] = 1 + wv + j * NWR;
+                const int y = y0 - K + rr[j];
+                const bool rowin = y >= 0 && y <= ny - 1;
+                irow[j] = y >= 1 && y <= ny - 2;
+                orow[j] = rr[j] >= K && rr[j] < NR - K && y <= ny - 2 && xin;
+                const uint32_t o = (uint32_t)(((size_t)(rowin ? y : 0) * nx + (xin ? x : 0)) * sizeof(float));
+                bo[j] = xin && rowin ? o : kOob;
+                so[j] = orow[j] ? o : kOob;
             }
-            // phase W
+            // V[j][i]: level 0 of plane z-1+i; Q[j][l][i]: level l of plane
+            // (z-l)-1+i after level l is computed; Rq[j][i]: rhs of plane z-i
+            float4 V[RPW][3], Q[RPW][K][3], Rq[RPW][K];
 #pragma unroll
             for (int j = 0; j < RPW; ++j) {
-                if (ld[j]) sts4(T(0, rr[j]) + 4 + 4 * lane, Q[j][0][1]);
 #pragma unroll
-                for (int l = 1; l < K; ++l)
-                    if (xin && rr[j] >= l && rr[j] < NR - l) sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][2]);
+                for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = z4;
+                V[j][0] = ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]);
+                V[j][1] = ldb4(plane_rsrc(a.in, zs, nz, plane), bo[j]);
+                V[j][2] = z4;
+                Rq[j][0] = z4;
+#pragma unroll
+                for (int i = 1; i < K; ++i) Rq[j][i] = ldb4(plane_rsrc(a.div, zs - i, nz, plane), bo[j]);
+                // read at step zs (even): plane zs + 1 and rhs zs in the odd buffers
+                dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], st_p1 + (rr[j] - 1) * 256);
+                dma_row(plane_rsrc4(a.div, zs, nz, plane), bo[j], st_r1 + (rr[j] - 1) * 256);
             }
-            __syncthreads();
-            // phase R
+            auto step = [&](int z, auto parc) {
+                constexpr int E = decltype(parc)::value;  // (z - zs) & 1
+                float *const pw = E ? st_p1 : st_p0;
+                float *const rw = E ? st_r1 : st_r0;
+                const float *const pr = E ? st_p0 : st_p1;
+                const float *const rdr = E ? st_r0 : st_r1;
+                {
+                    const v4i32 rp = plane_rsrc4(a.in, z + 2, nz, plane);
+                    const v4i32 rd = plane_rsrc4(a.div, z + 1, nz, plane);
 #pragma unroll
-            for (int l = 1; l <= K; ++l) {
-                const int p = z - l + 1;
-                const bool fx = fixedp(p);
+                    for (int j = 0; j < RPW; ++j) {
+                        dma_row(rp, bo[j], pw + (rr[j] - 1) * 256);
+                        dma_row(rd, bo[j], rw + (rr[j] - 1) * 256);
+                    }
+                }
+                // phase W: level 0 of plane z and level l of plane z - l
 #pragma unroll
                 for (int j = 0; j < RPW; ++j) {
-                    const int r = rr[j];
-                    if (r >= l && r < NR - l) {
-                        const float4 c = Q[j][l - 1][1];
-                        float wl = __shfl_up(c.w, 1, 64);
-                        float er = __shfl_down(c.x, 1, 64);
-                        const float *row = T(l - 1, r);
-                        const float wl_l = row[3], er_l = row[260];
-                        if (lane == 0) wl = wl_l;
-                        if (lane == 63) er = er_l;
-                        float4 v = c;
-                        if (xin) {
-                            const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
-                            const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
-                            const int y = y0 - K + r;
-                            v = level4<MODE, PRE>(c, wl, er, N, S, Q[j][l - 1][2], Q[j][l - 1][0],
-                                                  Rq[j][l - 1], x, nx, irow[j] && !fx, a,
-                                                  (a.zoff + p + y + 1 + ((l - 1) & 1)) & 1,
-                                                  orow[j] && p >= z0 && p < z1, chg[(l - 1) / 2]);
-                        }
-                        if (l < K) {
-                            Q[j][l][0] = Q[j][l][1];
-                            Q[j][l][1] = Q[j][l][2];
-                            Q[j][l][2] = v;
-                        } else if (orow[j] && p >= z0 && p < z1) {
-                            stg4(a.out + (size_t)p * plane + ofs[j], v);
+                    if (xin) sts4(T(0, rr[j]) + 4 + 4 * lane, V[j][1]);
+#pragma unroll
+                    for (int l = 1; l < K; ++l)
+                        if (xin && rr[j] >= l && rr[j] < NR - l) sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][2]);
+                }
+                // the previous step's DMAs have landed once at most this step's
+                // 2 * RPW remain in flight (they are issued in order)
+                wait_vmcnt<2 * RPW>();
+                lds_barrier();
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) {
+                    V[j][2] = lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
+#pragma unroll
+                    for (int i = K - 1; i > 0; --i) Rq[j][i] = Rq[j][i - 1];
+                    Rq[j][0] = lds4(rdr + (rr[j] - 1) * 256 + 4 * lane);
+                }
+                // phase R: level l of plane p = z - l + 1
+#pragma unroll
+                for (int l = 1; l <= K; ++l) {
+                    const int p = z - l + 1;
+                    const bool fx = fixedp(p);
+#pragma unroll
+                    for (int j = 0; j < RPW; ++j) {
+                        const int r = rr[j];
+                        if (r >= l && r < NR - l) {
+                            const float4 c = l == 1 ? V[j][1] : Q[j][l - 1][1];
+                            const float4 U = l == 1 ? V[j][2] : Q[j][l - 1][2];
+                            const float4 D = l == 1 ? V[j][0] : Q[j][l - 1][0];
+                            float wl = dpp_from_lower(c.w);
+                            float er = dpp_from_upper(c.x);
+                            const float *row = T(l - 1, r);
+                            const float wl_l = row[3], er_l = row[260];
+                            if (lane == 0) wl = wl_l;
+                            if (lane == 63) er = er_l;
+                            float4 v = c;
+                            if (xin) {
+                                const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
+                                const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
+                                const int y = y0 - K + r;
+                                v = level4<MODE, PRE>(c, wl, er, N, S, U, D, Rq[j][l - 1], x, nx,
+                                                      irow[j] && !fx, a,
+                                                      (a.zoff + p + y + 1 + ((l - 1) & 1)) & 1,
+                                                      orow[j] && p >= z0 && p < z1, chg[(l - 1) / 2]);
+                            }
+                            if (l < K) {
+                                Q[j][l][0] = Q[j][l][1];
+                                Q[j][l][1] = Q[j][l][2];
+                                Q[j][l][2] = v;
+                            } else {
+                                // unconditional buffer store: rows, lanes and planes this
+                                // tile does not own fall out of range and are dropped
+                                const bool own = p >= z0 && p < z1;
+                                const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+                                    a.out + (size_t)(own ? p : 0) * plane, (short)0,
+                                    own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
+                                const gv4f vv = {v.x, v.y, v.z, v.w};
+                                __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, 0);
+                            }
+                            // one (level, row) at a time: measured 0.4 % faster than
+                            // letting the scheduler interleave them
+                            __builtin_amdgcn_sched_barrier(0);
                         }
                     }
                 }
+                lds_barrier();
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) {
+                    V[j][0] = V[j][1];
+                    V[j][1] = V[j][2];
+                }
+            };
+            for (int zb = zs; zb <= zl; zb += 2) {
+                step(zb, std::integral_constant<int, 0>{});
+                if (zb + 1 <= zl) step(zb + 1, std::integral_constant<int, 1>{});
             }
-            __syncthreads();
+            wait_vmcnt<0>();  // no LDS-DMA outlives the wave
+        } else {
+            // ------------------------------------------------------------ row wave
+            int rr[RPW];
+            size_t ofs[RPW];
+            bool ld[RPW], irow[RPW], orow[RPW];
 #pragma unroll
             for (int j = 0; j < RPW; ++j) {
-                Q[j][0][0] = Q[j][0][1];
-                Q[j][0][1] = Q[j][0][2];
-                Q[j][0][2] = Cq[j][0];
+                rr[j] = 1 + wv + j * NWR;
+                const int y = y0 - K + rr[j];
+                const bool rowin = y >= 0 && y <= ny - 1;
+                ld[j] = xin && rowin;
+                irow[j] = y >= 1 && y <= ny - 2;
+                orow[j] = rr[j] >= K && rr[j] < NR - K && y <= ny - 2 && xin;
+                ofs[j] = (size_t)(rowin ? y : 0) * nx + (xin ? x : 0);
+            }
+            auto ldp = [&](int j, int p) {
+                return (ld[j] && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ofs[j]) : z4;
+            };
+            auto ldr = [&](int j, int p) {
+                return (ld[j] && p >= 0 && p <= nz - 1) ? ldg4(a.div + (size_t)p * plane + ofs[j]) : z4;
+            };
+            float4 Q[RPW][K][3];  // Q[j][l][i] = level l of plane (z - l) - 1 + i, row j
+            float4 Rq[RPW][K];    // Rq[j][i] = rhs of plane z - i
+            float4 Cq[RPW][PD], Rn[RPW][PD];
 #pragma unroll
-                for (int i = K - 1; i > 0; --i) Rq[j][i] = Rq[j][i - 1];
-                Rq[j][0] = Rn[j][0];
+            for (int j = 0; j < RPW; ++j) {
+#pragma unroll
+                for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = z4;
+                Q[j][0][0] = ldp(j, zs - 1);
+                Q[j][0][1] = ldp(j, zs);
+                Q[j][0][2] = ldp(j, zs + 1);
+#pragma unroll
+                for (int i = 0; i < K; ++i) Rq[j][i] = ldr(j, zs - i);
 #pragma unroll
                 for (int i = 0; i + 1 < PD; ++i) {
-                    Cq[j][i] = Cq[j][i + 1];
-                    Rn[j][i] = Rn[j][i + 1];
+                    Cq[j][i] = ldp(j, zs + 2 + i);
+                    Rn[j][i] = ldr(j, zs + 1 + i);
+                }
+            }
+            for (int z = zs; z <= zl; ++z) {
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) {
+                    Cq[j][PD - 1] = ldp(j, z + 1 + PD);
+                    Rn[j][PD - 1] = ldr(j, z + PD);
+                }
+                // phase W
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) {
+                    if (ld[j]) sts4(T(0, rr[j]) + 4 + 4 * lane, Q[j][0][1]);
+#pragma unroll
+                    for (int l = 1; l < K; ++l)
+                        if (xin && rr[j] >= l && rr[j] < NR - l) sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][2]);
+                }
+                __syncthreads();
+                // phase R
+#pragma unroll
+                for (int l = 1; l <= K; ++l) {
+                    const int p = z - l + 1;
+                    const bool fx = fixedp(p);
+#pragma unroll
+                    for (int j = 0; j < RPW; ++j) {
+                        const int r = rr[j];
+                        if (r >= l && r < NR - l) {
+                            const float4 c = Q[j][l - 1][1];
+                            float wl = __shfl_up(c.w, 1, 64);
+                            float er = __shfl_down(c.x, 1, 64);
+                            const float *row = T(l - 1, r);
+                            const float wl_l = row[3], er_l = row[260];
+                            if (lane == 0) wl = wl_l;
+                            if (lane == 63) er = er_l;
+                            float4 v = c;
+                            if (xin) {
+                                const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
+                                const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
+                                const int y = y0 - K + r;
+                                v = level4<MODE, PRE>(c, wl, er, N, S, Q[j][l - 1][2], Q[j][l - 1][0],
+                                                      Rq[j][l - 1], x, nx, irow[j] && !fx, a,
+                                                      (a.zoff + p + y + 1 + ((l - 1) & 1)) & 1,
+                                                      orow[j] && p >= z0 && p < z1, chg[(l - 1) / 2]);
+                            }
+                            if (l < K) {
+                                Q[j][l][0] = Q[j][l][1];
+                                Q[j][l][1] = Q[j][l][2];
+                                Q[j][l][2] = v;
+                            } else if (orow[j] && p >= z0 && p < z1) {
+                                stg4(a.out + (size_t)p * plane + ofs[j], v);
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) {
+                    Q[j][0][0] = Q[j][0][1];
+                    Q[j][0][1] = Q[j][0][2];
+                    Q[j][0][2] = Cq[j][0];
+#pragma unroll
+                    for (int i = K - 1; i > 0; --i) Rq[j][i] = Rq[j][i - 1];
+                    Rq[j][0] = Rn[j][0];
+#pragma unroll
+                    for (int i = 0; i + 1 < PD; ++i) {
+                        Cq[j][i] = Cq[j][i + 1];
+                        Rn[j][i] = Rn[j][i + 1];
+                    }
                 }
             }
         }
     } else {
-        // ------------------------------------------------------------ halo wave
-        const int ylo = y0 - K, yhi = y0 - K + NR - 1;
-        const bool elo = xin && ylo >= 0 && ylo <= ny - 1;
-        const bool ehi = xin && yhi >= 0 && yhi <= ny - 1;
-        const size_t olo = (size_t)(elo ? ylo : 0) * nx + (xin ? x : 0);
-        const size_t ohi = (size_t)(ehi ? yhi : 0) * nx + (xin ? x : 0);
-        const int hr = lane >> 1, side = lane & 1;
-        const int yr = y0 - K + hr;
-        const bool hact = lane < 2 * NR;
-        const bool hon = hact && yr >= 0 && yr <= ny - 1 && (side ? xs + 256 < nx : xs > 0);
-        const bool hint = hon && yr >= 1 && yr <= ny - 2;
-        const int hx = side ? xs + 256 : xs - 4;
-        const size_t hofs = (size_t)(hon ? yr : 0) * nx + (hon ? hx : 0);
-        const int col = side ? 260 : 0;
-        auto ldh = [&](const float *base, int p) {
-            return (hon && p >= 0 && p <= nz - 1) ? ldg4(base + (size_t)p * plane + hofs) : z4;
-        };
-        auto ldlo = [&](int p) { return (elo && p >= 0 && p <= nz - 1) ? ldg4(P(p) + olo) : z4; };
-        auto ldhi = [&](int p) { return (ehi && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ohi) : z4; };
-        float4 lo = ldlo(zs), hi = ldhi(zs);
-        float4 H[K][3];
-        float4 Hr[K];
-#pragma unroll
-        for (int l = 0; l < K; ++l) H[l][0] = H[l][1] = H[l][2] = z4;
-        H[0][0] = ldh(a.in, zs - 1);
-        H[0][1] = ldh(a.in, zs);
-        H[0][2] = ldh(a.in, zs + 1);
-#pragma unroll
-        for (int i = 0; i < K; ++i) Hr[i] = ldh(a.div, zs - i);
-        float4 Lq[PD], Uq[PD], Hq[PD], Rn[PD];
-#pragma unroll
-        for (int i = 0; i + 1 < PD; ++i) {
-            Lq[i] = ldlo(zs + 1 + i);
-            Uq[i] = ldhi(zs + 1 + i);
-            Hq[i] = ldh(a.in, zs + 2 + i);
-            Rn[i] = ldh(a.div, zs + 1 + i);
-        }
-        for (int z = zs; z <= zl; ++z) {
-            Lq[PD - 1] = ldlo(z + PD);
-            Uq[PD - 1] = ldhi(z + PD);
-            Hq[PD - 1] = ldh(a.in, z + 1 + PD);
-            Rn[PD - 1] = ldh(a.div, z + PD);
-            // phase W
-            if (elo) sts4(T(0, 0) + 4 + 4 * lane, lo);
-            if (ehi) sts4(T(0, NR - 1) + 4 + 4 * lane, hi);
-            if (hon) {
-                sts4(T(0, hr) + col, H[0][1]);
-#pragma unroll
-                for (int l = 1; l < K; ++l)
-                    if (hr >= l && hr < NR - l) sts4(T(l, hr) + col, H[l][2]);
-            }
-            __syncthreads();
-            // phase R: levels 1..K-1 of the halo chunks
-#pragma unroll
-            for (int l = 1; l < K; ++l) {
-                const int p = z - l + 1;
-                if (hact && hr >= l && hr < NR - l) {
-                    const float4 c = H[l - 1][1];
-                    const float inner = T(l - 1, hr)[side ? 259 : 4];
-                    float4 v = c;
-                    if (hon) {
-                        const float4 N = lds4(T(l - 1, hr + 1) + col);
-                        const float4 S = lds4(T(l - 1, hr - 1) + col);
-                        float dummy = 0.f;
-                        v = level4<MODE, PRE>(c, side ? inner : 0.f, side ? 0.f : inner, N, S,
-                                              H[l - 1][2], H[l - 1][0], Hr[l - 1], hx, nx,
-                                              hint && !fixedp(p), a,
-                                              (a.zoff + p + yr + 1 + ((l - 1) & 1)) & 1, false, dummy);
-                    }
-                    H[l][0] = H[l][1];
-                    H[l][1] = H[l][2];
-                    H[l][2] = v;
-                }
-            }
-            __syncthreads();
-            lo = Lq[0];
-            hi = Uq[0];
-            H[0][0] = H[0][1];
-            H[0][1] = H[0][2];
-            H[0][2] = Hq[0];
-#pragma unroll
-            for (int i = K - 1; i > 0; --i) Hr[i] = Hr[i - 1];
-            Hr[0] = Rn[0];
-#pragma unroll
-            for (int i = 0; i + 1 < PD; ++i) {
-                Lq[i] = Lq[i + 1];
-                Uq[i] = Uq[i + 1];
-                Hq[i] = Hq[i + 1];
-                Rn[i] = Rn[i + 1];
-            }
-        }
+        // the halo wave in its own (not inlined) function, so that its
+        // registers are allocated apart from the row waves'
+        tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE>(a, smem, z0, z1, y0, xs);
     }
     if (MODE == kRbgs && a.maxc) {
         __shared__ float red[NIT][NWR + 1];
