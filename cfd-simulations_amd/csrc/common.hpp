@@ -114,6 +114,28 @@ __device__ inline int xcd_swizzle(int bid, int nblocks) {
     return (bid % kNumXcd) * per + bid / kNumXcd;
 }
 
+// x-neighbours across lanes by DPP wave shifts (a VALU modifier, a few cycles)
+// instead of ds_bpermute (__shfl_up/down go through the LDS crossbar, ~100
+// cycles each, and a K-level row march chains 2K of them): lane i receives
+// lane i-1's value (from_lower, wave_shr:1) or lane i+1's (from_upper,
+// wave_shl:1).  Lane 0 / 63 receive 0: callers overwrite them or never use them.
+__device__ inline int dpp_i32_from_lower(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }
+__device__ inline int dpp_i32_from_upper(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false); }
+__device__ inline float dpp_from_lower(float v) { return __int_as_float(dpp_i32_from_lower(__float_as_int(v))); }
+__device__ inline float dpp_from_upper(float v) { return __int_as_float(dpp_i32_from_upper(__float_as_int(v))); }
+__device__ inline double dpp_from_lower(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)dpp_i32_from_lower((int)(unsigned)b);
+    const unsigned hi = (unsigned)dpp_i32_from_lower((int)(unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ inline double dpp_from_upper(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)dpp_i32_from_upper((int)(unsigned)b);
+    const unsigned hi = (unsigned)dpp_i32_from_upper((int)(unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 inline int ceil_div(long a, long b) { return static_cast<int>((a + b - 1) / b); }
 
 }  // namespace cfd

@@ -88,16 +88,6 @@ __device__ inline void wait_vmcnt() {
 // LDS barrier that leaves LDS-DMA in flight (__syncthreads' fence would wait
 // vmcnt(0)); the memory clobber keeps the compiler's LDS accesses in place
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-// x-neighbours across lanes by DPP (wave_shr:1 / wave_shl:1) instead of
-// ds_bpermute: lane i gets lane i-1's (from_lower) or lane i+1's (from_upper)
-// value; lane 0 / 63 get 0 and are overwritten from LDS by the caller
-__device__ inline float dpp_from_lower(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
-}
-__device__ inline float dpp_from_upper(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
-}
-
 enum { kJacobi = 0, kRbgs = 1 };
 
 struct TbrArgs {

@@ -102,8 +102,8 @@ __global__ __launch_bounds__(256) void jacobi2d_march(const T *__restrict__ in, 
             }
         }
         // x-neighbours across lanes: W of element 0 from lane-1, E of the last from lane+1
-        T wl = __shfl_up(cur[VEC - 1], 1, kWave);
-        T er = __shfl_down(cur[0], 1, kWave);
+        T wl = dpp_from_lower(cur[VEC - 1]);
+        T er = dpp_from_upper(cur[0]);
         if (lane == 0) wl = cl;
         if (lane == kWave - 1) er = cr;
         T o[VEC];
@@ -291,8 +291,8 @@ __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T 
         for (int l = 1; l <= K; ++l) {
             const int p = r - l + 1;
             const bool fixed = p == 0 || p == ny - 1;
-            const T wl = __shfl_up(Q[l - 1][1][VEC - 1], 1, 64);
-            const T er = __shfl_down(Q[l - 1][1][0], 1, 64);
+            const T wl = dpp_from_lower(Q[l - 1][1][VEC - 1]);
+            const T er = dpp_from_upper(Q[l - 1][1][0]);
             T v[VEC];
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
@@ -613,8 +613,8 @@ __global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
             if (valid && r + 1 <= y1 && r + 2 <= ny - 1) ld<float, VEC>(in + row(r + 2), app);
             // level 1 (colour 0) of row r
             const bool edge = r == 0 || r == ny - 1;
-            const float wl = __shfl_up(ac[VEC - 1], 1, 64);
-            const float er = __shfl_down(ac[0], 1, 64);
+            const float wl = dpp_from_lower(ac[VEC - 1]);
+            const float er = dpp_from_upper(ac[0]);
             float l1[VEC];
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
@@ -624,13 +624,15 @@ __global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
                     const float E = (k + 1 < VEC) ? ac[k + 1] : er;
                     const float W = (k > 0) ? ac[k - 1] : wl;
                     l1[k] = gs5(E, W, ap[k], am[k], dc[k], cx, cy, cd, dt_inv);
+                    // halo lanes 0 / 63 duplicate neighbour segments' cells, and
+                    // their outer cell sees no true x-neighbour: not counted
                     const float ch = fabsf(l1[k] - ac[k]);
-                    if (valid && ch > mx) mx = ch;
+                    if (writer && ch > mx) mx = ch;
                 }
             }
             // level 2 (colour 1) of row r-1
-            const float wl1 = __shfl_up(bc[VEC - 1], 1, 64);
-            const float er1 = __shfl_down(bc[0], 1, 64);
+            const float wl1 = dpp_from_lower(bc[VEC - 1]);
+            const float er1 = dpp_from_upper(bc[0]);
             if (r >= y0 + 1 && writer) {
                 float o[VEC];
 #pragma unroll
