@@ -162,6 +162,10 @@ def main():
     dev = torch.device("cuda", local)
     use_slab = world > 1 or ARGS.force_slab
     if use_slab:
+        # bound RCCL's send/recv kernel to 16 blocks: the overlapped slab
+        # drivers confine the exchange to 16 reserved CUs (slab.hip,
+        # partition_streams), where up to 48 such blocks fit at once
+        os.environ.setdefault("NCCL_MAX_P2P_NCHANNELS", "16")
         dist.init_process_group("nccl", device_id=dev)
 
     shape, dt_name, iters_default, bpc = WORKLOADS[ARGS.workload]

@@ -28,6 +28,10 @@ int jacobi3d_tbk_pass(int K, const float *in, float *out, const float *div, int 
                       int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt, int zchunk,
                       bool pre, hipStream_t s);
 // jacobi3d_tbr.hip: K = 3, 4 with several rows per wave (tall tiles)
+// CUs the tall-tile launches may plan for on this host thread: all of them,
+// minus those a slab solve reserved for its exchange stream (set_cu_reserve).
+int tbr_cus();
+void set_cu_reserve(int n);
 int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float *div, int nz,
                       int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
                       float dt, int zchunk, bool pre, hipStream_t s);

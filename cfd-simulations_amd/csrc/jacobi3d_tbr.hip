@@ -630,7 +630,11 @@ int num_cus() {
     }
     return n;
 }
+thread_local int g_cu_reserve = 0;
 }  // namespace
+
+int tbr_cus() { return num_cus() - g_cu_reserve; }
+void set_cu_reserve(int n) { g_cu_reserve = n; }
 
 // rows = output rows per tile (0: pick the shape and z-chunk by a cost model).
 // One workgroup fills a CU (LDS / VGPRs), so workgroups run in rounds of
@@ -645,7 +649,7 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
     const int pd = jacobi3d_tb_prefetch();
     const int L = a.ze - a.zb;
     const int nseg = ceil_div(a.nx, 256);
-    const int ncu = num_cus();
+    const int ncu = tbr_cus();
     const TbrShape *best = nullptr;
     int best_zlen = 0;
     double best_cost = 0.0;

@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -74,6 +75,82 @@ struct SlabComm {
     std::shared_ptr<LocalGroup> grp;  // in-process transport instead of RCCL
     int rank = 0, nranks = 1;
     hipEvent_t ev_boundary = nullptr, ev_comm = nullptr;
+    // CU partition of an overlapped solve (see partition_streams): a compute
+    // stream on all CUs but `reserve`, an exchange stream on those
+    int part_state = 0;  // 0 not tried, 1 ready, -1 off / unavailable
+    int reserve = 0;
+    hipStream_t cstream = nullptr, xstream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+};
+
+// Why a CU partition: the tall-tile kernels fill a CU per workgroup (VGPRs
+// and LDS), so an RCCL send/recv kernel launched beside the interior finds no
+// CU with room for its blocks and runs only after the interior -- the
+// exchange would be serialised, not overlapped (seen in rocprof traces of the
+// self-peered rehearsal: the RCCL kernel ends right after the interior).
+// The overlapped drivers therefore run their launches on a stream masked to
+// all CUs but R and the exchange on a stream masked to those R: R/8 per XCD
+// (workgroups are dealt round-robin to the 8 XCDs), with bit positions that
+// stay spread over the XCDs whether the queue's CU-mask bits map to CUs
+// XCD-major or interleaved.  The tile cost model plans for the remaining CUs
+// (16-row tiles become 18-row, one round of 228 workgroups at 1024^2).
+// CFD_SLAB_COMM_CUS = R (default 16, 0 = off).
+static int partition_streams(SlabComm *c) {
+    if (c->part_state) return c->part_state;
+    c->part_state = -1;
+    int R = 16;
+    if (const char *e = getenv("CFD_SLAB_COMM_CUS")) R = atoi(e);
+    int dev = 0, ncu = 0;
+    if (R <= 0 || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return c->part_state;
+    const int per = ncu / 8;
+    if (ncu % 8 || R % 8 || R / 8 >= per / 2 || ncu > 1024) return c->part_state;
+    std::vector<uint32_t> cm((ncu + 31) / 32, 0u), xm((ncu + 31) / 32, 0u);
+    for (int b = 0; b < ncu; ++b) cm[b / 32] |= 1u << (b % 32);
+    int got = 0;
+    for (int x = 0; x < 8; ++x)
+        for (int j = 0; j < R / 8; ++j) {
+            const int b = x * per + (x + 8 * j) % per;
+            if (!(xm[b / 32] & (1u << (b % 32)))) ++got;
+            xm[b / 32] |= 1u << (b % 32);
+            cm[b / 32] &= ~(1u << (b % 32));
+        }
+    if (got != R) return c->part_state;
+    if (hipExtStreamCreateWithCUMask(&c->cstream, (uint32_t)cm.size(), cm.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)xm.size(), xm.data()) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        return c->part_state;
+    }
+    c->reserve = R;
+    c->part_state = 1;
+    return c->part_state;
+}
+
+// Runs a solve on the partitioned streams: forks from the caller's stream on
+// entry, joins back (and clears the CU reserve) on every exit path.
+struct PartitionScope {
+    SlabComm *c = nullptr;
+    hipStream_t caller = nullptr;
+    bool on = false;
+    PartitionScope(SlabComm *c_, bool want, hipStream_t &s, hipStream_t &cs) : c(c_), caller(s) {
+        if (!want || partition_streams(c) != 1) return;
+        if (hipEventRecord(c->ev_fork, s) != hipSuccess ||
+            hipStreamWaitEvent(c->cstream, c->ev_fork, 0) != hipSuccess)
+            return;
+        on = true;
+        s = c->cstream;
+        cs = c->xstream;
+        set_cu_reserve(c->reserve);
+    }
+    ~PartitionScope() {
+        if (!on) return;
+        set_cu_reserve(0);
+        (void)hipEventRecord(c->ev_join, c->cstream);
+        (void)hipStreamWaitEvent(caller, c->ev_join, 0);
+    }
 };
 
 #define CFD_GROUP_BARRIER(g)                                                       \
@@ -253,6 +330,10 @@ int cfd_comm_destroy(void *comm) {
     SlabComm *c = reinterpret_cast<SlabComm *>(comm);
     if (c->ev_boundary) (void)hipEventDestroy(c->ev_boundary);
     if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    if (c->xstream) (void)hipStreamDestroy(c->xstream);
     if (c->grp) {
         LocalGroup::Slot &me = c->grp->slot[c->rank];
         if (me.ready) (void)hipEventDestroy(me.ready);
@@ -286,6 +367,8 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
     if (iters == 0) return CFD_OK;
     hipStream_t s = as_stream(stream);
     hipStream_t cs = comm_stream ? as_stream(comm_stream) : s;
+    PartitionScope part(c, overlap && (lo_peer >= 0 || hi_peer >= 0) &&
+                               z_update_end - z_update_begin >= 2 * ghost + 1, s, cs);
     const int nzt = nz_local + 2 * G;
     const size_t plane = (size_t)ny * nx;
     const float h2 = (float)(h * h);
@@ -314,7 +397,7 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
     const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
     // owned planes a neighbour needs after each pass: the G next to it
     const bool lo_b = lo_peer >= 0, hi_b = hi_peer >= 0;
-    const bool can_overlap = overlap && c->nranks > 1 && (ze - zb) >= 2 * G + 1;
+    const bool can_overlap = overlap && (lo_peer >= 0 || hi_peer >= 0) && (ze - zb) >= 2 * G + 1;
     float *a = phi, *b = phi_tmp;
     const int tk = timing_begin(s);
     int done = 0;
@@ -392,6 +475,8 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     CFD_REQUIRE(lo_peer < c->nranks && hi_peer < c->nranks, "slab_rbgs3d: bad peer");
     hipStream_t s = as_stream(stream);
     hipStream_t cs = comm_stream ? as_stream(comm_stream) : s;
+    PartitionScope part(c, overlap && (lo_peer >= 0 || hi_peer >= 0) &&
+                               z_update_end - z_update_begin >= 2 * ghost + 1, s, cs);
     RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
     const RbgsConsts k = rbgs3d_consts(dx, dy, dz, dt, tolerance);
     int rc = launch_rbgs_init(w, iterations, k.tol, iters_done, s);
@@ -400,7 +485,9 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     const size_t plane = (size_t)ny * nx;
     const int zb = z_update_begin, ze = z_update_end, zoff = z_global_offset;
     const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
-    const bool reduce = c->nranks > 1 && k.tol > 0.0f;
+    // a one-rank comm peered with itself (the per-rank rehearsal) reduces too
+    const bool self_peered = !c->grp && (lo_peer == c->rank || hi_peer == c->rank);
+    const bool reduce = (c->nranks > 1 || self_peered) && k.tol > 0.0f;
     auto allreduce = [&](int it, int cnt, hipStream_t st) -> int {
         if (reduce && c->grp) return allreduce_local(c, it, cnt, st);
         if (reduce)
@@ -433,7 +520,7 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     const int full_hi = fixed_hi ? nz_local + G - 1 : -1;
     if ((rc = launch_fix_faces3d(phi, phi_tmp, nullptr, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
         return rc;
-    const bool can_overlap = overlap && c->nranks > 1 && (ze - zb) >= 2 * G + 1;
+    const bool can_overlap = overlap && (lo_peer >= 0 || hi_peer >= 0) && (ze - zb) >= 2 * G + 1;
     float *a = phi, *b = phi_tmp;
     for (int it = 0; it < iterations;) {
         const int m = iterations - it >= pp ? pp : 1;

@@ -135,7 +135,11 @@ class RcclComm:
 
     def __init__(self, rank: int, nranks: int, group=None):
         import ctypes
+        import os
         import torch.distributed as dist
+        # RCCL reads this once, at its first communicator: bench.py sets it
+        # before the process group; see partition_streams in slab.hip
+        os.environ.setdefault("NCCL_MAX_P2P_NCHANNELS", "16")
         if dist.is_available() and dist.is_initialized() and nranks > 1:
             dev = torch.device("cuda", torch.cuda.current_device()) \
                 if dist.get_backend(group) == "nccl" else torch.device("cpu")
@@ -208,7 +212,9 @@ class SlabJacobi3D:
         self.rhs = torch.empty(shape, dtype=torch.float32, device=self.device) if rhs_workspace else None
         self.mask = None if mask is None else mask.to(torch.uint8).contiguous()
         self.comm = comm
-        self.comm_stream = torch.cuda.Stream(device=self.device)
+        # high priority: its own HW queue (ROCclr pools queues per priority), so
+        # the exchange is dispatched beside the interior launch, not behind it
+        self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1)
 
     def solve(self, iters: int, overlap: bool = True, zero_phi: bool = True):
         if zero_phi:
@@ -243,7 +249,9 @@ class SlabRBGS3D:
         self.iters_done = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.ws = None
         self.comm = comm
-        self.comm_stream = torch.cuda.Stream(device=self.device)
+        # high priority: its own HW queue (ROCclr pools queues per priority), so
+        # the exchange is dispatched beside the interior launch, not behind it
+        self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1)
 
     @property
     def z_global_offset(self) -> int:

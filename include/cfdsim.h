@@ -203,7 +203,10 @@ int cfd_comm_init_local(int nranks, void **comms);
  * planes next to a neighbour go into its ghost planes.  rhs_ws: optional
  * same-size workspace (see cfd_jacobi2d_f32).  overlap != 0: the boundary
  * planes are computed first, their exchange runs on comm_stream while the
- * interior computes on `stream`. */
+ * interior computes on `stream`.  A one-rank RCCL comm may name itself
+ * (rank 0) as lo_peer and hi_peer: the exchange is then an RCCL send/recv to
+ * self, a timing rehearsal of a middle rank's pass sequence on one GPU (RCCL
+ * kernels running beside the interior); its result is not a solve. */
 int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
                           float *rhs_ws, const uint8_t *mask, int nz_local, int ghost, int ny,
                           int nx, int lo_peer, int hi_peer, int z_update_begin, int z_update_end,

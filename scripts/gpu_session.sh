@@ -54,6 +54,15 @@ for s in "$@"; do
     prof_gs) step prof_gs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_fetch_gs) step pmc_fetch_gs 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
     pmc_write_gs) step pmc_write_gs 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 20 --no-cpu-baseline ;;
+    rehearse) step rehearse 900 bash -c 'python scripts/slab_rehearsal.py --ranks 1 && python scripts/slab_rehearsal.py --ranks 8 && python scripts/slab_rehearsal.py --ranks 8 --no-overlap && python scripts/slab_rehearsal.py --ranks 1 --nz 134 && python scripts/slab_rehearsal.py --ranks 2 && python scripts/slab_rehearsal.py --ranks 4' ;;
+    rehearse_gs) step rehearse_gs 900 bash -c 'python scripts/slab_rehearsal.py --workload rbgs --ranks 1 && python scripts/slab_rehearsal.py --workload rbgs --ranks 8' ;;
+    selfr) step selfr 900 bash -c 'for w in jacobi rbgs; do for R in 8 4 2; do python scripts/slab_rehearsal.py --rccl-self --workload $w --ranks $R || exit $?; done; python scripts/slab_rehearsal.py --rccl-self --workload $w --ranks 8 --no-overlap || exit $?; done' ;;
+    prof_selfr) step prof_selfr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_selfr -o run --output-format csv -- python3 scripts/slab_rehearsal.py --rccl-self --ranks 8 --steps 1 ;;
+    selfr2) step selfr2 900 bash -c 'for o in "--comm-priority 0" "--comm-priority 1" "--prefetch 2" "--prefetch 2 --no-overlap" "--workload rbgs" "--workload rbgs --prefetch 2"; do python scripts/slab_rehearsal.py --rccl-self --ranks 8 $o || exit $?; done' ;;
+    prof_selfr2) step prof_selfr2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_selfr2 -o run --output-format csv -- python3 scripts/slab_rehearsal.py --rccl-self --ranks 8 --steps 1 ;;
+    prof_selfr3) step prof_selfr3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_selfr3 -o run --output-format csv -- python3 scripts/slab_rehearsal.py --rccl-self --ranks 8 --steps 1 --prefetch 2 ;;
+    selfr3) step selfr3 900 bash -c 'for o in "" "--workload rbgs"; do python scripts/slab_rehearsal.py --rccl-self --ranks 8 $o && CFD_SLAB_COMM_CUS=0 python scripts/slab_rehearsal.py --rccl-self --ranks 8 $o && python scripts/slab_rehearsal.py --rccl-self --ranks 4 $o && python scripts/slab_rehearsal.py --rccl-self --ranks 2 $o || exit $?; done' ;;
+    testsslab) step pytest_slab 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "slab or local_group or rccl" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
