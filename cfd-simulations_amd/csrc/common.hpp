@@ -118,9 +118,10 @@ __device__ inline int xcd_swizzle(int bid, int nblocks) {
 // instead of ds_bpermute (__shfl_up/down go through the LDS crossbar, ~100
 // cycles each, and a K-level row march chains 2K of them): lane i receives
 // lane i-1's value (from_lower, wave_shr:1) or lane i+1's (from_upper,
-// wave_shl:1).  Lane 0 / 63 receive 0: callers overwrite them or never use them.
-__device__ inline int dpp_i32_from_lower(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false); }
-__device__ inline int dpp_i32_from_upper(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false); }
+// wave_shl:1).  Lane 0 / 63 receive 0 (bound_ctrl: no old value has to be
+// materialised first): callers overwrite them or never use them.
+__device__ inline int dpp_i32_from_lower(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, true); }
+__device__ inline int dpp_i32_from_upper(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, true); }
 __device__ inline float dpp_from_lower(float v) { return __int_as_float(dpp_i32_from_lower(__float_as_int(v))); }
 __device__ inline float dpp_from_upper(float v) { return __int_as_float(dpp_i32_from_upper(__float_as_int(v))); }
 __device__ inline double dpp_from_lower(double v) {

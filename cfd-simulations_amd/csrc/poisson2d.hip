@@ -204,7 +204,7 @@ static int jacobi2d_sweep(const T *in, T *out, const T *div, const uint8_t *mask
 }
 
 // ---------------------------------------------------------------------------
-// Temporally blocked 2-D Jacobi: K sweeps per pass (K = 2..6, 8): one pass reads
+// Temporally blocked 2-D Jacobi: K sweeps per pass (K = 2..6, 8, 10, 12): one pass reads
 // phi^k and the rhs once and writes phi^(k+K), 12 B (f32) / 24 B (f64) per
 // cell for K cell-updates.  A wave owns 64 lanes x VEC cells, but its
 // x-segments OVERLAP by HL = ceil(K / VEC) lanes on each side: it writes only
@@ -337,26 +337,50 @@ __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T 
     }
 }
 
+// Waves run in one round when the grid allows: the row chunk is sized so
+// nseg x nchunk waves fit the chip at the kernel's occupancy (a second,
+// partial round would leave most SIMDs idle while it drains), but never below
+// 16 (K-1) rows, so the 2K-2 re-marched rows stay a small fraction.
+// r01 8192^2 f64 K=8 (3 waves/SIMD): 41 chunks of 200 rows x 74 segments =
+// 3034 waves in one round, against 74 chunks of 112 rows (two rounds).
+template <typename T, int VEC, int K, bool PRE, bool MASK>
+static void jacobi2d_tbk_launch(const T *in, T *out, const T *div, const uint8_t *mask, int ny,
+                                int nx, T dx2, T dtv, hipStream_t s) {
+    constexpr int HL = (K + VEC - 1) / VEC;
+    constexpr int SOUT = (64 - 2 * HL) * VEC;
+    constexpr int wpb = 4;
+    const int nseg = ceil_div(nx, SOUT);
+    const int rows = ny - 2;
+    static int slots = 0;  // resident waves per chip
+    if (slots <= 0) {
+        int nb = 0, dev = 0, ncu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jacobi2d_tbk<T, VEC, K, PRE, MASK>,
+                                                         wpb * 64, 0) != hipSuccess ||
+            hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            nb <= 0 || ncu <= 0) {
+            (void)hipGetLastError();
+            nb = 2;
+            ncu = 256;
+        }
+        slots = nb * wpb * ncu;
+    }
+    int nchunk = slots / nseg;
+    if (nchunk < 1) nchunk = 1;
+    int rpc = ceil_div(rows, nchunk);
+    const int rmin = 16 * (K - 1);
+    if (rpc < rmin) rpc = rmin;
+    nchunk = ceil_div(rows, rpc);
+    const int blocks = ceil_div((long)nseg * nchunk, wpb);
+    hipLaunchKernelGGL((jacobi2d_tbk<T, VEC, K, PRE, MASK>), dim3(blocks), dim3(wpb * 64), 0, s, in,
+                       out, div, mask, ny, nx, nseg, rpc, dx2, dtv);
+}
+
 template <typename T, int VEC>
 static int jacobi2d_tbk_pass(int K, const T *in, T *out, const T *div, const uint8_t *mask, int ny,
                              int nx, T dx2, T dtv, bool pre, hipStream_t s) {
-    const int HL = (K + VEC - 1) / VEC;
-    const int SOUT = (64 - 2 * HL) * VEC;
-    const int nseg = ceil_div(nx, SOUT);
-    const int rows = ny - 2;
-    if (rows <= 0) return CFD_OK;
-    // ~8192 waves (32 per CU) when the grid allows; chunks long enough that
-    // the 2K-2 re-marched rows stay a small fraction
-    int rpc = ceil_div((long)rows * nseg, 8192);
-    const int rmin = 16 * (K - 1);
-    if (rpc < rmin) rpc = rmin;
-    if (rpc > 256) rpc = 256;
-    const int nchunk = ceil_div(rows, rpc);
-    const int wpb = 4;
-    const int blocks = ceil_div((long)nseg * nchunk, wpb);
-#define CFD_J2K(KV, PR, M)                                                                        \
-    hipLaunchKernelGGL((jacobi2d_tbk<T, VEC, KV, PR, M>), dim3(blocks), dim3(wpb * 64), 0, s, in, \
-                       out, div, mask, ny, nx, nseg, rpc, dx2, dtv)
+    if (ny - 2 <= 0) return CFD_OK;
+#define CFD_J2K(KV, PR, M) jacobi2d_tbk_launch<T, VEC, KV, PR, M>(in, out, div, mask, ny, nx, dx2, dtv, s)
 #define CFD_J2KK(KV)                                                              \
     do {                                                                          \
         if (mask) {                                                               \
@@ -371,6 +395,8 @@ static int jacobi2d_tbk_pass(int K, const T *in, T *out, const T *div, const uin
         case 4: CFD_J2KK(4); break;
         case 5: CFD_J2KK(5); break;
         case 6: CFD_J2KK(6); break;
+        case 10: CFD_J2KK(10); break;
+        case 12: CFD_J2KK(12); break;
         default: CFD_J2KK(8); break;
     }
 #undef CFD_J2KK
@@ -379,7 +405,7 @@ static int jacobi2d_tbk_pass(int K, const T *in, T *out, const T *div, const uin
     return CFD_OK;
 }
 
-static int g_j2_blocking = 0;  // sweeps per pass: 0 auto, 1 off, 2..6, 8
+static int g_j2_blocking = 0;  // sweeps per pass: 0 auto, 1 off, 2..6, 8, 10, 12
 // r01 at 8192^2 f64 (Gcell/s): K=2 368, 3 554, 4 752, 5 876, 6 1051, 8 1232,
 // 10 1228, 12 1155 (the pass turns latency-bound past 8 levels)
 constexpr int kDefaultLevels2d = 8;
@@ -426,7 +452,7 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
         int done = 0;
         while (done < iters) {
             int k = iters - done < K ? iters - done : K;
-            if (k == 7) k = 6;  // instantiated depths: 2..6, 8
+            if (k == 7 || k == 9 || k == 11) --k;  // instantiated depths: 2..6, 8, 10, 12
             rc = k == 1 ? jacobi2d_sweep<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, nullptr, s)
                         : jacobi2d_tbk_pass<T, V>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, s);
             if (rc) return rc;
@@ -779,8 +805,8 @@ int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rh
 int cfd_get_jacobi2d_levels(void) { return g_j2_blocking >= 2 ? g_j2_blocking : kDefaultLevels2d; }
 
 int cfd_set_jacobi2d_blocking(int steps) {
-    CFD_REQUIRE((steps >= 0 && steps <= 6) || steps == 8,
-                "blocking steps must be 0 (auto), 1 (off), 2..6 or 8");
+    CFD_REQUIRE((steps >= 0 && steps <= 6) || steps == 8 || steps == 10 || steps == 12,
+                "blocking steps must be 0 (auto), 1 (off), 2..6, 8, 10 or 12");
     g_j2_blocking = steps;
     return CFD_OK;
 }

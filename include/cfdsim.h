@@ -71,7 +71,7 @@ int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
 /* fp64 fields (memory_efficient=False, v5.py:287); dt promotes exactly. */
 /* Both 2-D solves fuse `steps` sweeps per HBM pass (temporal blocking, same
  * bits; a remainder iters % steps runs as a shorter pass): 0 auto (8), 1 off,
- * 2..6, 8.  Residual requests and unaligned / nx % (16/sizeof(T)) != 0 arrays
+ * 2..6, 8, 10, 12.  Residual requests and unaligned / nx % (16/sizeof(T)) != 0 arrays
  * always run single sweeps.  (The 2-D red-black GS fuses its two colours per
  * pass unless steps == 1.) */
 int cfd_set_jacobi2d_blocking(int steps);
