@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--n-gpus", type=int, default=1)
     ap.add_argument("--cell-updates", type=float, default=0.0)
     ap.add_argument("--bytes-per-update", type=float, default=12.0)
+    ap.add_argument("--trace", help="run_kernel_trace.csv: keep one mid-run window of the timeline")
+    ap.add_argument("--window", type=int, default=10, help="kernels in the --trace window")
     a = ap.parse_args()
     out_dir = ROOT / "profiles"
     out_dir.mkdir(exist_ok=True)
@@ -56,6 +58,25 @@ def main():
         print("wrote", p)
         for s in summ[:6]:
             print(f"  {s['kernel'][:70]:70s} calls={s['calls']:5d} avg={s['avg_ms']:.4f} ms {s['pct']:.2f}%")
+    if a.trace:
+        # a slice of the kernel timeline (start offsets, durations, HW queue):
+        # shows whether the exchange kernel runs beside the interior launch
+        rows = [r for r in csv.DictReader(open(a.trace))
+                if "rocclr" not in r["Kernel_Name"] and not r["Kernel_Name"].startswith("void at::")]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        big = [i for i, r in enumerate(rows) if a.kernel in r["Kernel_Name"]]
+        i0 = big[len(big) // 2] if big else 0
+        t0 = int(rows[i0]["Start_Timestamp"])
+        tl = [{"kernel": short(r["Kernel_Name"]), "queue": int(r["Queue_Id"]),
+               "start_us": round((int(r["Start_Timestamp"]) - t0) / 1e3, 1),
+               "dur_us": round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3, 1),
+               "grid": int(r["Grid_Size_X"]), "wg": int(r["Workgroup_Size_X"]),
+               "lds": int(r["LDS_Block_Size"])} for r in rows[i0:i0 + a.window]]
+        p = out_dir / f"{a.tag}_{a.workload}_timeline.json"
+        p.write_text(json.dumps(tl, indent=1) + "\n")
+        print("wrote", p)
+        for e in tl:
+            print(f"  q{e['queue']} {e['start_us']:8.1f} +{e['dur_us']:7.1f} us  {e['kernel'][:60]}")
     if a.fetch and a.write:
         def counter(path, cname):
             vals = collections.defaultdict(list)
