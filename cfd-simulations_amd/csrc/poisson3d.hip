@@ -455,7 +455,7 @@ int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int
     if (iters == 1 && (g_j3.tb_rows == 5 || g_j3.tb_rows == 13))
         return rbgs3d_tb_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, ws, s);
     const int r = g_j3.tb_rows;
-    const bool shape_ok = iters == 1 ? (r == 18 || r == 20 || r == 28) : (r == 15 || r == 16);
+    const bool shape_ok = iters == 1 ? (r == 16 || r == 18 || r == 20 || r == 28) : (r == 15 || r == 16);
     return rbgs3d_tbr_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, iters,
                            ws, 0, 0, shape_ok ? r : 0, s);
 }
@@ -502,7 +502,7 @@ int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
     CFD_REQUIRE(steps >= 0 && steps <= 4, "blocking steps must be 0 (auto), 1 (off) or 2..4");
     CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13 || rows == 9 || rows == 11 || rows == 15 ||
                     rows == 16 || rows == 17 || rows == 18 || rows == 20 || rows == 28,
-                "blocking rows must be 0 (auto), 5, 13, 18, 20, 28 (2 levels), 11, 16, 17, 18 (3), "
+                "blocking rows must be 0 (auto), 5, 13, 16, 18, 20, 28 (2 levels), 11, 16, 17, 18 (3), "
                 "9, 15, 16 (4)");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
     g_j3.tb_steps = steps;
