@@ -616,10 +616,11 @@ struct TbrShape {
 // (4, 11, 2) spills 9 VGPRs at 168 and runs slower than (4, 7, 3): explicit only.
 // K = 2 shapes serve the red-black GS passes (one iteration per pass); r01 at
 // 1024^3: 20 rows 2.48 ms, 18 rows 2.51 ms, 28 rows 2.60 ms per iteration.
-// (2, 9, 2): 16-row GS tiles, 256 workgroups at 1024^2 -- one full round.
+// (2, 9, 2): 16-row GS tiles, 256 workgroups at 1024^2 -- one full round;
+// (2, 10, 2): 18-row, 228 workgroups, for the 240 CUs of a partitioned slab.
 constexpr TbrShape kShapes[] = {{3, 11, 2, true}, {3, 10, 2, true}, {3, 7, 3, false},
                                 {4, 7, 3, true}, {4, 11, 2, false}, {2, 11, 2, true},
-                                {2, 10, 2, false}, {2, 10, 3, false}, {2, 9, 2, true}};
+                                {2, 10, 2, true}, {2, 10, 3, false}, {2, 9, 2, true}};
 
 int num_cus() {
     static int n = 0;
