@@ -95,6 +95,30 @@ struct SlabComm {
 // XCD-major or interleaved.  The tile cost model plans for the remaining CUs
 // (16-row tiles become 18-row, one round of 228 workgroups at 1024^2).
 // CFD_SLAB_COMM_CUS = R (default 16, 0 = off).
+}  // namespace cfd
+
+extern "C" int cfd_slab_cu_partition(int ncu, int reserve, uint32_t *compute_mask,
+                                     uint32_t *exchange_mask, int words) {
+    CFD_REQUIRE(compute_mask && exchange_mask && ncu > 0 && words >= (ncu + 31) / 32,
+                "slab_cu_partition: bad arguments");
+    const int per = ncu / 8, R = reserve;
+    // (x + 8j) % per is distinct for j < per / 8: at most per / 8 CUs per XCD
+    CFD_REQUIRE(ncu % 8 == 0 && per % 8 == 0 && R > 0 && R % 8 == 0 && R <= per,
+                "slab_cu_partition: need ncu %% 64 == 0 and reserve (%d) = 8k <= ncu / 8", R);
+    for (int w = 0; w < words; ++w) compute_mask[w] = exchange_mask[w] = 0u;
+    for (int b = 0; b < ncu; ++b) compute_mask[b / 32] |= 1u << (b % 32);
+    for (int x = 0; x < 8; ++x)
+        for (int j = 0; j < R / 8; ++j) {
+            // R/8 CUs of XCD x under both bit orders: b / per == x and b % 8 == x
+            const int b = x * per + (x + 8 * j) % per;
+            exchange_mask[b / 32] |= 1u << (b % 32);
+            compute_mask[b / 32] &= ~(1u << (b % 32));
+        }
+    return CFD_OK;
+}
+
+namespace cfd {
+
 static int partition_streams(SlabComm *c) {
     if (c->part_state) return c->part_state;
     c->part_state = -1;
@@ -104,19 +128,10 @@ static int partition_streams(SlabComm *c) {
     if (R <= 0 || hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return c->part_state;
-    const int per = ncu / 8;
-    if (ncu % 8 || R % 8 || R / 8 >= per / 2 || ncu > 1024) return c->part_state;
+    if (ncu <= 0 || ncu > 1024) return c->part_state;
     std::vector<uint32_t> cm((ncu + 31) / 32, 0u), xm((ncu + 31) / 32, 0u);
-    for (int b = 0; b < ncu; ++b) cm[b / 32] |= 1u << (b % 32);
-    int got = 0;
-    for (int x = 0; x < 8; ++x)
-        for (int j = 0; j < R / 8; ++j) {
-            const int b = x * per + (x + 8 * j) % per;
-            if (!(xm[b / 32] & (1u << (b % 32)))) ++got;
-            xm[b / 32] |= 1u << (b % 32);
-            cm[b / 32] &= ~(1u << (b % 32));
-        }
-    if (got != R) return c->part_state;
+    if (cfd_slab_cu_partition(ncu, R, cm.data(), xm.data(), (int)cm.size()) != CFD_OK)
+        return c->part_state;
     if (hipExtStreamCreateWithCUMask(&c->cstream, (uint32_t)cm.size(), cm.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)xm.size(), xm.data()) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||

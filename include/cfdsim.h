@@ -212,6 +212,16 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
                           int nx, int lo_peer, int hi_peer, int z_update_begin, int z_update_end,
                           double h, float dt, int iters, int overlap, void *stream,
                           void *comm_stream);
+/* CU partition of an overlapped slab solve (CFD_SLAB_COMM_CUS = reserve,
+ * default 16, 0 = off): the drivers run their launches on a stream masked to
+ * compute_mask and the RCCL exchange on one masked to exchange_mask, so the
+ * exchange kernel finds free CUs beside the one-workgroup-per-CU interior.
+ * reserve / 8 CUs per XCD (bits b with b / (ncu/8) == x and b % 8 == x for
+ * each XCD x, so the split holds for XCD-major and interleaved bit orders).
+ * ncu % 64 == 0, reserve = 8k <= ncu / 8; words >= ceil(ncu / 32).  Host
+ * only (no GPU call). */
+int cfd_slab_cu_partition(int ncu, int reserve, uint32_t *compute_mask, uint32_t *exchange_mask,
+                          int words);
 /* Single-sweep building block (also used by the slab tests on one GPU):
  * update planes [z_begin, z_end) of in -> out (local array of nz planes);
  * x/y faces copied through, masked cells -> 0.  resid (optional, device float,

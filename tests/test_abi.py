@@ -56,3 +56,34 @@ def test_device_arch_of_code_object():
     """The fat binary carries a gfx950 code object."""
     data = _lib.LIB_PATH.read_bytes()
     assert b"gfx950" in data
+
+
+@pytest.mark.parametrize("ncu,reserve", [(256, 8), (256, 16), (256, 24), (256, 32), (512, 16), (64, 8)])
+def test_slab_cu_partition_spreads_reserve_over_xcds(ncu, reserve):
+    """The exchange CUs of a partitioned slab solve (cfd_slab_cu_partition,
+    host only): disjoint from the compute CUs, together all CUs, reserve/8 on
+    each of the 8 XCDs whether mask bit b maps to XCD b // (ncu/8) or b % 8."""
+    import numpy as np
+    words = (ncu + 31) // 32
+    cm = (ctypes.c_uint32 * words)()
+    xm = (ctypes.c_uint32 * words)()
+    _lib.call("cfd_slab_cu_partition", ncu, reserve, ctypes.addressof(cm), ctypes.addressof(xm), words)
+
+    def bits(m):
+        return np.array([(m[b // 32] >> (b % 32)) & 1 for b in range(ncu)], dtype=bool)
+
+    c, x = bits(cm), bits(xm)
+    assert x.sum() == reserve and c.sum() == ncu - reserve
+    assert not (c & x).any() and (c | x).all()
+    b = np.nonzero(x)[0]
+    for xcd in (b // (ncu // 8), b % 8):
+        assert np.bincount(xcd, minlength=8).tolist() == [reserve // 8] * 8
+
+
+@pytest.mark.parametrize("ncu,reserve", [(256, 0), (256, 12), (256, 40), (100, 8)])
+def test_slab_cu_partition_rejects_unbalanced_requests(ncu, reserve):
+    words = (ncu + 31) // 32
+    cm = (ctypes.c_uint32 * words)()
+    xm = (ctypes.c_uint32 * words)()
+    with pytest.raises(_lib.CfdError, match="slab_cu_partition"):
+        _lib.call("cfd_slab_cu_partition", ncu, reserve, ctypes.addressof(cm), ctypes.addressof(xm), words)

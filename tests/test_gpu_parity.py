@@ -584,6 +584,42 @@ def test_slab_rbgs_rccl_single_rank(overlap, ghost, steps, tol):
         comm.close()
 
 
+@pytest.mark.parametrize("gs", [False, True])
+def test_slab_rccl_self_peered_rehearsal(gs):
+    """The per-rank rehearsal mode (scripts/slab_rehearsal.py --rccl-self): a
+    one-rank RCCL comm named as both neighbours runs a middle rank's pass
+    sequence -- boundary planes, RCCL send/recv to self on the reserved-CU
+    exchange stream beside the interior (the CU partition), the GS max
+    allreduce.  Its result is not a solve, but the overlapped (partitioned)
+    schedule must equal the serial one bit for bit, and repeat exactly."""
+    nzl, ny, nx, iters = 24, 34, 64, 10
+    G = 2 if gs else 3
+    rng = np.random.default_rng(5)
+    div = dev(rng.standard_normal((nzl + 2 * G, ny, nx)).astype(np.float32) * np.float32(1e-3))
+    comm = S.RcclComm(0, 1)
+    cs = torch.cuda.Stream(priority=-1)
+    ws = torch.zeros(int(lib().cfd_rbgs_workspace_bytes(iters)), dtype=torch.uint8, device=DEV)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    outs = []
+    try:
+        for overlap in (0, 1, 1):
+            phi, tmp = torch.zeros_like(div), torch.zeros_like(div)
+            if gs:
+                call("cfd_slab_rbgs3d_f32", comm.handle, ptr(div), ptr(phi), ptr(tmp), None, nzl, G, ny, nx,
+                     0, 0, G, nzl + G, 100, 0.05, 0.05, 0.05, 1e-2, iters, 1e-30, ptr(ws), ptr(done),
+                     overlap, stream_handle(), cs.cuda_stream)
+            else:
+                rhs = torch.empty_like(div)
+                call("cfd_slab_jacobi3d_f32", comm.handle, ptr(div), ptr(phi), ptr(tmp), ptr(rhs), None, nzl,
+                     G, ny, nx, 0, 0, G, nzl + G, 0.05, 1e-3, iters, overlap, stream_handle(),
+                     cs.cuda_stream)
+            outs.append(host(phi))
+    finally:
+        comm.close()
+    assert np.isfinite(outs[0]).all() and np.abs(outs[0]).max() > 0
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
+
+
 # ------------------------------------------------- multi-rank, one GPU (threads)
 def _run_local_group(R, make, run):
     """R ranks of an in-process slab group (cfd_comm_init_local), one host
