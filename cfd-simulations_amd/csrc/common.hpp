@@ -137,6 +137,45 @@ __device__ inline double dpp_from_upper(double v) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// LDS-DMA of one 1 KiB row (64 lanes x 16 B) into lds_row[0..255]: the data
+// lands in LDS without passing through VGPRs (buffer_load_dwordx4 ... lds,
+// destination M0 + 16 * lane; a lane whose offset is outside the resource
+// writes zeros).  Issued as inline asm on purpose: for a DMA the compiler can
+// see, the waitcnt pass cannot tell the destination from other LDS data and
+// drains every DMA (vmcnt(0)) before each LDS access.  Consumers wait with
+// wait_vmcnt<> themselves; the compiler's own vmcnt counts only grow stricter
+// with the extra in-flight operations.
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOob = 0x80000000u;  // a buffer offset past any resource: reads 0
+// raw buffer resource over [base, base + bytes), stride 0
+__device__ inline v4i32 buf_rsrc4(const void *base, uint32_t bytes) {
+    const unsigned long long b = (unsigned long long)base;
+    v4i32 r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    r.y = __builtin_amdgcn_readfirstlane((int)((unsigned)(b >> 32) & 0xffffu));
+    r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+    r.w = 0x00020000;
+    return r;
+}
+__device__ inline void dma_row(v4i32 rs, uint32_t byte_ofs, void *lds_row) {
+    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lds_row;
+    int saved;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "s"(__builtin_amdgcn_readfirstlane(la)), "v"(byte_ofs), "s"(rs)
+        : "memory");
+}
+// s_waitcnt vmcnt(N) (expcnt, lgkmcnt: no wait)
+template <int N>
+__device__ inline void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+
 inline int ceil_div(long a, long b) { return static_cast<int>((a + b - 1) / b); }
 
 }  // namespace cfd

@@ -40,7 +40,8 @@ struct RbgsWs;
 struct RbgsConsts;
 int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                     int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
-                    int iters, RbgsWs *ws, int rollback, int npairs, int rows, hipStream_t s);
+                    int iters, RbgsWs *ws, int rollback, int npairs, int rows, hipStream_t s,
+                    int lag = 0);
 // red-black GS workspace (cfd_rbgs_workspace_bytes): flags[0] = iterations,
 // flags[1] = iterations done, flags[2] = tolerance (float bits), float
 // maxc[iterations] at byte 16
@@ -75,7 +76,7 @@ int rbgs3d_colour_pass(int colour, float *phi, const float *div, const uint8_t *
 int rbgs3d_iters_per_pass();  // 1, or 2 (blocking depth 4)
 int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
-                      int iters, RbgsWs *ws, hipStream_t s);
+                      int iters, RbgsWs *ws, hipStream_t s, int lag = 0);
 // one fused iteration (both colours) of planes [zb, ze) of `out` from `in`;
 // max|change| into ws->maxc[it], stop counter ws->flags[1]
 int rbgs3d_tb_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,

@@ -37,7 +37,6 @@ __device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p)
 // Plane rows through buffer resources: one resource per (array, plane) in
 // SGPRs with num_records = the plane's bytes (0 for a plane outside the
 // array); a lane outside the grid passes kOob and reads 0, with no branch.
-constexpr uint32_t kOob = 0x80000000u;
 typedef float gv4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ inline __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, int p, int nz, size_t plane) {
@@ -49,14 +48,7 @@ __device__ inline float4 ldb4(__amdgpu_buffer_rsrc_t r, uint32_t byte_ofs) {
     const gv4f v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_ofs, 0, 0);
     return make_float4(v.x, v.y, v.z, v.w);
 }
-// LDS-DMA of one 1 KiB row (64 lanes x 16 B) into lds_row[0..255]: the data
-// lands in LDS without passing through VGPRs (buffer_load_dwordx4 ... lds,
-// destination M0 + 16 * lane).  Issued as inline asm on purpose: for a DMA the
-// compiler can see, the waitcnt pass cannot tell the level tiles from the
-// staging buffers and drains every DMA (vmcnt(0)) before each tile access.
-// Consumers wait with wait_vmcnt<> themselves; the compiler's own vmcnt
-// counts only grow stricter with the extra in-flight operations.
-typedef int v4i32 __attribute__((ext_vector_type(4)));
+// (dma_row, wait_vmcnt: common.hpp)
 __device__ inline v4i32 plane_rsrc4(const float *base, int p, int nz, size_t plane) {
     const bool in = p >= 0 && p <= nz - 1;
     const unsigned long long b = (unsigned long long)(in ? base + (size_t)p * plane : base);
@@ -66,24 +58,6 @@ __device__ inline v4i32 plane_rsrc4(const float *base, int p, int nz, size_t pla
     r.z = __builtin_amdgcn_readfirstlane(in ? (int)(plane * sizeof(float)) : 0);
     r.w = 0x00020000;
     return r;
-}
-__device__ inline void dma_row(v4i32 rs, uint32_t byte_ofs, float *lds_row) {
-    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float *)lds_row;
-    int saved;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %1\n\t"
-        "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(saved)
-        : "s"(__builtin_amdgcn_readfirstlane(la)), "v"(byte_ofs), "s"(rs)
-        : "memory");
-}
-// s_waitcnt vmcnt(N) (expcnt, lgkmcnt: no wait)
-template <int N>
-__device__ inline void wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
 }
 // LDS barrier that leaves LDS-DMA in flight (__syncthreads' fence would wait
 // vmcnt(0)); the memory clobber keeps the compiler's LDS accesses in place
@@ -103,6 +77,7 @@ struct TbrArgs {
     int rollback;    // GS: the conditional re-run of one iteration (see rbgs3d_rollback)
     int npairs;      // GS rollback: pair passes the solve scheduled
     const int *count;  // GS rollback: iterations done (device)
+    int lag;         // GS: the stop test reads maxc[it-1-lag], maxc[it-2-lag] (see rbgs3d_tbr_pass)
 };
 
 // One level on the float4 of cells x .. x+3.  Jacobi: every interior cell.
@@ -331,8 +306,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 a.in = a.out;
                 a.out = t_;
             }
-        } else if ((a.it >= 1 && a.maxc[a.it - 1] < a.tol) || (a.it >= 2 && a.maxc[a.it - 2] < a.tol)) {
-            return;  // an earlier iteration met the tolerance (v5.py:224-225)
+        } else {
+            const int d = 1 + a.lag;
+            if ((a.it >= d && a.maxc[a.it - d] < a.tol) || (a.it >= d + 1 && a.maxc[a.it - d - 1] < a.tol))
+                return;  // an earlier iteration met the tolerance (v5.py:224-225)
         }
     }
     const int nz = a.nz, ny = a.ny, nx = a.nx;
@@ -730,7 +707,8 @@ int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float 
 // the direction from the count in ws->flags[1], see rbgs_count).
 int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                     int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
-                    int iters, RbgsWs *ws, int rollback, int npairs, int rows, hipStream_t s) {
+                    int iters, RbgsWs *ws, int rollback, int npairs, int rows, hipStream_t s,
+                    int lag) {
     if (ze <= zb || ny < 3) return CFD_OK;
     TbrArgs a{};
     a.in = in; a.out = out; a.div = div;
@@ -742,6 +720,7 @@ int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int n
     a.rollback = rollback;
     a.npairs = npairs;
     a.count = &ws->flags[1];
+    a.lag = lag;
     return tbr_launch<kRbgs>(a, 2 * iters, rows, jacobi3d_tb_zchunk(), false, s);
 }
 

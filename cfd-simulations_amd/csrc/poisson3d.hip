@@ -448,16 +448,17 @@ RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double toler
 int rbgs3d_iters_per_pass() { return g_j3.tb_steps == 4 ? 2 : 1; }
 
 // One fused GS pass of `iters` (1, 2) iterations: the tuned 2-level kernel
-// when its rows are set explicitly (5, 13), the tall-tile kernel otherwise.
+// when its rows are set explicitly (5, 13), the tall-tile kernel otherwise
+// (always for a lagged stop test, which only the tall-tile kernel has).
 int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
-                      int iters, RbgsWs *ws, hipStream_t s) {
-    if (iters == 1 && (g_j3.tb_rows == 5 || g_j3.tb_rows == 13))
+                      int iters, RbgsWs *ws, hipStream_t s, int lag) {
+    if (iters == 1 && !lag && (g_j3.tb_rows == 5 || g_j3.tb_rows == 13))
         return rbgs3d_tb_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, ws, s);
     const int r = g_j3.tb_rows;
     const bool shape_ok = iters == 1 ? (r == 16 || r == 18 || r == 20 || r == 28) : (r == 15 || r == 16);
     return rbgs3d_tbr_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, iters,
-                           ws, 0, 0, shape_ok ? r : 0, s);
+                           ws, 0, 0, shape_ok ? r : 0, s, lag);
 }
 
 // One pass of k Jacobi sweeps over planes [zb, ze) (k = 1..4), with the tile

@@ -151,7 +151,9 @@ struct PartitionScope {
     hipStream_t caller = nullptr;
     bool on = false;
     PartitionScope(SlabComm *c_, bool want, hipStream_t &s, hipStream_t &cs) : c(c_), caller(s) {
-        if (!want || partition_streams(c) != 1) return;
+        // not for an in-process group: its ranks share one GPU's CUs anyway,
+        // and 2 masked queues per rank oversubscribe the hardware queues
+        if (!want || c->grp || partition_streams(c) != 1) return;
         if (hipEventRecord(c->ev_fork, s) != hipSuccess ||
             hipStreamWaitEvent(c->cstream, c->ev_fork, 0) != hipSuccess)
             return;
@@ -539,13 +541,21 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     if ((rc = launch_fix_faces3d(phi, phi_tmp, nullptr, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
         return rc;
     const bool can_overlap = overlap && (lo_peer >= 0 || hi_peer >= 0) && (ze - zb) >= 2 * G + 1;
+    // Lagged stop test (overlapped, one iteration per pass): pass j tests
+    // maxc[j-2] and maxc[j-3] instead of maxc[j-1] and maxc[j-2], so the
+    // allreduce of iteration j-1 runs beside pass j's boundary launches
+    // instead of between the passes.  A stop at iteration n then costs one
+    // wasted pass n+1; it writes the buffer of iteration n-1, so iteration n's
+    // result is intact, and maxc of a skipped pass stays 0 (< tol), which keeps
+    // every later pass skipped.  rbgs_count / rbgs_copy are unchanged.
+    const int lag = can_overlap && reduce && pp == 1 ? 1 : 0;
     float *a = phi, *b = phi_tmp;
     for (int it = 0; it < iterations;) {
         const int m = iterations - it >= pp ? pp : 1;
         auto run = [&](int z0, int z1) -> int {
             if (z1 <= z0) return CFD_OK;
             return rbgs3d_fused_pass(a, b, div, nzt, ny, nx, z0, z1, z0 == zb && fixed_lo,
-                                     z1 == ze && fixed_hi, zoff, k, it, m, w, s);
+                                     z1 == ze && fixed_hi, zoff, k, it, m, w, s, lag);
         };
         if (!can_overlap) {
             if ((rc = run(zb, ze))) return rc;
@@ -566,19 +576,26 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
             if ((rc = run(ib, ie))) return rc;
             CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
             if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, cs))) return rc;
+            // lagged: the next pass waits for the exchange only (and, through
+            // the in-order exchange stream, for the previous allreduce)
+            if (lag) CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
             if (reduce) {
                 // the global max needs the interior's contribution too
                 CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
                 CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
                 if ((rc = allreduce(it, m, cs))) return rc;
             }
-            CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
+            if (!lag) CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
             CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
         }
         it += m;
         float *t = a;
         a = b;
         b = t;
+    }
+    if (lag) {  // the last allreduce
+        CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
+        CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
     }
     timing_end(tk, s, iterations);
     // count (same on every rank: the maxima are global), re-run a pair
