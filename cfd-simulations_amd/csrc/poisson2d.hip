@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T 
 // Waves run in one round when the grid allows: the row chunk is sized so
 // nseg x nchunk waves fit the chip at the kernel's occupancy (a second,
 // partial round would leave most SIMDs idle while it drains), but never below
-// 16 (K-1) rows, so the 2K-2 re-marched rows stay a small fraction.
+// 2 (K-1) rows.
 // r01 8192^2 f64 K=8 (3 waves/SIMD): 41 chunks of 200 rows x 74 segments =
 // 3034 waves in one round, against 74 chunks of 112 rows (two rounds).
 template <typename T, int VEC, int K, bool PRE, bool MASK>
@@ -368,7 +368,9 @@ static void jacobi2d_tbk_launch(const T *in, T *out, const T *div, const uint8_t
     int nchunk = slots / nseg;
     if (nchunk < 1) nchunk = 1;
     int rpc = ceil_div(rows, nchunk);
-    const int rmin = 16 * (K - 1);
+    // at least 2 (K-1) rows: the 2K-2 re-marched rows are at most half the
+    // march (large grids get long chunks from the round sizing anyway)
+    const int rmin = 2 * (K - 1);
     if (rpc < rmin) rpc = rmin;
     nchunk = ceil_div(rows, rpc);
     const int blocks = ceil_div((long)nseg * nchunk, wpb);
@@ -700,8 +702,11 @@ static int rbgs2d_tb_pass(const float *in, float *out, const float *div, const u
     constexpr int SOUT = 64 * 4 - 2 * 4;
     const int nseg = ceil_div(nx, SOUT);
     const int rows = ny - 2;
+    // short chunks on small grids: the 600 x 180 cylinder has 3 segments, and
+    // 2-row chunks give 267 waves (8-row chunks: 69 waves, 11.3 us per
+    // iteration, latency-bound); the re-marched row per chunk is cheap there
     int rpc = ceil_div((long)rows * nseg, 8192);
-    if (rpc < 8) rpc = 8;
+    if (rpc < 2) rpc = 2;
     if (rpc > 64) rpc = 64;
     const int nchunk = ceil_div(rows, rpc);
     const int wpb = 4;

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""End-to-end rate of the v5 cylinder solver's time_step() on one GPU.
+
+    python scripts/cylinder_bench.py [--nx 600 --ny 180] [--steps 20] [--jacobi]
+
+The reference's own configuration (OptimizedTurbulentConfig defaults,
+v5.py:41-94): 600 x 180 grid, Re 600, SUPG predictor, 1500 red-black GS
+iterations per step at tolerance 1e-8 (in fp32 the stop never fires, so all
+1500 run).  Prints one JSON line: steps/s, ms per step, the pressure solve's
+share, and the GS cell-update rate inside it.  The CPU reference is not timed
+here (its numba build is absent).
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import _pkgpath  # noqa: E402
+
+_pkgpath.load()
+from cfd_simulations_amd.solver import OptimizedTurbulentConfig, OptimizedTurbulentSolver  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nx", type=int, default=600)
+    ap.add_argument("--ny", type=int, default=180)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--jacobi", action="store_true", help="use_fast_pressure=False (NumPy-branch Jacobi)")
+    a = ap.parse_args()
+    cfg = OptimizedTurbulentConfig(nx=a.nx, ny=a.ny, use_fast_pressure=not a.jacobi)
+    s = OptimizedTurbulentSolver(cfg)
+    for _ in range(a.warmup):
+        s.time_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        s.time_step()
+    torch.cuda.synchronize()
+    t_step = (time.perf_counter() - t0) / a.steps
+    # the pressure solve alone, same state
+    div = s.div_u_star.clone()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        s.solve_pressure_fast(div)
+    torch.cuda.synchronize()
+    t_p = (time.perf_counter() - t0) / a.steps
+    it = cfg.pressure_iterations
+    cells = (a.ny - 2) * (a.nx - 2) * it
+    out = {"workload": f"cylinder_v5_{a.nx}x{a.ny}", "pressure": "jacobi" if a.jacobi else "rbgs",
+           "pressure_iterations": it, "steps_per_s": round(1.0 / t_step, 2),
+           "ms_per_step": round(t_step * 1e3, 3), "pressure_ms": round(t_p * 1e3, 3),
+           "pressure_share": round(t_p / t_step, 3),
+           "pressure_us_per_iteration": round(t_p / it * 1e6, 2),
+           "pressure_gcell_updates_s": round(cells / t_p / 1e9, 2),
+           "u_finite": bool(torch.isfinite(s.u).all().item()),
+           "energy_last": float(np.float64(s.energy_history[-1][1]))}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

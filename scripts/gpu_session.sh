@@ -65,6 +65,8 @@ for s in "$@"; do
     testsslab) step pytest_slab 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "slab or local_group or rccl" ;;
     prof_selfgs) step prof_selfgs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_selfgs -o run --output-format csv -- python3 scripts/slab_rehearsal.py --rccl-self --workload rbgs --ranks 8 --steps 1 ;;
     ab2d) step ab2d 600 bash -c 'for e in 0 1; do echo "CFD_J2_RHS_REGS=$e"; CFD_J2_RHS_REGS=$e python bench.py --workload jacobi2d_8192_f64 --no-cpu-baseline --steps 5 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
+    cyl) step cyl 600 bash -c 'python scripts/cylinder_bench.py && python scripts/cylinder_bench.py --jacobi' ;;
+    prof_cyl) step prof_cyl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cyl -o run --output-format csv -- python3 scripts/cylinder_bench.py --steps 3 --warmup 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
