@@ -411,6 +411,18 @@ static int g_j2_blocking = 0;  // sweeps per pass: 0 auto, 1 off, 2..6, 8, 10, 1
 // r01 at 8192^2 f64 (Gcell/s): K=2 368, 3 554, 4 752, 5 876, 6 1051, 8 1232,
 // 10 1228, 12 1155 (the pass turns latency-bound past 8 levels)
 constexpr int kDefaultLevels2d = 8;
+// Auto depth: 8 levels when the grid fills the chip with long row chunks
+// (at least 16 rows per wave with ~12 resident waves per CU), else 2 -- on a
+// small grid a pass is a chain of row-step latencies, 2(K-1) of them wasted
+// per chunk.  r01 on the 600 x 180 cylinder (f32, masked): K = 1 / 2 / 3 / 4
+// / 6 / 8 -> 5.0 / 2.7 / 3.1 / 3.7 / 4.8 / 5.8 us per sweep.
+template <typename T>
+static int auto_levels2d(int ny, int nx) {
+    constexpr int V = 16 / sizeof(T);
+    const int sout = (64 - 2 * ((kDefaultLevels2d + V - 1) / V)) * V;
+    const long work = (long)(ny - 2) * ceil_div(nx, sout);
+    return work >= 16L * 12 * 256 ? kDefaultLevels2d : 2;
+}
 
 template <typename T>
 __global__ void k_rhs2d(const T *__restrict__ div, T *__restrict__ rhs, size_t n, T dx2, T dtv) {
@@ -450,7 +462,7 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
     const int tk = timing_begin(s);
     if (g_j2_blocking != 1 && vec_ok && resid_every <= 0 && iters >= 2 && ny >= 3) {
         // temporally blocked: passes of K sweeps, the remainder last
-        const int K = g_j2_blocking >= 2 ? g_j2_blocking : kDefaultLevels2d;
+        const int K = g_j2_blocking >= 2 ? g_j2_blocking : auto_levels2d<T>(ny, nx);
         int done = 0;
         while (done < iters) {
             int k = iters - done < K ? iters - done : K;
@@ -597,10 +609,12 @@ __global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
                                                  int it) {
     constexpr int VEC = 4;
     constexpr int SOUT = 64 * VEC - 2 * VEC;
-    if (it > 0 && ws->maxc[it - 1] < tol) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&ws->flags[1], it);
-        return;
-    }
+    // the stop test (a global load) is read here but acted on after the first
+    // row loads are issued, so the two latencies overlap (small grids run a
+    // pass in a few microseconds)
+    const float prev = it > 0 ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 1]) : 0.f;
+    const bool stopped = it > 0 && prev < tol;
+    if (stopped && blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&ws->flags[1], it);
     const int lane = threadIdx.x & 63;
     const int wpb = blockDim.x / 64;
     const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -637,6 +651,7 @@ __global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
                 for (int k = 0; k < VEC; ++k) { mc[k] = mask[row(rs) + k]; mn[k] = mask[row(rs + 1) + k]; }
             }
         }
+        if (stopped) return;  // an earlier iteration met the tolerance (v5.py:224-225)
         for (int r = rs; r <= y1; ++r) {
             if (valid && r + 1 <= y1 && r + 2 <= ny - 1) ld<float, VEC>(in + row(r + 2), app);
             // level 1 (colour 0) of row r
@@ -693,7 +708,127 @@ __global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
             }
         }
     }
+    if (stopped) return;
     wave_reduce_max_store(mx, &ws->maxc[it]);
+}
+
+// rbgs2d_tb for small grids: each wave owns TWO output rows and loads every
+// row it needs up front (level 0 rows y0-2 .. y0+3, div / mask rows y0-1 ..
+// y0+2), so a pass is one load latency, the two colour levels, and the
+// stores -- no row march with a load per step.  The 600 x 180 cylinder pass
+// (latency-bound) drops from ~9 us to ~? us.  Same cells, same
+// operation order and same max|change| accounting as rbgs2d_tb.
+template <bool MASK>
+__global__ __launch_bounds__(256) void rbgs2d_tb2r(const float *__restrict__ in,
+                                                   float *__restrict__ out,
+                                                   const float *__restrict__ div,
+                                                   const uint8_t *__restrict__ mask, int ny, int nx,
+                                                   int nseg, float cx, float cy, float cd,
+                                                   float dt_inv, float tol, RbgsWs *ws, int it) {
+    constexpr int VEC = 4;
+    constexpr int SOUT = 64 * VEC - 2 * VEC;
+    const float prev = it > 0 ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 1]) : 0.f;
+    const bool stopped = it > 0 && prev < tol;
+    if (stopped && blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&ws->flags[1], it);
+    const int lane = threadIdx.x & 63;
+    const int wpb = blockDim.x / 64;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const long wave = (long)bid * wpb + threadIdx.x / 64;
+    const int seg = (int)(wave % nseg);
+    const int y0 = 1 + 2 * (int)(wave / nseg);
+    float mx = 0.f;
+    if (y0 < ny - 1) {  // wave-uniform
+        const int y1 = min(y0 + 2, ny - 1);
+        const int x0 = seg * SOUT - VEC + lane * VEC;
+        const bool valid = x0 >= 0 && x0 < nx;
+        const bool writer = lane >= 1 && lane <= 62 && valid;
+        auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
+        float L0[6][VEC], D[4][VEC];  // level 0 rows y0-2+i, div rows y0-1+i
+        uint8_t Mk[4][VEC];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) L0[i][k] = 0.f;
+            const int y = y0 - 2 + i;
+            if (valid && y >= 0 && y <= ny - 1) ld<float, VEC>(in + row(y), L0[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) { D[i][k] = 0.f; Mk[i][k] = 0; }
+            const int y = y0 - 1 + i;
+            if (valid && y >= 0 && y <= ny - 1) {
+                ld<float, VEC>(div + row(y), D[i]);
+                if (MASK) {  // 4 mask bytes in one load (nx % 4 == 0, x0 % 4 == 0)
+                    const uint32_t m4 = *reinterpret_cast<const uint32_t *>(mask + row(y));
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) Mk[i][k] = (uint8_t)(m4 >> (8 * k));
+                }
+            }
+        }
+        if (!stopped) {
+        // level 1 (colour 0) of rows y0-1 .. y0+2
+        float L1[4][VEC];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = y0 - 1 + i;
+            const bool edge = r == 0 || r == ny - 1;
+            const float *ac = L0[i + 1];
+            const float wl = dpp_from_lower(ac[VEC - 1]);
+            const float er = dpp_from_upper(ac[0]);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const int x = x0 + k;
+                L1[i][k] = ac[k];
+                if (!edge && x >= 1 && x < nx - 1 && ((r + x + 1) & 1) == 0 && !(MASK && Mk[i][k])) {
+                    const float E = (k + 1 < VEC) ? ac[k + 1] : er;
+                    const float W = (k > 0) ? ac[k - 1] : wl;
+                    L1[i][k] = gs5(E, W, L0[i + 2][k], L0[i][k], D[i][k], cx, cy, cd, dt_inv);
+                    // rows y0-1 .. y1 as rbgs2d_tb counts them (halo rows repeat
+                    // a neighbour chunk's values; a row past y1 may be outside
+                    // the grid); halo lanes 0 / 63 are not counted
+                    const float ch = fabsf(L1[i][k] - ac[k]);
+                    if (writer && r <= y1 && ch > mx) mx = ch;
+                }
+            }
+        }
+        // level 2 (colour 1) of rows y0, y0+1
+#pragma unroll
+        for (int i = 1; i <= 2; ++i) {
+            const int p = y0 - 1 + i;
+            if (p >= y1) break;
+            const float *bc = L1[i];
+            const float wl1 = dpp_from_lower(bc[VEC - 1]);
+            const float er1 = dpp_from_upper(bc[0]);
+            if (writer) {
+                float o[VEC];
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const int x = x0 + k;
+                    o[k] = bc[k];
+                    if (x >= 1 && x < nx - 1 && ((p + x + 2) & 1) == 0 && !(MASK && Mk[i][k])) {
+                        const float E = (k + 1 < VEC) ? bc[k + 1] : er1;
+                        const float W = (k > 0) ? bc[k - 1] : wl1;
+                        o[k] = gs5(E, W, L1[i + 1][k], L1[i - 1][k], D[i][k], cx, cy, cd, dt_inv);
+                        const float ch = fabsf(o[k] - bc[k]);
+                        if (ch > mx) mx = ch;
+                    }
+                }
+                st<float, VEC>(out + row(p), o);
+            }
+        }
+        }  // !stopped
+    }
+    // one atomic per workgroup, without the read-first guard (a dependent
+    // load at the end of a few-microsecond kernel)
+    __shared__ float red[4];
+    const float m = wave_max(mx);
+    if (lane == 0) red[threadIdx.x / 64] = m;
+    __syncthreads();
+    if (threadIdx.x == 0 && !stopped) {
+        const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        if (b > 0.0f) atomic_max_nonneg(&ws->maxc[it], b);
+    }
 }
 
 static int rbgs2d_tb_pass(const float *in, float *out, const float *div, const uint8_t *mask,
@@ -706,7 +841,18 @@ static int rbgs2d_tb_pass(const float *in, float *out, const float *div, const u
     // 2-row chunks give 267 waves (8-row chunks: 69 waves, 11.3 us per
     // iteration, latency-bound); the re-marched row per chunk is cheap there
     int rpc = ceil_div((long)rows * nseg, 8192);
-    if (rpc < 2) rpc = 2;
+    if (rpc <= 2) {
+        // small grid: two-row chunks with every row loaded up front
+        const int blocks = ceil_div((long)nseg * ceil_div(rows, 2), 4);
+        if (mask)
+            hipLaunchKernelGGL(rbgs2d_tb2r<true>, dim3(blocks), dim3(256), 0, s, in, out, div, mask, ny, nx,
+                               nseg, cx, cy, cd, dt_inv, tol, ws, it);
+        else
+            hipLaunchKernelGGL(rbgs2d_tb2r<false>, dim3(blocks), dim3(256), 0, s, in, out, div, mask, ny,
+                               nx, nseg, cx, cy, cd, dt_inv, tol, ws, it);
+        CFD_LAUNCH_CHECK();
+        return CFD_OK;
+    }
     if (rpc > 64) rpc = 64;
     const int nchunk = ceil_div(rows, rpc);
     const int wpb = 4;

@@ -70,12 +70,15 @@ int cfd_jacobi2d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
                      int resid_every, float *resid_out, void *stream);
 /* fp64 fields (memory_efficient=False, v5.py:287); dt promotes exactly. */
 /* Both 2-D solves fuse `steps` sweeps per HBM pass (temporal blocking, same
- * bits; a remainder iters % steps runs as a shorter pass): 0 auto (8), 1 off,
+ * bits; a remainder iters % steps runs as a shorter pass): 0 auto (8 on grids
+ * that fill the chip with long row chunks, e.g. 8192^2; 2 on small ones such as
+ * the 600 x 180 cylinder, where a pass is latency-bound), 1 off,
  * 2..6, 8, 10, 12.  Residual requests and unaligned / nx % (16/sizeof(T)) != 0 arrays
  * always run single sweeps.  (The 2-D red-black GS fuses its two colours per
  * pass unless steps == 1.) */
 int cfd_set_jacobi2d_blocking(int steps);
-/* 2-D Jacobi sweeps per blocked pass currently in effect. */
+/* 2-D Jacobi sweeps per blocked pass: the set depth, or the large-grid auto
+ * depth (8). */
 int cfd_get_jacobi2d_levels(void);
 int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,

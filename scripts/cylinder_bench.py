@@ -34,7 +34,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--jacobi", action="store_true", help="use_fast_pressure=False (NumPy-branch Jacobi)")
+    ap.add_argument("--levels", type=int, default=0, help="cfd_set_jacobi2d_blocking (0 auto)")
     a = ap.parse_args()
+    from cfd_simulations_amd._lib import call
+    call("cfd_set_jacobi2d_blocking", a.levels)
     cfg = OptimizedTurbulentConfig(nx=a.nx, ny=a.ny, use_fast_pressure=not a.jacobi)
     s = OptimizedTurbulentSolver(cfg)
     for _ in range(a.warmup):
@@ -56,6 +59,7 @@ def main():
     it = cfg.pressure_iterations
     cells = (a.ny - 2) * (a.nx - 2) * it
     out = {"workload": f"cylinder_v5_{a.nx}x{a.ny}", "pressure": "jacobi" if a.jacobi else "rbgs",
+           "levels": a.levels,
            "pressure_iterations": it, "steps_per_s": round(1.0 / t_step, 2),
            "ms_per_step": round(t_step * 1e3, 3), "pressure_ms": round(t_p * 1e3, 3),
            "pressure_share": round(t_p / t_step, 3),

@@ -62,7 +62,7 @@ def test_jacobi2d_golden_bitexact(golden, name):
     assert np.array_equal(out, d["phi"])
 
 
-@pytest.mark.parametrize("blocking", [1, 2, 3, 4, 5, 6, 8])
+@pytest.mark.parametrize("blocking", [0, 1, 2, 3, 4, 5, 6, 8, 10, 12])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("shape,iters", [((37, 53), 17), ((3, 3), 4), ((130, 260), 31),
                                          ((66, 516), 8), ((2, 9), 3), ((200, 248), 10), ((9, 124), 6),
@@ -268,8 +268,10 @@ def test_rbgs2d_golden_bitexact(golden, name, fused):
 
 
 @pytest.mark.parametrize("fused", [False, True])
-@pytest.mark.parametrize("shape", [(31, 45), (31, 44), (64, 128), (5, 4), (130, 520), (3, 8)])
+@pytest.mark.parametrize("shape", [(31, 45), (31, 44), (64, 128), (5, 4), (130, 520), (3, 8), (2050, 2048)])
 def test_rbgs2d_random_bitexact(shape, fused):
+    """Small grids run the preloaded two-row fused kernel, 2050 x 2048 the row
+    march (rbgs2d_tb); both bit-identical to the serial oracle."""
     _gs_fused(fused)
     rng = np.random.default_rng(4)
     div = rng.standard_normal(shape).astype(np.float32)
