@@ -224,24 +224,71 @@ __global__ __launch_bounds__(256) void k_project(const float *__restrict__ phi,
 
 // ------------------------------------------------------------ epilogue
 // clean_divergence_fast phi sweep (v5.py:250-253) in the serial lexicographic
-// order: a single workgroup walks the anti-diagonals d = i + j; every cell of
-// a diagonal depends only on earlier diagonals (W, S: new) and later ones
+// order: a single workgroup walks the anti-diagonals; every cell of a
+// diagonal depends only on earlier diagonals (W, S: new) and later ones
 // (E, N: old), so updating one diagonal at a time reproduces the serial loop
-// exactly.  Global memory stays coherent inside one workgroup (one CU).
+// exactly.  Thread t owns row b0+t of a band of blockDim rows and updates
+// column j = s - t + 1 at step s, so the NEW values never go through global
+// memory: W is the thread's own last output (a register), S the output of
+// thread t-1 one step earlier (LDS, double-buffered by step parity, one
+// barrier per step).  The OLD values -- E, div, and N -- are fetched PD steps
+// ahead (N within a wave is lane t+1's E of the same step, by DPP).  Row b0-1
+// (the previous band, finished) and the boundary rows are fetched like E.
 __global__ __launch_bounds__(1024) void k_lex_gs_sweep(float *__restrict__ phi,
                                                        const float *__restrict__ div, int ny,
                                                        int nx, float cx, float cy, float cd) {
+    constexpr int PD = 4;  // prefetch distance (steps)
+    __shared__ float outb[2][1024];
+    const int t = threadIdx.x, nt = blockDim.x, lane = t & 63;
     const int imax = ny - 2, jmax = nx - 2;
-    for (int d = 2; d <= imax + jmax; ++d) {
-        const int ilo = max(1, d - jmax), ihi = min(imax, d - 1);
-        for (int i = ilo + (int)threadIdx.x; i <= ihi; i += blockDim.x) {
-            const int j = d - i;
-            const size_t c = (size_t)i * nx + j;
-            const float a = cx * (phi[c + 1] + phi[c - 1]);
-            const float b = cy * (phi[c + nx] + phi[c - nx]);
-            phi[c] = ((a + b) - div[c]) * cd;
-        }
+    for (int b0 = 1; b0 <= imax; b0 += nt) {
+        __threadfence();  // the previous band's rows are final and visible
         __syncthreads();
+        const int nrows = min(nt, imax - b0 + 1);
+        const int i = b0 + t;
+        const bool rowok = t < nrows;
+        const size_t rowc = (size_t)(rowok ? i : 0) * nx;
+        // N from memory for the last row of the band / grid and for lane 63
+        // (its lower neighbour row is in another wave); S for thread 0
+        const bool nmem = lane == 63 || t == nrows - 1;
+        float qE[PD], qD[PD], qN[PD], qS[PD];
+        auto fetch = [&](int st, float &e, float &d, float &n, float &sv) {
+            const int j = st - t + 1;
+            const bool act = rowok && j >= 1 && j <= jmax;
+            e = (rowok && j >= 0 && j <= jmax) ? phi[rowc + j + 1] : 0.f;
+            d = act ? div[rowc + j] : 0.f;
+            n = (act && nmem) ? phi[rowc + j + nx] : 0.f;
+            sv = (act && t == 0) ? phi[rowc + j - nx] : 0.f;
+        };
+#pragma unroll
+        for (int p = 0; p < PD; ++p) fetch(p, qE[p], qD[p], qN[p], qS[p]);
+        float w = rowok ? phi[rowc] : 0.f;  // phi(i, 0): W of column 1
+        const int nsteps = nrows - 1 + jmax;
+        for (int st = 0; st < nsteps; ++st) {
+            const int j = st - t + 1;
+            const bool act = rowok && j >= 1 && j <= jmax;
+            const float E = qE[0], D = qD[0], Nm = qN[0], S0 = qS[0];
+            const float nup = dpp_from_upper(E);  // lane t+1's E: old phi(i+1, j)
+#pragma unroll
+            for (int p = 0; p + 1 < PD; ++p) {
+                qE[p] = qE[p + 1];
+                qD[p] = qD[p + 1];
+                qN[p] = qN[p + 1];
+                qS[p] = qS[p + 1];
+            }
+            fetch(st + PD, qE[PD - 1], qD[PD - 1], qN[PD - 1], qS[PD - 1]);
+            if (act) {
+                const float S = t == 0 ? S0 : outb[(st + 1) & 1][t - 1];  // thread t-1 at step st-1
+                const float N = nmem ? Nm : nup;
+                const float a = cx * (E + w);
+                const float b = cy * (N + S);
+                const float v = ((a + b) - D) * cd;
+                phi[rowc + j] = v;
+                w = v;
+                outb[st & 1][t] = v;
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -505,7 +552,9 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
         hipLaunchKernelGGL(k_divergence, grid2d(ny, nx), dim3(256), 0, s, u, v, div, ny, nx, cx, cy,
                            (float *)nullptr);
         if (ny > 2 && nx > 2)
-            hipLaunchKernelGGL(k_lex_gs_sweep, dim3(1), dim3(1024), 0, s, phi, div, ny, nx,
+            // one thread per row of a band: as many waves as rows (idle
+            // waves would only add barrier traffic to every step)
+            hipLaunchKernelGGL(k_lex_gs_sweep, dim3(1), dim3(ny - 2 >= 1024 ? 1024 : 64 * ceil_div(ny - 2, 64)), 0, s, phi, div, ny, nx,
                                (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
         hipLaunchKernelGGL(k_sub_gradient, grid2d(ny, nx), dim3(256), 0, s, phi, u, v, ny, nx, cx,
                            cy);
