@@ -713,50 +713,76 @@ __global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
 }
 
 // rbgs2d_tb for small grids: each wave owns TWO output rows and loads every
-// row it needs up front (level 0 rows y0-2 .. y0+3, div / mask rows y0-1 ..
-// y0+2), so a pass is one load latency, the two colour levels, and the
-// stores -- no row march with a load per step.  The 600 x 180 cylinder pass
-// (latency-bound) drops from ~9 us to ~? us.  Same cells, same
-// operation order and same max|change| accounting as rbgs2d_tb.
-template <bool MASK>
-__global__ __launch_bounds__(256) void rbgs2d_tb2r(const float *__restrict__ in,
-                                                   float *__restrict__ out,
-                                                   const float *__restrict__ div,
-                                                   const uint8_t *__restrict__ mask, int ny, int nx,
-                                                   int nseg, float cx, float cy, float cd,
-                                                   float dt_inv, float tol, RbgsWs *ws, int it) {
+// row it needs up front, so a pass is one load latency, the colour levels and
+// the stores -- no row march with a load per step.  NI = 2 fuses two
+// iterations (four colour levels: level 0 rows y0-4 .. y0+5, div / mask rows
+// y0-3 .. y0+4; the halo lane of 4 cells absorbs the 4-cell x-erosion).  A
+// stop after the first iteration of a pair is undone after the loop by a
+// rollback run of that iteration alone (NI = 1, rollback != 0: it reads the
+// count and re-runs iteration 2m from the pair's input buffer, which no later
+// pass overwrote), as the 3-D pair passes do.  Same cells, operation order
+// and max|change| accounting as rbgs2d_tb (own rows; halo rows repeat a
+// neighbour chunk's values).
+template <bool MASK, int NI>
+__global__ __launch_bounds__(256) void rbgs2d_small(const float *__restrict__ in,
+                                                    float *__restrict__ out,
+                                                    const float *__restrict__ div,
+                                                    const uint8_t *__restrict__ mask, int ny, int nx,
+                                                    int nseg, float cx, float cy, float cd,
+                                                    float dt_inv, float tol, RbgsWs *ws, int it,
+                                                    int rollback, int npairs) {
     constexpr int VEC = 4;
     constexpr int SOUT = 64 * VEC - 2 * VEC;
-    const float prev = it > 0 ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 1]) : 0.f;
-    const bool stopped = it > 0 && prev < tol;
-    if (stopped && blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&ws->flags[1], it);
+    constexpr int L = 2 * NI;            // colour levels
+    constexpr int NR0 = 2 + 2 * L;       // level-0 rows y0-L .. y0+1+L
+    constexpr int ND = 2 + 2 * (L - 1);  // div / mask rows y0-(L-1) .. y0+L
+    bool stopped = false;
+    if (rollback) {
+        const int c = ws->flags[1];
+        if (!((c & 1) && (c - 1) / 2 < npairs)) return;  // grid-uniform
+        if (((c - 1) / 2) & 1) {                           // pair m read phi_tmp
+            float *t_ = const_cast<float *>(in);
+            in = out;
+            out = t_;
+        }
+    } else {
+        // the stop test's loads are issued here but acted on after the row
+        // loads, so the latencies overlap; a pair skips when either iteration
+        // of the previous pair met the tolerance
+        const float p1 = it > 0 ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 1]) : 0.f;
+        const float p2 = (NI == 2 && it > 1) ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 2]) : 0.f;
+        stopped = (it > 0 && p1 < tol) || (NI == 2 && it > 1 && p2 < tol);
+        if (stopped && blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&ws->flags[1], it);
+    }
     const int lane = threadIdx.x & 63;
-    const int wpb = blockDim.x / 64;
     const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
-    const long wave = (long)bid * wpb + threadIdx.x / 64;
+    const long wave = (long)bid * 4 + threadIdx.x / 64;
     const int seg = (int)(wave % nseg);
     const int y0 = 1 + 2 * (int)(wave / nseg);
-    float mx = 0.f;
+    float mx[NI];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) mx[q] = 0.f;
     if (y0 < ny - 1) {  // wave-uniform
         const int y1 = min(y0 + 2, ny - 1);
         const int x0 = seg * SOUT - VEC + lane * VEC;
         const bool valid = x0 >= 0 && x0 < nx;
         const bool writer = lane >= 1 && lane <= 62 && valid;
         auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
-        float L0[6][VEC], D[4][VEC];  // level 0 rows y0-2+i, div rows y0-1+i
-        uint8_t Mk[4][VEC];
+        float A[NR0][VEC];  // level l lives in rows [l, NR0 - l) of A (row i = y0 - L + i)
+        float D[ND][VEC];   // div row y0 - (L-1) + i
+        uint8_t Mk[ND][VEC];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
+        for (int i = 0; i < NR0; ++i) {
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) L0[i][k] = 0.f;
-            const int y = y0 - 2 + i;
-            if (valid && y >= 0 && y <= ny - 1) ld<float, VEC>(in + row(y), L0[i]);
+            for (int k = 0; k < VEC; ++k) A[i][k] = 0.f;
+            const int y = y0 - L + i;
+            if (valid && y >= 0 && y <= ny - 1) ld<float, VEC>(in + row(y), A[i]);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < ND; ++i) {
 #pragma unroll
             for (int k = 0; k < VEC; ++k) { D[i][k] = 0.f; Mk[i][k] = 0; }
-            const int y = y0 - 1 + i;
+            const int y = y0 - (L - 1) + i;
             if (valid && y >= 0 && y <= ny - 1) {
                 ld<float, VEC>(div + row(y), D[i]);
                 if (MASK) {  // 4 mask bytes in one load (nx % 4 == 0, x0 % 4 == 0)
@@ -767,68 +793,88 @@ __global__ __launch_bounds__(256) void rbgs2d_tb2r(const float *__restrict__ in,
             }
         }
         if (!stopped) {
-        // level 1 (colour 0) of rows y0-1 .. y0+2
-        float L1[4][VEC];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = y0 - 1 + i;
-            const bool edge = r == 0 || r == ny - 1;
-            const float *ac = L0[i + 1];
-            const float wl = dpp_from_lower(ac[VEC - 1]);
-            const float er = dpp_from_upper(ac[0]);
+            for (int l = 1; l <= L; ++l) {
+                const int par = (l - 1) & 1;  // colour of this level
+                float B[NR0][VEC];
+                // rows [l, NR0 - l): level l from level l-1 (rows i-1, i, i+1)
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const int x = x0 + k;
-                L1[i][k] = ac[k];
-                if (!edge && x >= 1 && x < nx - 1 && ((r + x + 1) & 1) == 0 && !(MASK && Mk[i][k])) {
-                    const float E = (k + 1 < VEC) ? ac[k + 1] : er;
-                    const float W = (k > 0) ? ac[k - 1] : wl;
-                    L1[i][k] = gs5(E, W, L0[i + 2][k], L0[i][k], D[i][k], cx, cy, cd, dt_inv);
-                    // rows y0-1 .. y1 as rbgs2d_tb counts them (halo rows repeat
-                    // a neighbour chunk's values; a row past y1 may be outside
-                    // the grid); halo lanes 0 / 63 are not counted
-                    const float ch = fabsf(L1[i][k] - ac[k]);
-                    if (writer && r <= y1 && ch > mx) mx = ch;
-                }
-            }
-        }
-        // level 2 (colour 1) of rows y0, y0+1
+                for (int i = l; i < NR0 - l; ++i) {
+                    const int r = y0 - L + i;
+                    const bool edge = r <= 0 || r >= ny - 1;
+                    const float *ac = A[i];
+                    const float wl = dpp_from_lower(ac[VEC - 1]);
+                    const float er = dpp_from_upper(ac[0]);
+                    const int di = i - 1;  // div / mask row index of row r
 #pragma unroll
-        for (int i = 1; i <= 2; ++i) {
-            const int p = y0 - 1 + i;
-            if (p >= y1) break;
-            const float *bc = L1[i];
-            const float wl1 = dpp_from_lower(bc[VEC - 1]);
-            const float er1 = dpp_from_upper(bc[0]);
-            if (writer) {
-                float o[VEC];
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    const int x = x0 + k;
-                    o[k] = bc[k];
-                    if (x >= 1 && x < nx - 1 && ((p + x + 2) & 1) == 0 && !(MASK && Mk[i][k])) {
-                        const float E = (k + 1 < VEC) ? bc[k + 1] : er1;
-                        const float W = (k > 0) ? bc[k - 1] : wl1;
-                        o[k] = gs5(E, W, L1[i + 1][k], L1[i - 1][k], D[i][k], cx, cy, cd, dt_inv);
-                        const float ch = fabsf(o[k] - bc[k]);
-                        if (ch > mx) mx = ch;
+                    for (int k = 0; k < VEC; ++k) {
+                        const int x = x0 + k;
+                        B[i][k] = ac[k];
+                        if (!edge && x >= 1 && x < nx - 1 && ((r + x + 1 + par) & 1) == 0 &&
+                            !(MASK && Mk[di][k])) {
+                            const float E = (k + 1 < VEC) ? ac[k + 1] : er;
+                            const float W = (k > 0) ? ac[k - 1] : wl;
+                            B[i][k] = gs5(E, W, A[i + 1][k], A[i - 1][k], D[di][k], cx, cy, cd, dt_inv);
+                            const float ch = fabsf(B[i][k] - ac[k]);
+                            if (writer && r >= y0 && r < y1 && ch > mx[(l - 1) / 2]) mx[(l - 1) / 2] = ch;
+                        }
                     }
                 }
-                st<float, VEC>(out + row(p), o);
+#pragma unroll
+                for (int i = l; i < NR0 - l; ++i)
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) A[i][k] = B[i][k];
+            }
+            if (writer) {
+#pragma unroll
+                for (int i = L; i < L + 2; ++i) {
+                    const int p = y0 - L + i;
+                    if (p < y1) st<float, VEC>(out + row(p), A[i]);
+                }
             }
         }
-        }  // !stopped
     }
-    // one atomic per workgroup, without the read-first guard (a dependent
-    // load at the end of a few-microsecond kernel)
-    __shared__ float red[4];
-    const float m = wave_max(mx);
-    if (lane == 0) red[threadIdx.x / 64] = m;
+    if (rollback) return;
+    // one atomic per workgroup and iteration, no read-first guard (a
+    // dependent load at the end of a few-microsecond kernel)
+    __shared__ float red[NI][4];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+        const float m = wave_max(mx[q]);
+        if (lane == 0) red[q][threadIdx.x / 64] = m;
+    }
     __syncthreads();
-    if (threadIdx.x == 0 && !stopped) {
-        const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-        if (b > 0.0f) atomic_max_nonneg(&ws->maxc[it], b);
+    if (threadIdx.x < NI && !stopped) {
+        const int q = threadIdx.x;
+        const float b = fmaxf(fmaxf(red[q][0], red[q][1]), fmaxf(red[q][2], red[q][3]));
+        if (b > 0.0f) atomic_max_nonneg(&ws->maxc[it + q], b);
     }
+}
+
+// Small grid: launch rbgs2d_small (NI iterations from `it`; rollback mode
+// re-runs the first iteration of the pair the stop fell in).
+static void rbgs2d_small_launch(int NI, const float *in, float *out, const float *div,
+                                const uint8_t *mask, int ny, int nx, float cx, float cy, float cd,
+                                float dt_inv, float tol, RbgsWs *ws, int it, int rollback, int npairs,
+                                hipStream_t s) {
+    constexpr int SOUT = 64 * 4 - 2 * 4;
+    const int nseg = ceil_div(nx, SOUT);
+    const int blocks = ceil_div((long)nseg * ceil_div(ny - 2, 2), 4);
+#define CFD_GSS(M, N)                                                                                \
+    hipLaunchKernelGGL((rbgs2d_small<M, N>), dim3(blocks), dim3(256), 0, s, in, out, div, mask, ny, nx, \
+                       nseg, cx, cy, cd, dt_inv, tol, ws, it, rollback, npairs)
+    if (mask) {
+        if (NI == 2) CFD_GSS(true, 2); else CFD_GSS(true, 1);
+    } else {
+        if (NI == 2) CFD_GSS(false, 2); else CFD_GSS(false, 1);
+    }
+#undef CFD_GSS
+}
+
+// rbgs2d_small serves grids whose row march would use chunks of <= 2 rows
+static bool rbgs2d_small_grid(int ny, int nx) {
+    const int nseg = ceil_div(nx, 64 * 4 - 2 * 4);
+    return ceil_div((long)(ny - 2) * nseg, 8192) <= 2;
 }
 
 static int rbgs2d_tb_pass(const float *in, float *out, const float *div, const uint8_t *mask,
@@ -841,15 +887,8 @@ static int rbgs2d_tb_pass(const float *in, float *out, const float *div, const u
     // 2-row chunks give 267 waves (8-row chunks: 69 waves, 11.3 us per
     // iteration, latency-bound); the re-marched row per chunk is cheap there
     int rpc = ceil_div((long)rows * nseg, 8192);
-    if (rpc <= 2) {
-        // small grid: two-row chunks with every row loaded up front
-        const int blocks = ceil_div((long)nseg * ceil_div(rows, 2), 4);
-        if (mask)
-            hipLaunchKernelGGL(rbgs2d_tb2r<true>, dim3(blocks), dim3(256), 0, s, in, out, div, mask, ny, nx,
-                               nseg, cx, cy, cd, dt_inv, tol, ws, it);
-        else
-            hipLaunchKernelGGL(rbgs2d_tb2r<false>, dim3(blocks), dim3(256), 0, s, in, out, div, mask, ny,
-                               nx, nseg, cx, cy, cd, dt_inv, tol, ws, it);
+    if (rpc <= 2) {  // small grid: one iteration of the preloaded kernel
+        rbgs2d_small_launch(1, in, out, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, ws, it, 0, 0, s);
         CFD_LAUNCH_CHECK();
         return CFD_OK;
     }
@@ -988,6 +1027,26 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
         // fused: one out-of-place pass per iteration (both colours), ping-pong
         if ((rc = fix_edge_rows<float>(phi, phi_tmp, nullptr, ny, nx, s))) return rc;
         float *a = phi, *b = phi_tmp;
+        if (rbgs2d_small_grid(ny, nx)) {
+            // small grid (the v5 cylinder): two iterations per launch, a single
+            // one for an odd remainder, the rollback of a stop inside a pair
+            const int npairs = iterations / 2;
+            for (int it = 0; it < iterations;) {
+                const int m = iterations - it >= 2 ? 2 : 1;
+                rbgs2d_small_launch(m, a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, 0, 0, s);
+                CFD_LAUNCH_CHECK();
+                it += m;
+                float *t = a; a = b; b = t;
+            }
+            timing_end(tk, s, iterations);
+            if ((rc = launch_rbgs_count(w, iters_done, s))) return rc;
+            if (npairs > 0) {
+                rbgs2d_small_launch(1, phi, phi_tmp, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, 0, 1,
+                                    npairs, s);
+                CFD_LAUNCH_CHECK();
+            }
+            return launch_rbgs_copy(w, phi, phi_tmp, (size_t)ny * nx, 2, s);
+        }
         for (int it = 0; it < iterations; ++it) {
             if ((rc = rbgs2d_tb_pass(a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, s)))
                 return rc;
