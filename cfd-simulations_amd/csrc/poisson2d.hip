@@ -407,6 +407,128 @@ static int jacobi2d_tbk_pass(int K, const T *in, T *out, const T *div, const uin
     return CFD_OK;
 }
 
+// K-level Jacobi for small grids (the v5 cylinder, config 1): each wave owns
+// two output rows and loads every row it needs up front (level 0 rows
+// y0-K .. y0+1+K, rhs / mask rows y0-(K-1) .. y0+K), so a pass of K sweeps is
+// one load latency plus K levels of VALU -- the row march of jacobi2d_tbk is a
+// chain of row-step latencies on a grid too small to hide them.  x-segments
+// overlap by HL = ceil(K/VEC) halo lanes (erosion), as in jacobi2d_tbk; same
+// operation order, fixed rows / columns and mask rule, bit-identical.
+template <typename T, int VEC, int K, bool PRE, bool MASK>
+__global__ __launch_bounds__(256) void jacobi2d_small(const T *__restrict__ in, T *__restrict__ out,
+                                                      const T *__restrict__ div,
+                                                      const uint8_t *__restrict__ mask, int ny, int nx,
+                                                      int nseg, T dx2, T dtv) {
+    constexpr int HL = (K + VEC - 1) / VEC;
+    constexpr int SOUT = (64 - 2 * HL) * VEC;
+    constexpr int NR0 = 2 + 2 * K;
+    constexpr int ND = 2 * K;  // rows y0-(K-1) .. y0+K
+    const int lane = threadIdx.x & 63;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const long wave = (long)bid * 4 + threadIdx.x / 64;
+    const int seg = (int)(wave % nseg);
+    const int y0 = 1 + 2 * (int)(wave / nseg);
+    if (y0 >= ny - 1) return;  // wave-uniform
+    const int y1 = min(y0 + 2, ny - 1);
+    const int x0 = seg * SOUT - HL * VEC + lane * VEC;
+    const bool valid = x0 >= 0 && x0 < nx;
+    const bool writer = lane >= HL && lane < 64 - HL && valid;
+    auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
+    T A[NR0][VEC];  // level l in rows [l, NR0 - l) (row i = y0 - K + i)
+    T R[ND][VEC];   // rhs row y0 - (K-1) + i
+    uint8_t M[ND][VEC];
+#pragma unroll
+    for (int i = 0; i < NR0; ++i) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) A[i][k] = T(0);
+        const int y = y0 - K + i;
+        if (valid && y >= 0 && y <= ny - 1) ld<T, VEC>(in + row(y), A[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) { R[i][k] = T(0); M[i][k] = 0; }
+        const int y = y0 - (K - 1) + i;
+        if (valid && y >= 0 && y <= ny - 1) {
+            ld<T, VEC>(div + row(y), R[i]);
+            if (MASK) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) M[i][k] = mask[row(y) + k];
+            }
+        }
+    }
+#pragma unroll
+    for (int l = 1; l <= K; ++l) {
+        T B[NR0][VEC];
+#pragma unroll
+        for (int i = l; i < NR0 - l; ++i) {
+            const int p = y0 - K + i;
+            const bool fixed = p == 0 || p == ny - 1;
+            const int di = i - 1;  // rhs / mask row of row p
+            const T wl = dpp_from_lower(A[i][VEC - 1]);
+            const T er = dpp_from_upper(A[i][0]);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const T E = (k + 1 < VEC) ? A[i][k + 1] : er;
+                const T W = (k > 0) ? A[i][k - 1] : wl;
+                const int x = x0 + k;
+                T val = (fixed || x <= 0 || x >= nx - 1)
+                            ? A[i][k]
+                            : jac5<T>(E, W, A[i + 1][k], A[i - 1][k], R[di][k], dx2, dtv, PRE);
+                if (MASK && M[di][k]) val = T(0);
+                B[i][k] = val;
+            }
+        }
+#pragma unroll
+        for (int i = l; i < NR0 - l; ++i)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) A[i][k] = B[i][k];
+    }
+    if (writer) {
+#pragma unroll
+        for (int i = K; i < K + 2; ++i) {
+            const int p = y0 - K + i;
+            if (p < y1) st<T, VEC>(out + row(p), A[i]);
+        }
+    }
+}
+
+template <typename T, int VEC>
+static int jacobi2d_small_pass(int K, const T *in, T *out, const T *div, const uint8_t *mask, int ny,
+                               int nx, T dx2, T dtv, bool pre, hipStream_t s) {
+    if (ny - 2 <= 0) return CFD_OK;
+#define CFD_J2S(KV, PR, M)                                                                           \
+    do {                                                                                             \
+        constexpr int HL_ = (KV + VEC - 1) / VEC;                                                    \
+        const int nseg = ceil_div(nx, (64 - 2 * HL_) * VEC);                                         \
+        const int blocks = ceil_div((long)nseg * ceil_div(ny - 2, 2), 4);                            \
+        hipLaunchKernelGGL((jacobi2d_small<T, VEC, KV, PR, M>), dim3(blocks), dim3(256), 0, s, in, out, \
+                           div, mask, ny, nx, nseg, dx2, dtv);                                       \
+    } while (0)
+#define CFD_J2SK(KV)                                                              \
+    do {                                                                          \
+        if (mask) {                                                               \
+            if (pre) CFD_J2S(KV, true, true); else CFD_J2S(KV, false, true);      \
+        } else {                                                                  \
+            if (pre) CFD_J2S(KV, true, false); else CFD_J2S(KV, false, false);    \
+        }                                                                         \
+    } while (0)
+    switch (K) {
+        case 1: CFD_J2SK(1); break;
+        case 2: CFD_J2SK(2); break;
+        case 3: CFD_J2SK(3); break;
+        case 4: CFD_J2SK(4); break;
+        case 5: CFD_J2SK(5); break;
+        case 6: CFD_J2SK(6); break;
+        case 7: CFD_J2SK(7); break;
+        default: CFD_J2SK(8); break;
+    }
+#undef CFD_J2SK
+#undef CFD_J2S
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
 static int g_j2_blocking = 0;  // sweeps per pass: 0 auto, 1 off, 2..6, 8, 10, 12
 // r01 at 8192^2 f64 (Gcell/s): K=2 368, 3 554, 4 752, 5 876, 6 1051, 8 1232,
 // 10 1228, 12 1155 (the pass turns latency-bound past 8 levels)
@@ -462,13 +584,17 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
     const int tk = timing_begin(s);
     if (g_j2_blocking != 1 && vec_ok && resid_every <= 0 && iters >= 2 && ny >= 3) {
         // temporally blocked: passes of K sweeps, the remainder last
-        const int K = g_j2_blocking >= 2 ? g_j2_blocking : auto_levels2d<T>(ny, nx);
+        // small grids (auto depth 2) take the preloaded kernel, 4 sweeps a pass
+        const bool small = g_j2_blocking == 0 && auto_levels2d<T>(ny, nx) != kDefaultLevels2d;
+        static const int ks = [] { const char *e = getenv("CFD_J2_SMALL_K"); return e ? atoi(e) : 4; }();
+        const int K = small ? ks : g_j2_blocking >= 2 ? g_j2_blocking : auto_levels2d<T>(ny, nx);
         int done = 0;
         while (done < iters) {
             int k = iters - done < K ? iters - done : K;
-            if (k == 7 || k == 9 || k == 11) --k;  // instantiated depths: 2..6, 8, 10, 12
-            rc = k == 1 ? jacobi2d_sweep<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, nullptr, s)
-                        : jacobi2d_tbk_pass<T, V>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, s);
+            if (!small && (k == 7 || k == 9 || k == 11)) --k;  // tbk depths: 2..6, 8, 10, 12
+            rc = small    ? jacobi2d_small_pass<T, V>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, s)
+                 : k == 1 ? jacobi2d_sweep<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, nullptr, s)
+                          : jacobi2d_tbk_pass<T, V>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, s);
             if (rc) return rc;
             if (done == 0 && (rc = fix_edge_rows<T>(tmp, phi, nullptr, ny, nx, s))) return rc;
             done += k;
