@@ -292,22 +292,31 @@ __global__ __launch_bounds__(1024) void k_lex_gs_sweep(float *__restrict__ phi,
     }
 }
 
-// The same sweep with its old-value stream kept in flight.  In the kernel
-// above every step drains the memory queue (__syncthreads waits vmcnt(0), and
-// the register queue's moves wait on their loads), so each of the ~1000
-// dependent steps pays a full memory latency.  Here the old values travel
-// memory -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds), LX blocks of 4 steps
-// ahead, into a ring ring[LX][field][thread] of float4: lane t's window for a
-// block is 4 consecutive columns of its own row (E, div), of the row below (N,
-// lane 63 and the last row only) and of the row above (S, thread 0 only); the
-// other lanes get an out-of-range offset and cost no memory access.  Results
-// are written once per block: one dwordx4 store for a lane whose 4 columns are
-// all interior, single-dword stores at the row ends.  Every memory operation
-// is inline asm in a fixed order, so the wait for block b is an exact count:
-// after block b's 4 DMAs come that block's 5 stores and (LX-1) x (4 DMAs + 5
-// stores).  The per-step barrier waits only for LDS.  Needs n*4 < 2^31 (32-bit
+// The same sweep with its old-value stream kept in flight and no per-step
+// barrier.  In the kernel above every step drains the memory queue
+// (__syncthreads waits vmcnt(0), and the register queue's moves wait on their
+// loads), so each of the ~1000 dependent steps pays a full memory latency.
+// Here:
+//  * the old values travel memory -> LDS by LDS-DMA (buffer_load_dwordx4 ...
+//    lds), LX blocks of 4 steps ahead, into a ring ring[LX][field][thread] of
+//    float4: lane t's window for a block is 4 consecutive columns of its own
+//    row (E, div), of the row below (N: lane 63 and the last row only) and of
+//    the row above (S: thread 0 only); other lanes get an out-of-range offset
+//    and cost no memory access;
+//  * S inside a wave is lane t-1's output of the previous step, by DPP; N is
+//    lane t+1's E (old values), by DPP;
+//  * wave k runs kLexLag steps behind wave k-1 and takes the row above from
+//    wave k-1's lane-63 outputs in a small LDS ring written at least one
+//    barrier phase earlier, so the waves synchronise once per kLexLag steps;
+//  * results are written once per block: one dwordx4 store for a lane whose 4
+//    columns are all interior, single-dword stores at the row ends.
+// Every memory operation of the step loop is inline asm in a fixed order, so
+// the wait for block b is an exact count: after block b's 4 DMAs come that
+// block's 5 stores and (LX-1) x (4 DMAs + 5 stores).  Needs n*4 < 2^31 (32-bit
 // buffer offsets; kOob = 2^31 is the out-of-range offset).
-constexpr int kLexLX = 4;  // blocks of prefetch (16 steps)
+constexpr int kLexLX = 4;    // blocks of prefetch (16 steps)
+constexpr int kLexLag = 16;  // steps between waves = steps per barrier phase
+constexpr int kLexRing = 4 * kLexLag;  // lane-63 output ring per wave (steps)
 __device__ inline void lex_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ inline void buf_store_x4(float4 v, uint32_t ofs, v4i32 rs) {
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -322,10 +331,10 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
                                                           const float *__restrict__ div, int ny,
                                                           int nx, float cx, float cy, float cd) {
     constexpr int LX = kLexLX;
-    extern __shared__ float4 lex_lds[];  // ring[LX][4][nt] float4, then outb[2][nt] float
+    extern __shared__ float4 lex_lds[];  // ring[LX][4][nt] float4, then below[nwaves][kLexRing] float
     const int t = threadIdx.x, nt = blockDim.x, lane = t & 63, wv = t >> 6;
     float4 *ring = lex_lds;
-    float *outb = reinterpret_cast<float *>(lex_lds + LX * 4 * nt);
+    float *below = reinterpret_cast<float *>(lex_lds + LX * 4 * nt);  // wave k's lane-63 outputs by step
     const long n = (long)ny * nx;
     const v4i32 rp = buf_rsrc4(phi, (uint32_t)(n * 4)), rd = buf_rsrc4(div, (uint32_t)(n * 4));
     const int imax = ny - 2, jmax = nx - 2;
@@ -334,10 +343,12 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
         __threadfence();  // the previous band's rows are final and visible
         __syncthreads();  // (and its DMAs have landed: the fence drained vmcnt)
         const int nrows = min(nt, imax - b0 + 1);
+        const int nwaves = (nrows + 63) / 64;
         const int i = b0 + t;
         const bool rowok = t < nrows;
         const long rowc = (long)(rowok ? i : 0) * nx;
         const bool nmem = lane == 63 || t == nrows - 1;
+        const int lag = wv * kLexLag;  // this wave's step = time - lag
         // block starting at step s0: lane t's columns j0..j0+3, j0 = s0 - t + 1
         auto issue = [&](int s0, int slot) {
             const long j0 = s0 - t + 1;
@@ -347,43 +358,52 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
             dma_row(rp, rowok && nmem ? ofs(rowc + nx + j0) : kOob, base + 2 * nt);
             dma_row(rp, rowok && t == 0 ? ofs(rowc - nx + j0) : kOob, base + 3 * nt);
         };
-        auto idle_stores = [&]() {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) buf_store_x1(0.f, kOob, rp);
-        };
         const float w0 = rowok ? phi[rowc] : 0.f;  // phi(i, 0): W of column 1
         wait_vmcnt<0>();  // w0 landed: the waitcnt pass would otherwise drain at every block
 #pragma unroll
         for (int p = 0; p < LX; ++p) {
-            issue(4 * p, p);
-            idle_stores();
+            issue(4 * p - lag, p);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) buf_store_x1(0.f, kOob, rp);  // the loop's store slots
         }
-        float w = w0;
-        const int nblocks = (nrows - 1 + jmax + 3) / 4;  // steps past the last are idle for all rows
-        for (int b = 0; b < nblocks; ++b) {
-            const int s0 = 4 * b, slot = b % LX;
+        float w = w0, vprev = 0.f;
+        // time blocks: the last wave's last step, rounded up to whole phases
+        const int tsteps = nrows - 1 + jmax + (nwaves - 1) * kLexLag;
+        const int nblocks = (tsteps + kLexLag - 1) / kLexLag * (kLexLag / 4);
+        const float *above = below + (wv - 1) * kLexRing;  // wave k-1's ring (wv >= 1)
+        for (int tb = 0; tb < nblocks; ++tb) {
+            const int s0 = 4 * tb - lag, slot = tb % LX;
             wait_vmcnt<5 + 9 * (LX - 1)>();
             const float4 *rb = ring + (size_t)slot * 4 * nt + t;
             const float4 e4 = rb[0], d4 = rb[nt], n4 = rb[2 * nt], s4 = rb[3 * nt];
+            float sa[4] = {s4.x, s4.y, s4.z, s4.w};
+            if (lane == 0 && wv > 0) {  // row above = wave k-1's lane 63, steps s0-1 .. s0+2
+#pragma unroll
+                for (int k = 0; k < 4; ++k) sa[k] = above[(s0 - 1 + k) & (kLexRing - 1)];
+            }
             const float ea[4] = {e4.x, e4.y, e4.z, e4.w}, da[4] = {d4.x, d4.y, d4.z, d4.w};
-            const float na[4] = {n4.x, n4.y, n4.z, n4.w}, sa[4] = {s4.x, s4.y, s4.z, s4.w};
+            const float na[4] = {n4.x, n4.y, n4.z, n4.w};
             const int j0 = s0 - t + 1;
             float res[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int s = s0 + k, j = j0 + k;
+                const int j = j0 + k;
                 const bool act = rowok && j >= 1 && j <= jmax;
                 const float E = ea[k];
-                const float nup = dpp_from_upper(E);  // lane t+1's E: old phi(i+1, j)
-                const float S = t == 0 ? sa[k] : outb[((s + 1) & 1) * nt + t - 1];  // thread t-1 at step s-1
+                const float nup = dpp_from_upper(E);     // lane t+1's E: old phi(i+1, j)
+                const float sup = dpp_from_lower(vprev);  // lane t-1 at step s-1: new phi(i-1, j)
+                const float S = lane == 0 ? sa[k] : sup;
                 const float N = nmem ? na[k] : nup;
                 const float a = cx * (E + w);
                 const float bb = cy * (N + S);
                 const float v = ((a + bb) - da[k]) * cd;
                 w = act ? v : w;
+                vprev = v;
                 res[k] = v;
-                outb[(s & 1) * nt + t] = v;
-                lex_lds_barrier();
+            }
+            if (lane == 63) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) below[wv * kLexRing + ((s0 + k) & (kLexRing - 1))] = res[k];
             }
             issue(s0 + 4 * LX, slot);
             const bool full = rowok && j0 >= 1 && j0 + 3 <= jmax;
@@ -394,10 +414,13 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
                 const bool act = rowok && !full && j >= 1 && j <= jmax;
                 buf_store_x1(res[k], act ? (uint32_t)((rowc + j) * 4) : kOob, rp);
             }
+            if ((tb + 1) % (kLexLag / 4) == 0) lex_lds_barrier();
         }
     }
 }
-size_t lex_dma_lds_bytes(int nt) { return (size_t)kLexLX * 4 * nt * sizeof(float4) + 2 * (size_t)nt * sizeof(float); }
+size_t lex_dma_lds_bytes(int nt) {
+    return (size_t)kLexLX * 4 * nt * sizeof(float4) + (size_t)(nt / 64) * kLexRing * sizeof(float);
+}
 
 // u[1:-1,1:-1] -= grad_x[1:-1,1:-1] (no dt: v5.py:255-256)
 __global__ void k_sub_gradient(const float *__restrict__ phi, float *__restrict__ u,
@@ -663,7 +686,12 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
             // waves would only add barrier traffic to every step)
             if (n * 4 < ((size_t)1 << 31)) {
                 // bands of at most 512 rows (the ring's LDS), one wave per 64 rows
-                const int nt = ny - 2 >= 512 ? 512 : 64 * ceil_div(ny - 2, 64);
+                static const int band = [] {
+                    const char *e = getenv("CFD_LEX_BAND");  // rows per band (A/B knob)
+                    const int b = e ? atoi(e) : 512;
+                    return b >= 64 && b <= 512 ? b / 64 * 64 : 512;
+                }();
+                const int nt = ny - 2 >= band ? band : 64 * ceil_div(ny - 2, 64);
                 const size_t lds = lex_dma_lds_bytes(nt);
                 static bool attr = false;
                 if (!attr) {
