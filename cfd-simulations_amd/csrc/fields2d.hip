@@ -314,7 +314,7 @@ __global__ __launch_bounds__(1024) void k_lex_gs_sweep(float *__restrict__ phi,
 // the wait for block b is an exact count: after block b's 4 DMAs come that
 // block's 5 stores and (LX-1) x (4 DMAs + 5 stores).  Needs n*4 < 2^31 (32-bit
 // buffer offsets; kOob = 2^31 is the out-of-range offset).
-constexpr int kLexLX = 4;    // blocks of prefetch (16 steps)
+constexpr int kLexLX = 4;    // blocks of prefetch (16 steps; 28 measured the same: the loop is issue-bound)
 constexpr int kLexLag = 16;  // steps between waves = steps per barrier phase
 constexpr int kLexRing = 4 * kLexLag;  // lane-63 output ring per wave (steps)
 __device__ inline void lex_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -327,10 +327,23 @@ __device__ inline void buf_store_x1(float v, uint32_t ofs, v4i32 rs) {
     asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(ofs), "s"(rs) : "memory");
 }
 
+// buffer_load_dwordx4 ... lds with the LDS destination given as a (uniform) byte address
+__device__ inline void lex_dma_x4(v4i32 rs, uint32_t ofs, uint32_t lds_addr) {
+    int saved;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "s"(lds_addr), "v"(ofs), "s"(rs)
+        : "memory");
+}
+
+template <int LX>
 __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ phi,
                                                           const float *__restrict__ div, int ny,
                                                           int nx, float cx, float cy, float cd) {
-    constexpr int LX = kLexLX;
     extern __shared__ float4 lex_lds[];  // ring[LX][4][nt] float4, then below[nwaves][kLexRing] float
     const int t = threadIdx.x, nt = blockDim.x, lane = t & 63, wv = t >> 6;
     float4 *ring = lex_lds;
@@ -338,7 +351,6 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
     const long n = (long)ny * nx;
     const v4i32 rp = buf_rsrc4(phi, (uint32_t)(n * 4)), rd = buf_rsrc4(div, (uint32_t)(n * 4));
     const int imax = ny - 2, jmax = nx - 2;
-    auto ofs = [&](long cell) -> uint32_t { return (cell >= 0 && cell + 4 <= n) ? (uint32_t)(cell * 4) : kOob; };
     for (int b0 = 1; b0 <= imax; b0 += nt) {
         __threadfence();  // the previous band's rows are final and visible
         __syncthreads();  // (and its DMAs have landed: the fence drained vmcnt)
@@ -346,23 +358,35 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
         const int nwaves = (nrows + 63) / 64;
         const int i = b0 + t;
         const bool rowok = t < nrows;
-        const long rowc = (long)(rowok ? i : 0) * nx;
+        const uint32_t rowc = (uint32_t)(rowok ? i : 0) * (uint32_t)nx;
         const bool nmem = lane == 63 || t == nrows - 1;
         const int lag = wv * kLexLag;  // this wave's step = time - lag
-        // block starting at step s0: lane t's columns j0..j0+3, j0 = s0 - t + 1
-        auto issue = [&](int s0, int slot) {
-            const long j0 = s0 - t + 1;
-            float4 *base = ring + (size_t)slot * 4 * nt + wv * 64;
-            dma_row(rp, rowok ? ofs(rowc + j0 + 1) : kOob, base);
-            dma_row(rd, rowok ? ofs(rowc + j0) : kOob, base + nt);
-            dma_row(rp, rowok && nmem ? ofs(rowc + nx + j0) : kOob, base + 2 * nt);
-            dma_row(rp, rowok && t == 0 ? ofs(rowc - nx + j0) : kOob, base + 3 * nt);
+        // Time block tb covers this wave's steps s0 = 4 tb - lag .. s0 + 3, lane
+        // t's columns j0 = jb + 4 tb .. j0 + 3.  Every per-lane byte offset is
+        // a band constant plus 16 tb (32-bit; a window outside the row reads
+        // other rows' cells, which no active step uses, or lies past the
+        // buffer and reads zeros; kOob + 16 tb stays out of range).
+        const int jb = 1 - t - lag;
+        const uint32_t oE = rowok ? (rowc + jb + 1) * 4u : kOob;
+        const uint32_t oD = rowok ? (rowc + jb) * 4u : kOob;
+        const uint32_t oN = rowok && nmem ? (rowc + nx + jb) * 4u : kOob;
+        const uint32_t oS = rowok && t == 0 ? (rowc - nx + jb) * 4u : kOob;
+        const uint32_t oW = (rowc + jb) * 4u;
+        const uint32_t la = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(ring + wv * 64));
+        const uint32_t fstride = (uint32_t)nt * 16u;  // bytes per ring field
+        auto issue = [&](int tb, int slot) {  // block tb's windows into ring slot
+            const uint32_t d = 16u * (uint32_t)tb, m = la + (uint32_t)slot * 4u * fstride;
+            lex_dma_x4(rp, oE + d, m);
+            lex_dma_x4(rd, oD + d, m + fstride);
+            lex_dma_x4(rp, oN + d, m + 2 * fstride);
+            lex_dma_x4(rp, oS + d, m + 3 * fstride);
         };
         const float w0 = rowok ? phi[rowc] : 0.f;  // phi(i, 0): W of column 1
         wait_vmcnt<0>();  // w0 landed: the waitcnt pass would otherwise drain at every block
 #pragma unroll
         for (int p = 0; p < LX; ++p) {
-            issue(4 * p - lag, p);
+            issue(p, p);
 #pragma unroll
             for (int k = 0; k < 5; ++k) buf_store_x1(0.f, kOob, rp);  // the loop's store slots
         }
@@ -372,7 +396,7 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
         const int nblocks = (tsteps + kLexLag - 1) / kLexLag * (kLexLag / 4);
         const float *above = below + (wv - 1) * kLexRing;  // wave k-1's ring (wv >= 1)
         for (int tb = 0; tb < nblocks; ++tb) {
-            const int s0 = 4 * tb - lag, slot = tb % LX;
+            const int s0 = 4 * tb - lag, slot = tb % LX, j0 = jb + 4 * tb;
             wait_vmcnt<5 + 9 * (LX - 1)>();
             const float4 *rb = ring + (size_t)slot * 4 * nt + t;
             const float4 e4 = rb[0], d4 = rb[nt], n4 = rb[2 * nt], s4 = rb[3 * nt];
@@ -383,21 +407,20 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
             }
             const float ea[4] = {e4.x, e4.y, e4.z, e4.w}, da[4] = {d4.x, d4.y, d4.z, d4.w};
             const float na[4] = {n4.x, n4.y, n4.z, n4.w};
-            const int j0 = s0 - t + 1;
+            bool act[4];
             float res[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int j = j0 + k;
-                const bool act = rowok && j >= 1 && j <= jmax;
+                act[k] = rowok && (uint32_t)(j0 + k - 1) < (uint32_t)jmax;
                 const float E = ea[k];
-                const float nup = dpp_from_upper(E);     // lane t+1's E: old phi(i+1, j)
+                const float nup = dpp_from_upper(E);      // lane t+1's E: old phi(i+1, j)
                 const float sup = dpp_from_lower(vprev);  // lane t-1 at step s-1: new phi(i-1, j)
                 const float S = lane == 0 ? sa[k] : sup;
                 const float N = nmem ? na[k] : nup;
                 const float a = cx * (E + w);
                 const float bb = cy * (N + S);
                 const float v = ((a + bb) - da[k]) * cd;
-                w = act ? v : w;
+                w = act[k] ? v : w;
                 vprev = v;
                 res[k] = v;
             }
@@ -405,21 +428,18 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
 #pragma unroll
                 for (int k = 0; k < 4; ++k) below[wv * kLexRing + ((s0 + k) & (kLexRing - 1))] = res[k];
             }
-            issue(s0 + 4 * LX, slot);
-            const bool full = rowok && j0 >= 1 && j0 + 3 <= jmax;
-            buf_store_x4(make_float4(res[0], res[1], res[2], res[3]), full ? (uint32_t)((rowc + j0) * 4) : kOob, rp);
+            issue(tb + LX, slot);
+            const uint32_t o = oW + 16u * (uint32_t)tb;
+            const bool full = act[0] && act[3];
+            buf_store_x4(make_float4(res[0], res[1], res[2], res[3]), full ? o : kOob, rp);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int j = j0 + k;
-                const bool act = rowok && !full && j >= 1 && j <= jmax;
-                buf_store_x1(res[k], act ? (uint32_t)((rowc + j) * 4) : kOob, rp);
-            }
+            for (int k = 0; k < 4; ++k) buf_store_x1(res[k], !full && act[k] ? o + 4u * k : kOob, rp);
             if ((tb + 1) % (kLexLag / 4) == 0) lex_lds_barrier();
         }
     }
 }
-size_t lex_dma_lds_bytes(int nt) {
-    return (size_t)kLexLX * 4 * nt * sizeof(float4) + (size_t)(nt / 64) * kLexRing * sizeof(float);
+size_t lex_dma_lds_bytes(int nt, int lx) {
+    return (size_t)lx * 4 * nt * sizeof(float4) + (size_t)(nt / 64) * kLexRing * sizeof(float);
 }
 
 // u[1:-1,1:-1] -= grad_x[1:-1,1:-1] (no dt: v5.py:255-256)
@@ -692,15 +712,15 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
                     return b >= 64 && b <= 512 ? b / 64 * 64 : 512;
                 }();
                 const int nt = ny - 2 >= band ? band : 64 * ceil_div(ny - 2, 64);
-                const size_t lds = lex_dma_lds_bytes(nt);
+                const size_t lds = lex_dma_lds_bytes(nt, kLexLX);
                 static bool attr = false;
                 if (!attr) {
-                    CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lex_gs_sweep_dma),
+                    CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lex_gs_sweep_dma<kLexLX>),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)lex_dma_lds_bytes(512)));
+                                                      (int)lex_dma_lds_bytes(512, kLexLX)));
                     attr = true;
                 }
-                hipLaunchKernelGGL(k_lex_gs_sweep_dma, dim3(1), dim3(nt), lds, s, phi, div, ny, nx,
+                hipLaunchKernelGGL(k_lex_gs_sweep_dma<kLexLX>, dim3(1), dim3(nt), lds, s, phi, div, ny, nx,
                                    (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
             } else {
                 hipLaunchKernelGGL(k_lex_gs_sweep, dim3(1), dim3(ny - 2 >= 1024 ? 1024 : 64 * ceil_div(ny - 2, 64)), 0, s, phi, div, ny, nx,
