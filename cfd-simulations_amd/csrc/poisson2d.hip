@@ -414,22 +414,22 @@ static int jacobi2d_tbk_pass(int K, const T *in, T *out, const T *div, const uin
 // chain of row-step latencies on a grid too small to hide them.  x-segments
 // overlap by HL = ceil(K/VEC) halo lanes (erosion), as in jacobi2d_tbk; same
 // operation order, fixed rows / columns and mask rule, bit-identical.
-template <typename T, int VEC, int K, bool PRE, bool MASK>
+template <typename T, int VEC, int K, bool PRE, bool MASK, int RW = 2>
 __global__ __launch_bounds__(256) void jacobi2d_small(const T *__restrict__ in, T *__restrict__ out,
                                                       const T *__restrict__ div,
                                                       const uint8_t *__restrict__ mask, int ny, int nx,
                                                       int nseg, T dx2, T dtv) {
     constexpr int HL = (K + VEC - 1) / VEC;
     constexpr int SOUT = (64 - 2 * HL) * VEC;
-    constexpr int NR0 = 2 + 2 * K;
-    constexpr int ND = 2 * K;  // rows y0-(K-1) .. y0+K
+    constexpr int NR0 = RW + 2 * K;
+    constexpr int ND = RW + 2 * K - 2;  // rows y0-(K-1) .. y0+RW-1+K-1
     const int lane = threadIdx.x & 63;
     const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
     const long wave = (long)bid * 4 + threadIdx.x / 64;
     const int seg = (int)(wave % nseg);
-    const int y0 = 1 + 2 * (int)(wave / nseg);
+    const int y0 = 1 + RW * (int)(wave / nseg);
     if (y0 >= ny - 1) return;  // wave-uniform
-    const int y1 = min(y0 + 2, ny - 1);
+    const int y1 = min(y0 + RW, ny - 1);
     const int x0 = seg * SOUT - HL * VEC + lane * VEC;
     const bool valid = x0 >= 0 && x0 < nx;
     const bool writer = lane >= HL && lane < 64 - HL && valid;
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256) void jacobi2d_small(const T *__restrict__ in, 
     }
     if (writer) {
 #pragma unroll
-        for (int i = K; i < K + 2; ++i) {
+        for (int i = K; i < K + RW; ++i) {
             const int p = y0 - K + i;
             if (p < y1) st<T, VEC>(out + row(p), A[i]);
         }
@@ -495,23 +495,28 @@ __global__ __launch_bounds__(256) void jacobi2d_small(const T *__restrict__ in, 
 
 template <typename T, int VEC>
 static int jacobi2d_small_pass(int K, const T *in, T *out, const T *div, const uint8_t *mask, int ny,
-                               int nx, T dx2, T dtv, bool pre, hipStream_t s) {
+                               int nx, T dx2, T dtv, bool pre, int rw, hipStream_t s) {
     if (ny - 2 <= 0) return CFD_OK;
-#define CFD_J2S(KV, PR, M)                                                                           \
+#define CFD_J2S(KV, PR, M, RWV)                                                                      \
     do {                                                                                             \
         constexpr int HL_ = (KV + VEC - 1) / VEC;                                                    \
         const int nseg = ceil_div(nx, (64 - 2 * HL_) * VEC);                                         \
-        const int blocks = ceil_div((long)nseg * ceil_div(ny - 2, 2), 4);                            \
-        hipLaunchKernelGGL((jacobi2d_small<T, VEC, KV, PR, M>), dim3(blocks), dim3(256), 0, s, in, out, \
-                           div, mask, ny, nx, nseg, dx2, dtv);                                       \
+        const int blocks = ceil_div((long)nseg * ceil_div(ny - 2, RWV), 4);                          \
+        hipLaunchKernelGGL((jacobi2d_small<T, VEC, KV, PR, M, RWV>), dim3(blocks), dim3(256), 0, s, in, \
+                           out, div, mask, ny, nx, nseg, dx2, dtv);                                  \
     } while (0)
-#define CFD_J2SK(KV)                                                              \
-    do {                                                                          \
-        if (mask) {                                                               \
-            if (pre) CFD_J2S(KV, true, true); else CFD_J2S(KV, false, true);      \
-        } else {                                                                  \
-            if (pre) CFD_J2S(KV, true, false); else CFD_J2S(KV, false, false);    \
-        }                                                                         \
+#define CFD_J2SR(KV, RWV)                                                              \
+    do {                                                                               \
+        if (mask) {                                                                    \
+            if (pre) CFD_J2S(KV, true, true, RWV); else CFD_J2S(KV, false, true, RWV); \
+        } else {                                                                       \
+            if (pre) CFD_J2S(KV, true, false, RWV); else CFD_J2S(KV, false, false, RWV); \
+        }                                                                              \
+    } while (0)
+#define CFD_J2SK(KV)                       \
+    do {                                   \
+        if (rw == 2) CFD_J2SR(KV, 2);      \
+        else CFD_J2SR(KV, 1);              \
     } while (0)
     switch (K) {
         case 1: CFD_J2SK(1); break;
@@ -524,6 +529,7 @@ static int jacobi2d_small_pass(int K, const T *in, T *out, const T *div, const u
         default: CFD_J2SK(8); break;
     }
 #undef CFD_J2SK
+#undef CFD_J2SR
 #undef CFD_J2S
     CFD_LAUNCH_CHECK();
     return CFD_OK;
@@ -587,12 +593,16 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
         // small grids (auto depth 2) take the preloaded kernel, 4 sweeps a pass
         const bool small = g_j2_blocking == 0 && auto_levels2d<T>(ny, nx) != kDefaultLevels2d;
         static const int ks = [] { const char *e = getenv("CFD_J2_SMALL_K"); return e ? atoi(e) : 4; }();
+        // the preloaded kernel's shape: output rows per wave (1 or 2), cells per lane (1 or 16 B)
+        static const int srw = [] { const char *e = getenv("CFD_J2_SMALL_RW"); return e ? atoi(e) : 1; }();
+        static const int svec = [] { const char *e = getenv("CFD_J2_SMALL_VEC"); return e ? atoi(e) : 1; }();
         const int K = small ? ks : g_j2_blocking >= 2 ? g_j2_blocking : auto_levels2d<T>(ny, nx);
         int done = 0;
         while (done < iters) {
             int k = iters - done < K ? iters - done : K;
             if (!small && (k == 7 || k == 9 || k == 11)) --k;  // tbk depths: 2..6, 8, 10, 12
-            rc = small    ? jacobi2d_small_pass<T, V>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, s)
+            rc = small    ? (svec == 1 ? jacobi2d_small_pass<T, 1>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, srw, s)
+                                       : jacobi2d_small_pass<T, V>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, srw, s))
                  : k == 1 ? jacobi2d_sweep<T, V>(a, b, src, mask, ny, nx, dx2, dtv, pre, nullptr, s)
                           : jacobi2d_tbk_pass<T, V>(k, a, b, src, mask, ny, nx, dx2, dtv, pre, s);
             if (rc) return rc;
@@ -849,19 +859,19 @@ __global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
 // pass overwrote), as the 3-D pair passes do.  Same cells, operation order
 // and max|change| accounting as rbgs2d_tb (own rows; halo rows repeat a
 // neighbour chunk's values).
-template <bool MASK, int NI>
-__global__ __launch_bounds__(256) void rbgs2d_small(const float *__restrict__ in,
+template <bool MASK, int NI, int VEC = 4, int RW = 2, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict__ in,
                                                     float *__restrict__ out,
                                                     const float *__restrict__ div,
                                                     const uint8_t *__restrict__ mask, int ny, int nx,
                                                     int nseg, float cx, float cy, float cd,
                                                     float dt_inv, float tol, RbgsWs *ws, int it,
                                                     int rollback, int npairs) {
-    constexpr int VEC = 4;
-    constexpr int SOUT = 64 * VEC - 2 * VEC;
-    constexpr int L = 2 * NI;            // colour levels
-    constexpr int NR0 = 2 + 2 * L;       // level-0 rows y0-L .. y0+1+L
-    constexpr int ND = 2 + 2 * (L - 1);  // div / mask rows y0-(L-1) .. y0+L
+    constexpr int L = 2 * NI;                    // colour levels
+    constexpr int HL = (L + VEC - 1) / VEC;      // halo lanes per side (erosion)
+    constexpr int SOUT = (64 - 2 * HL) * VEC;    // output cells per wave
+    constexpr int NR0 = RW + 2 * L;              // level-0 rows y0-L .. y0+RW-1+L
+    constexpr int ND = RW + 2 * (L - 1);         // div / mask rows y0-(L-1) .. y0+RW-1+L-1
     bool stopped = false;
     if (rollback) {
         const int c = ws->flags[1];
@@ -882,17 +892,17 @@ __global__ __launch_bounds__(256) void rbgs2d_small(const float *__restrict__ in
     }
     const int lane = threadIdx.x & 63;
     const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
-    const long wave = (long)bid * 4 + threadIdx.x / 64;
+    const long wave = (long)bid * WPB + threadIdx.x / 64;
     const int seg = (int)(wave % nseg);
-    const int y0 = 1 + 2 * (int)(wave / nseg);
+    const int y0 = 1 + RW * (int)(wave / nseg);
     float mx[NI];
 #pragma unroll
     for (int q = 0; q < NI; ++q) mx[q] = 0.f;
     if (y0 < ny - 1) {  // wave-uniform
-        const int y1 = min(y0 + 2, ny - 1);
-        const int x0 = seg * SOUT - VEC + lane * VEC;
+        const int y1 = min(y0 + RW, ny - 1);
+        const int x0 = seg * SOUT - HL * VEC + lane * VEC;
         const bool valid = x0 >= 0 && x0 < nx;
-        const bool writer = lane >= 1 && lane <= 62 && valid;
+        const bool writer = lane >= HL && lane < 64 - HL && valid;
         auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
         float A[NR0][VEC];  // level l lives in rows [l, NR0 - l) of A (row i = y0 - L + i)
         float D[ND][VEC];   // div row y0 - (L-1) + i
@@ -911,10 +921,13 @@ __global__ __launch_bounds__(256) void rbgs2d_small(const float *__restrict__ in
             const int y = y0 - (L - 1) + i;
             if (valid && y >= 0 && y <= ny - 1) {
                 ld<float, VEC>(div + row(y), D[i]);
-                if (MASK) {  // 4 mask bytes in one load (nx % 4 == 0, x0 % 4 == 0)
+                if (MASK && VEC == 4) {  // 4 mask bytes in one load (nx % 4 == 0, x0 % 4 == 0)
                     const uint32_t m4 = *reinterpret_cast<const uint32_t *>(mask + row(y));
 #pragma unroll
                     for (int k = 0; k < VEC; ++k) Mk[i][k] = (uint8_t)(m4 >> (8 * k));
+                } else if (MASK) {
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) Mk[i][k] = mask[row(y) + k];
                 }
             }
         }
@@ -953,7 +966,7 @@ __global__ __launch_bounds__(256) void rbgs2d_small(const float *__restrict__ in
             }
             if (writer) {
 #pragma unroll
-                for (int i = L; i < L + 2; ++i) {
+                for (int i = L; i < L + RW; ++i) {
                     const int p = y0 - L + i;
                     if (p < y1) st<float, VEC>(out + row(p), A[i]);
                 }
@@ -963,7 +976,7 @@ __global__ __launch_bounds__(256) void rbgs2d_small(const float *__restrict__ in
     if (rollback) return;
     // one atomic per workgroup and iteration, no read-first guard (a
     // dependent load at the end of a few-microsecond kernel)
-    __shared__ float red[NI][4];
+    __shared__ float red[NI][WPB];
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
         const float m = wave_max(mx[q]);
@@ -972,7 +985,9 @@ __global__ __launch_bounds__(256) void rbgs2d_small(const float *__restrict__ in
     __syncthreads();
     if (threadIdx.x < NI && !stopped) {
         const int q = threadIdx.x;
-        const float b = fmaxf(fmaxf(red[q][0], red[q][1]), fmaxf(red[q][2], red[q][3]));
+        float b = red[q][0];
+#pragma unroll
+        for (int w = 1; w < WPB; ++w) b = fmaxf(b, red[q][w]);
         if (b > 0.0f) atomic_max_nonneg(&ws->maxc[it + q], b);
     }
 }
@@ -983,18 +998,39 @@ static void rbgs2d_small_launch(int NI, const float *in, float *out, const float
                                 const uint8_t *mask, int ny, int nx, float cx, float cy, float cd,
                                 float dt_inv, float tol, RbgsWs *ws, int it, int rollback, int npairs,
                                 hipStream_t s) {
-    constexpr int SOUT = 64 * 4 - 2 * 4;
-    const int nseg = ceil_div(nx, SOUT);
-    const int blocks = ceil_div((long)nseg * ceil_div(ny - 2, 2), 4);
-#define CFD_GSS(M, N)                                                                                \
-    hipLaunchKernelGGL((rbgs2d_small<M, N>), dim3(blocks), dim3(256), 0, s, in, out, div, mask, ny, nx, \
-                       nseg, cx, cy, cd, dt_inv, tol, ws, it, rollback, npairs)
+    // shape: output rows per wave (1 or 2) and cells per lane (1 or 4)
+    static const int rw = [] { const char *e = getenv("CFD_GS_SMALL_RW"); return e && atoi(e) == 1 ? 1 : 2; }();
+    static const int vec = [] { const char *e = getenv("CFD_GS_SMALL_VEC"); return e && atoi(e) == 1 ? 1 : 4; }();
+    static const int wpb = [] { const char *e = getenv("CFD_GS_SMALL_WPB"); return e && atoi(e) == 16 ? 16 : 4; }();
+#define CFD_GSS_W(M, N, V, R, W)                                                                     \
+    do {                                                                                             \
+        constexpr int HL_ = (2 * N + V - 1) / V;                                                     \
+        const int nseg = ceil_div(nx, (64 - 2 * HL_) * V);                                           \
+        const int blocks = ceil_div((long)nseg * ceil_div(ny - 2, R), W);                            \
+        hipLaunchKernelGGL((rbgs2d_small<M, N, V, R, W>), dim3(blocks), dim3(64 * W), 0, s, in, out, \
+                           div, mask, ny, nx, nseg, cx, cy, cd, dt_inv, tol, ws, it, rollback, npairs); \
+    } while (0)
+#define CFD_GSS(M, N, V, R)                              \
+    do {                                                 \
+        if (wpb == 16) CFD_GSS_W(M, N, V, R, 16);        \
+        else CFD_GSS_W(M, N, V, R, 4);                   \
+    } while (0)
+#define CFD_GSS_VR(M, N)                                       \
+    do {                                                       \
+        if (vec == 1) {                                        \
+            if (rw == 1) CFD_GSS(M, N, 1, 1); else CFD_GSS(M, N, 1, 2); \
+        } else {                                               \
+            if (rw == 1) CFD_GSS(M, N, 4, 1); else CFD_GSS(M, N, 4, 2); \
+        }                                                      \
+    } while (0)
     if (mask) {
-        if (NI == 2) CFD_GSS(true, 2); else CFD_GSS(true, 1);
+        if (NI == 2) CFD_GSS_VR(true, 2); else CFD_GSS_VR(true, 1);
     } else {
-        if (NI == 2) CFD_GSS(false, 2); else CFD_GSS(false, 1);
+        if (NI == 2) CFD_GSS_VR(false, 2); else CFD_GSS_VR(false, 1);
     }
+#undef CFD_GSS_VR
 #undef CFD_GSS
+#undef CFD_GSS_W
 }
 
 // rbgs2d_small serves grids whose row march would use chunks of <= 2 rows
