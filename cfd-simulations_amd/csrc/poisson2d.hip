@@ -948,15 +948,17 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
 #pragma unroll
                     for (int k = 0; k < VEC; ++k) {
                         const int x = x0 + k;
-                        B[i][k] = ac[k];
-                        if (!edge && x >= 1 && x < nx - 1 && ((r + x + 1 + par) & 1) == 0 &&
-                            !(MASK && Mk[di][k])) {
-                            const float E = (k + 1 < VEC) ? ac[k + 1] : er;
-                            const float W = (k > 0) ? ac[k - 1] : wl;
-                            B[i][k] = gs5(E, W, A[i + 1][k], A[i - 1][k], D[di][k], cx, cy, cd, dt_inv);
-                            const float ch = fabsf(B[i][k] - ac[k]);
-                            if (writer && r >= y0 && r < y1 && ch > mx[(l - 1) / 2]) mx[(l - 1) / 2] = ch;
-                        }
+                        // branch-free: every lane computes, selects keep the old value
+                        // (same bits as the conditional update; fmaxf ignores a NaN
+                        // change like the `ch > mx` test did)
+                        const bool upd = !edge && x >= 1 && x < nx - 1 && ((r + x + 1 + par) & 1) == 0 &&
+                                         !(MASK && Mk[di][k]);
+                        const float E = (k + 1 < VEC) ? ac[k + 1] : er;
+                        const float W = (k > 0) ? ac[k - 1] : wl;
+                        const float nv = gs5(E, W, A[i + 1][k], A[i - 1][k], D[di][k], cx, cy, cd, dt_inv);
+                        B[i][k] = upd ? nv : ac[k];
+                        const float ch = upd ? fabsf(nv - ac[k]) : 0.f;
+                        if (writer && r >= y0 && r < y1) mx[(l - 1) / 2] = fmaxf(mx[(l - 1) / 2], ch);
                     }
                 }
 #pragma unroll
