@@ -888,6 +888,9 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
         const float p1 = it > 0 ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 1]) : 0.f;
         const float p2 = (NI == 2 && it > 1) ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 2]) : 0.f;
         stopped = (it > 0 && p1 < tol) || (NI == 2 && it > 1 && p2 < tol);
+        // grid-uniform (every lane read the same words): a scalar branch, so the
+        // level arrays below need no exec-masked copies (584 v_mov without it)
+        stopped = __builtin_amdgcn_readfirstlane((int)stopped) != 0;
         if (stopped && blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&ws->flags[1], it);
     }
     const int lane = threadIdx.x & 63;
@@ -907,28 +910,54 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
         float A[NR0][VEC];  // level l lives in rows [l, NR0 - l) of A (row i = y0 - L + i)
         float D[ND][VEC];   // div row y0 - (L-1) + i
         uint8_t Mk[ND][VEC];
+        // unconditional loads from clamped rows, then selects: a load under a
+        // branch makes the compiler copy the whole row array at every merge
+        // (584 v_mov at one cell per lane)
 #pragma unroll
         for (int i = 0; i < NR0; ++i) {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) A[i][k] = 0.f;
             const int y = y0 - L + i;
-            if (valid && y >= 0 && y <= ny - 1) ld<float, VEC>(in + row(y), A[i]);
+            const bool in_ = valid && y >= 0 && y <= ny - 1;
+            ld<float, VEC>(in + row(min(max(y, 0), ny - 1)), A[i]);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) A[i][k] = in_ ? A[i][k] : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < ND; ++i) {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) { D[i][k] = 0.f; Mk[i][k] = 0; }
             const int y = y0 - (L - 1) + i;
-            if (valid && y >= 0 && y <= ny - 1) {
-                ld<float, VEC>(div + row(y), D[i]);
-                if (MASK && VEC == 4) {  // 4 mask bytes in one load (nx % 4 == 0, x0 % 4 == 0)
-                    const uint32_t m4 = *reinterpret_cast<const uint32_t *>(mask + row(y));
+            const bool in_ = valid && y >= 0 && y <= ny - 1;
+            const size_t rc = row(min(max(y, 0), ny - 1));
+            ld<float, VEC>(div + rc, D[i]);
+            uint32_t m4 = 0;
+            if (MASK && VEC == 4) {  // 4 mask bytes in one load (nx % 4 == 0, x0 % 4 == 0)
+                m4 = *reinterpret_cast<const uint32_t *>(mask + rc);
+            } else if (MASK) {
 #pragma unroll
-                    for (int k = 0; k < VEC; ++k) Mk[i][k] = (uint8_t)(m4 >> (8 * k));
-                } else if (MASK) {
+                for (int k = 0; k < VEC; ++k) m4 |= (uint32_t)mask[rc + k] << (8 * k);
+            }
 #pragma unroll
-                    for (int k = 0; k < VEC; ++k) Mk[i][k] = mask[row(y) + k];
-                }
+            for (int k = 0; k < VEC; ++k) {
+                D[i][k] = in_ ? D[i][k] : 0.f;
+                Mk[i][k] = in_ ? (uint8_t)(m4 >> (8 * k)) : 0;
+            }
+        }
+        // level-invariant per cell, computed once: the rhs (-div * dt_inv, the
+        // same product gs5 forms) and which colour updates the cell (none for
+        // edges, masked cells and x outside [1, nx-2]); colour c updates cells
+        // with (r + x + 1 + c) even
+        float RH[ND][VEC];
+        bool U0[ND][VEC], U1[ND][VEC];  // updated by colour 0 / colour 1
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+            const int r = y0 - (L - 1) + i;
+            const bool edge = r <= 0 || r >= ny - 1;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const int x = x0 + k;
+                RH[i][k] = -D[i][k] * dt_inv;
+                const bool ok = !edge && x >= 1 && x < nx - 1 && !(MASK && Mk[i][k]);
+                const bool even = ((r + x + 1) & 1) == 0;
+                U0[i][k] = ok && even;
+                U1[i][k] = ok && !even;
             }
         }
         if (!stopped) {
@@ -940,22 +969,19 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
 #pragma unroll
                 for (int i = l; i < NR0 - l; ++i) {
                     const int r = y0 - L + i;
-                    const bool edge = r <= 0 || r >= ny - 1;
                     const float *ac = A[i];
                     const float wl = dpp_from_lower(ac[VEC - 1]);
                     const float er = dpp_from_upper(ac[0]);
                     const int di = i - 1;  // div / mask row index of row r
 #pragma unroll
                     for (int k = 0; k < VEC; ++k) {
-                        const int x = x0 + k;
                         // branch-free: every lane computes, selects keep the old value
                         // (same bits as the conditional update; fmaxf ignores a NaN
                         // change like the `ch > mx` test did)
-                        const bool upd = !edge && x >= 1 && x < nx - 1 && ((r + x + 1 + par) & 1) == 0 &&
-                                         !(MASK && Mk[di][k]);
+                        const bool upd = par ? U1[di][k] : U0[di][k];
                         const float E = (k + 1 < VEC) ? ac[k + 1] : er;
                         const float W = (k > 0) ? ac[k - 1] : wl;
-                        const float nv = gs5(E, W, A[i + 1][k], A[i - 1][k], D[di][k], cx, cy, cd, dt_inv);
+                        const float nv = ((cx * (E + W) + cy * (A[i + 1][k] + A[i - 1][k])) - RH[di][k]) * cd;
                         B[i][k] = upd ? nv : ac[k];
                         const float ch = upd ? fabsf(nv - ac[k]) : 0.f;
                         if (writer && r >= y0 && r < y1) mx[(l - 1) / 2] = fmaxf(mx[(l - 1) / 2], ch);
