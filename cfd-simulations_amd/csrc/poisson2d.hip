@@ -859,6 +859,19 @@ __global__ __launch_bounds__(256) void rbgs2d_tb(const float *__restrict__ in,
 // pass overwrote), as the 3-D pair passes do.  Same cells, operation order
 // and max|change| accounting as rbgs2d_tb (own rows; halo rows repeat a
 // neighbour chunk's values).
+constexpr int kGsSlots = 16;  // per-iteration maxima slots of rbgs2d_small
+
+// maxc[k] = max over the slots of iteration k (before rbgs_count)
+__global__ void rbgs_fold_slots(RbgsWs *ws, int niters) {
+    const float *slots = ws->maxc + niters;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < niters; k += gridDim.x * blockDim.x) {
+        float m = 0.f;
+#pragma unroll
+        for (int q = 0; q < kGsSlots; ++q) m = fmaxf(m, slots[(size_t)q * niters + k]);
+        ws->maxc[k] = m;
+    }
+}
+
 template <bool MASK, int NI, int VEC = 4, int RW = 2, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict__ in,
                                                     float *__restrict__ out,
@@ -866,7 +879,12 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
                                                     const uint8_t *__restrict__ mask, int ny, int nx,
                                                     int nseg, float cx, float cy, float cd,
                                                     float dt_inv, float tol, RbgsWs *ws, int it,
-                                                    int rollback, int npairs) {
+                                                    int rollback, int npairs, int niters) {
+    // per-iteration maxima go to kGsSlots slot rows (slot-major, after
+    // maxc[niters]) instead of one word: the workgroups' device-scope atomics
+    // spread over kGsSlots addresses in different lines (same-address ones
+    // serialise, ~10 ns each); rbgs_fold_slots folds them into maxc
+    float *slots = ws->maxc + niters;
     constexpr int L = 2 * NI;                    // colour levels
     constexpr int HL = (L + VEC - 1) / VEC;      // halo lanes per side (erosion)
     constexpr int SOUT = (64 - 2 * HL) * VEC;    // output cells per wave
@@ -885,8 +903,12 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
         // the stop test's loads are issued here but acted on after the row
         // loads, so the latencies overlap; a pair skips when either iteration
         // of the previous pair met the tolerance
-        const float p1 = it > 0 ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 1]) : 0.f;
-        const float p2 = (NI == 2 && it > 1) ? *reinterpret_cast<volatile float *>(&ws->maxc[it - 2]) : 0.f;
+        // lane l < kGsSlots reads slot l of iteration it-1, lane kGsSlots+l of it-2
+        const int ln = threadIdx.x & 63, sl = ln % kGsSlots, back = 1 + ln / kGsSlots;
+        const bool rd = ln < 2 * kGsSlots && it - back >= 0;
+        const float pv = rd ? *reinterpret_cast<volatile float *>(&slots[(size_t)sl * niters + it - back]) : 0.f;
+        const float p1 = wave_max(ln < kGsSlots ? pv : 0.f);
+        const float p2 = wave_max(ln < kGsSlots ? 0.f : pv);
         stopped = (it > 0 && p1 < tol) || (NI == 2 && it > 1 && p2 < tol);
         // grid-uniform (every lane read the same words): a scalar branch, so the
         // level arrays below need no exec-masked copies (584 v_mov without it)
@@ -1016,7 +1038,7 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
         float b = red[q][0];
 #pragma unroll
         for (int w = 1; w < WPB; ++w) b = fmaxf(b, red[q][w]);
-        if (b > 0.0f) atomic_max_nonneg(&ws->maxc[it + q], b);
+        if (b > 0.0f) atomic_max_nonneg(&slots[(size_t)(blockIdx.x % kGsSlots) * niters + it + q], b);
     }
 }
 
@@ -1025,10 +1047,11 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
 static void rbgs2d_small_launch(int NI, const float *in, float *out, const float *div,
                                 const uint8_t *mask, int ny, int nx, float cx, float cy, float cd,
                                 float dt_inv, float tol, RbgsWs *ws, int it, int rollback, int npairs,
-                                hipStream_t s) {
-    // shape: output rows per wave (1 or 2) and cells per lane (1 or 4)
+                                int niters, hipStream_t s) {
+    // shape: output rows per wave (1 or 2) and cells per lane (1 or 4); r01 at
+    // 600 x 180, us per iteration: (1, 2) 2.36, (1, 1) 2.42, (4, 2) 3.38
     static const int rw = [] { const char *e = getenv("CFD_GS_SMALL_RW"); return e && atoi(e) == 1 ? 1 : 2; }();
-    static const int vec = [] { const char *e = getenv("CFD_GS_SMALL_VEC"); return e && atoi(e) == 1 ? 1 : 4; }();
+    static const int vec = [] { const char *e = getenv("CFD_GS_SMALL_VEC"); return e && atoi(e) == 4 ? 4 : 1; }();
     static const int wpb = [] { const char *e = getenv("CFD_GS_SMALL_WPB"); return e && atoi(e) == 16 ? 16 : 4; }();
 #define CFD_GSS_W(M, N, V, R, W)                                                                     \
     do {                                                                                             \
@@ -1036,7 +1059,8 @@ static void rbgs2d_small_launch(int NI, const float *in, float *out, const float
         const int nseg = ceil_div(nx, (64 - 2 * HL_) * V);                                           \
         const int blocks = ceil_div((long)nseg * ceil_div(ny - 2, R), W);                            \
         hipLaunchKernelGGL((rbgs2d_small<M, N, V, R, W>), dim3(blocks), dim3(64 * W), 0, s, in, out, \
-                           div, mask, ny, nx, nseg, cx, cy, cd, dt_inv, tol, ws, it, rollback, npairs); \
+                           div, mask, ny, nx, nseg, cx, cy, cd, dt_inv, tol, ws, it, rollback, npairs, \
+                           niters);                                                          \
     } while (0)
 #define CFD_GSS(M, N, V, R)                              \
     do {                                                 \
@@ -1073,15 +1097,8 @@ static int rbgs2d_tb_pass(const float *in, float *out, const float *div, const u
     constexpr int SOUT = 64 * 4 - 2 * 4;
     const int nseg = ceil_div(nx, SOUT);
     const int rows = ny - 2;
-    // short chunks on small grids: the 600 x 180 cylinder has 3 segments, and
-    // 2-row chunks give 267 waves (8-row chunks: 69 waves, 11.3 us per
-    // iteration, latency-bound); the re-marched row per chunk is cheap there
+    // (grids with chunks of <= 2 rows take rbgs2d_small in the solve instead)
     int rpc = ceil_div((long)rows * nseg, 8192);
-    if (rpc <= 2) {  // small grid: one iteration of the preloaded kernel
-        rbgs2d_small_launch(1, in, out, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, ws, it, 0, 0, s);
-        CFD_LAUNCH_CHECK();
-        return CFD_OK;
-    }
     if (rpc > 64) rpc = 64;
     const int nchunk = ceil_div(rows, rpc);
     const int wpb = 4;
@@ -1192,7 +1209,8 @@ int cfd_set_jacobi2d_blocking(int steps) {
 }
 
 size_t cfd_rbgs_workspace_bytes(int iterations) {
-    return 16 + sizeof(float) * (size_t)(iterations > 0 ? iterations : 1);
+    // flags, maxc[iterations], then the small-grid kernel's kGsSlots slot rows
+    return 16 + sizeof(float) * (size_t)(1 + kGsSlots) * (size_t)(iterations > 0 ? iterations : 1);
 }
 
 int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
@@ -1221,18 +1239,21 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
             // small grid (the v5 cylinder): two iterations per launch, a single
             // one for an odd remainder, the rollback of a stop inside a pair
             const int npairs = iterations / 2;
+            CFD_CHECK_HIP(hipMemsetAsync(w->maxc + iterations, 0, sizeof(float) * kGsSlots * (size_t)iterations, s));
             for (int it = 0; it < iterations;) {
                 const int m = iterations - it >= 2 ? 2 : 1;
-                rbgs2d_small_launch(m, a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, 0, 0, s);
+                rbgs2d_small_launch(m, a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, 0, 0, iterations, s);
                 CFD_LAUNCH_CHECK();
                 it += m;
                 float *t = a; a = b; b = t;
             }
             timing_end(tk, s, iterations);
+            hipLaunchKernelGGL(rbgs_fold_slots, dim3(ceil_div(iterations, 256)), dim3(256), 0, s, w, iterations);
+            CFD_LAUNCH_CHECK();
             if ((rc = launch_rbgs_count(w, iters_done, s))) return rc;
             if (npairs > 0) {
                 rbgs2d_small_launch(1, phi, phi_tmp, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, 0, 1,
-                                    npairs, s);
+                                    npairs, iterations, s);
                 CFD_LAUNCH_CHECK();
             }
             return launch_rbgs_copy(w, phi, phi_tmp, (size_t)ny * nx, 2, s);
