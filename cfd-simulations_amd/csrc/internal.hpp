@@ -44,7 +44,8 @@ int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int n
                     int lag = 0);
 // red-black GS workspace (cfd_rbgs_workspace_bytes): flags[0] = iterations,
 // flags[1] = iterations done, flags[2] = tolerance (float bits), float
-// maxc[iterations] at byte 16
+// maxc[iterations] at byte 16, then the small-grid 2-D kernel's 16 slot rows
+// of per-iteration maxima (slot-major, folded into maxc after its loop)
 struct RbgsWs {
     int flags[4];
     float maxc[1];
