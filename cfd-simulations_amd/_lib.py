@@ -49,6 +49,7 @@ PROTOTYPES = {
     "cfd_clean_divergence_workspace_bytes": (c_size_t, [c_int, c_int]),
     "cfd_clean_divergence2d_f32": (c_int, [P, P, c_int, c_int, c_double, c_double, c_int, P, P]),
     "cfd_apply_bc2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_int, P]),
+    "cfd_apply_lid_bc2d_f32": (c_int, [P, P, c_int, c_int, c_float, P]),
     "cfd_apply_ibm2d_f32": (c_int, [P, P, P, c_int, c_double, P]),
     "cfd_clip_f32": (c_int, [P, c_size_t, c_float, c_float, P]),
     "cfd_absmax_f32": (c_int, [P, c_size_t, P, P]),
@@ -57,6 +58,7 @@ PROTOTYPES = {
     "cfd_vorticity_absmax2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, P, P]),
     "cfd_vorticity2d_f32": (c_int, [P, P, P, P, c_int, c_int, c_double, c_double, P]),
     "cfd_nonfinite_count_f32": (c_int, [P, P, c_size_t, P, P]),
+    "cfd_numpy_powf_f32": (c_int, [P, c_float, P, c_size_t, P]),
     "cfd_comm_unique_id": (c_int, [P, c_size_t]),
     "cfd_comm_init": (c_int, [P, c_int, c_int, ctypes.POINTER(c_void_p)]),
     "cfd_comm_destroy": (c_int, [P]),
@@ -79,6 +81,9 @@ PROTOTYPES = {
     "cfd_get_jacobi2d_levels": (c_int, []),
     "cfd_set_jacobi3d_prefetch": (c_int, [c_int]),
     "cfd_set_jacobi2d_blocking": (c_int, [c_int]),
+    "cfd_reset_tuning": (c_int, []),
+    "cfd_get_last_tbr_shape": (c_int, [ctypes.POINTER(c_int)] * 4),
+    "cfd_set_small2d_shape": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "cfd_timing_enable": (c_int, [c_int]),
     "cfd_timing_read": (c_int, [ctypes.POINTER(c_double), ctypes.POINTER(ctypes.c_longlong), c_int]),
 }

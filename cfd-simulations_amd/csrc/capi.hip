@@ -2,7 +2,7 @@
 #include <cstring>
 #include <vector>
 
-#include "common.hpp"
+#include "internal.hpp"
 
 namespace cfd {
 static thread_local char g_err[512] = "";
@@ -22,7 +22,32 @@ struct Timing {
     std::vector<long long> sweeps;
     size_t used = 0;
 };
-static Timing g_timing;
+static thread_local Timing g_timing;  // per host thread, like the tuning knobs
+
+// Process defaults of the tuning knobs: the CFD_* environment variables (A/B
+// knobs of the bench scripts), validated, read once.
+static int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+static Tuning process_defaults() {
+    static const Tuning d = [] {
+        Tuning t;
+        const int k = env_int("CFD_J2_SMALL_K", 4);
+        t.j2s_k = k >= 1 && k <= 8 ? k : 4;
+        t.j2s_rw = env_int("CFD_J2_SMALL_RW", 1) == 2 ? 2 : 1;
+        t.j2s_vec = env_int("CFD_J2_SMALL_VEC", 1) == 1 ? 1 : 0;  // 0: 16 bytes per lane
+        t.gs_rw = env_int("CFD_GS_SMALL_RW", 2) == 1 ? 1 : 2;
+        t.gs_vec = env_int("CFD_GS_SMALL_VEC", 1) == 4 ? 4 : 1;
+        t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;
+        return t;
+    }();
+    return d;
+}
+Tuning &tuning() {
+    static thread_local Tuning t = process_defaults();
+    return t;
+}
 
 int timing_begin(hipStream_t s) {
     if (!g_timing.on) return -1;
@@ -51,6 +76,30 @@ extern "C" {
 int cfd_abi_version(void) { return CFD_ABI_VERSION; }
 const char *cfd_last_error(void) { return cfd::g_err; }
 const char *cfd_device_arch(void) { return "gfx950"; }
+
+int cfd_reset_tuning(void) {
+    tuning() = process_defaults();
+    return CFD_OK;
+}
+
+int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec, int gs_wpb) {
+    CFD_REQUIRE(j2_k >= 0 && j2_k <= 8, "small-grid Jacobi sweeps per launch must be 0 (default) or 1..8");
+    CFD_REQUIRE(j2_rw >= 0 && j2_rw <= 2, "small-grid Jacobi rows per wave must be 0 (default), 1 or 2");
+    CFD_REQUIRE(j2_vec == 0 || j2_vec == 1 || j2_vec == 4,
+                "small-grid Jacobi cells per lane must be 0 (default), 1 or 4 (16 bytes)");
+    CFD_REQUIRE(gs_rw >= 0 && gs_rw <= 2, "small-grid GS rows per wave must be 0 (default), 1 or 2");
+    CFD_REQUIRE(gs_vec == 0 || gs_vec == 1 || gs_vec == 4, "small-grid GS cells per lane must be 0, 1 or 4");
+    CFD_REQUIRE(gs_wpb == 0 || gs_wpb == 4 || gs_wpb == 16, "small-grid GS waves per workgroup must be 0, 4 or 16");
+    const Tuning d = process_defaults();
+    Tuning &t = tuning();
+    t.j2s_k = j2_k ? j2_k : d.j2s_k;
+    t.j2s_rw = j2_rw ? j2_rw : d.j2s_rw;
+    t.j2s_vec = j2_vec ? (j2_vec == 1 ? 1 : 0) : d.j2s_vec;
+    t.gs_rw = gs_rw ? gs_rw : d.gs_rw;
+    t.gs_vec = gs_vec ? gs_vec : d.gs_vec;
+    t.gs_wpb = gs_wpb ? gs_wpb : d.gs_wpb;
+    return CFD_OK;
+}
 
 int cfd_timing_enable(int enable) {
     g_timing.on = enable != 0;

@@ -5,14 +5,14 @@
 // Arithmetic follows the reference as it executes in NumPy-scalar form: every
 // Python-float constant is rounded to float32 where it meets float32 data
 // (NEP 50), operations run in float32 in the source order, nothing is fused
-// (-ffp-contract=off).  The only intended deviation: |V| = sqrtf(u^2+v^2)
-// (correctly rounded) where the stubbed reference evaluates float32 `** 0.5`
-// through powf; they differ by at most 1 ulp on ~0.07% of inputs, which the
-// tests bound with a relative tolerance.
+// (-ffp-contract=off).  |V| = (u**2 + v**2) ** 0.5 goes through the device
+// copy of glibc's powf (libm_powf.hpp), as NumPy's float32 scalar `**` does
+// in the reference, so the predictor is bit-exact too.
 //
 // These kernels are one-pass per cell and HBM-bound; the fused predictor
 // reads u, v once (5-point neighbourhoods from L1/L2) and writes u*, v*, tau.
 #include "common.hpp"
+#include "libm_powf.hpp"
 
 namespace cfd {
 
@@ -41,9 +41,10 @@ static PredConst make_pred_const(double dx, double dy) {
     return k;
 }
 
-// compute_supg_stabilization_fast body, v5.py:155-161
+// compute_supg_stabilization_fast body, v5.py:155-161: vel_mag =
+// (u**2 + v**2) ** 0.5 on float32 scalars, i.e. libm powf three times
 __device__ inline float supg_tau(float u, float v, float nu, float dt, const PredConst &k) {
-    const float vm = sqrtf(u * u + v * v);
+    const float vm = libm::powf(libm::powf(u, 2.0f) + libm::powf(v, 2.0f), 0.5f);
     if (vm > k.eps) {
         const float pe = (vm * k.h) / (nu + k.eps);
         const float half = pe / 2.0f;
@@ -481,6 +482,28 @@ __global__ void k_bc(float *__restrict__ u, float *__restrict__ v, const double 
     }
 }
 
+// Lid-driven cavity walls (BASELINE config 1; the reference has no
+// incompressible cavity, so the walls follow the assignment pattern of
+// v5.py:349-360): no-slip u = v = 0 on the left, right and bottom walls, the
+// lid u = u_lid, v = 0 on the top row y = y_max (row ny-1), the lid written
+// last so it owns the two top corners.
+__global__ void k_lid_bc(float *__restrict__ u, float *__restrict__ v, int ny, int nx, float u_lid) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ny - 1) {  // side walls, rows 0 .. ny-2
+        const size_t r = (size_t)t * nx;
+        u[r] = 0.0f;
+        v[r] = 0.0f;
+        u[r + nx - 1] = 0.0f;
+        v[r + nx - 1] = 0.0f;
+    }
+    if (t < nx) {
+        u[t] = 0.0f;  // bottom wall
+        v[t] = 0.0f;
+        u[(size_t)(ny - 1) * nx + t] = u_lid;  // lid
+        v[(size_t)(ny - 1) * nx + t] = 0.0f;
+    }
+}
+
 // apply_ibm_fast, v5.py:228-237 (float64 mask => float64 arithmetic)
 __global__ void k_ibm(float *__restrict__ u, float *__restrict__ v, const double *__restrict__ m,
                       int n, double fs) {
@@ -575,6 +598,14 @@ __global__ void k_nonfinite(const float *__restrict__ a, const float *__restrict
         if (b) cnt += !isfinite(b[c]);
     }
     if (cnt) atomicAdd(out, cnt);
+}
+
+// NumPy float32 scalar power (glibc powf, libm_powf.hpp) elementwise: the
+// parity hook for the device powf the SUPG tau uses.
+__global__ void k_numpy_powf(const float *__restrict__ x, float y, float *__restrict__ out, size_t n) {
+    for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < n;
+         c += (size_t)gridDim.x * blockDim.x)
+        out[c] = libm::powf(x[c], y);
 }
 
 static dim3 grid2d(int ny, int nx) { return dim3(ceil_div(nx, 256), ny); }
@@ -745,6 +776,15 @@ int cfd_apply_bc2d_f32(float *u, float *v, const double *y, int ny, int nx, doub
     return CFD_OK;
 }
 
+int cfd_apply_lid_bc2d_f32(float *u, float *v, int ny, int nx, float u_lid, void *stream) {
+    CFD_REQUIRE(u && v, "apply_lid_bc2d: null pointer");
+    CFD_REQUIRE(ny >= 2 && nx >= 2, "apply_lid_bc2d: grid must be at least 2x2");
+    const int n = ny > nx ? ny : nx;
+    hipLaunchKernelGGL(k_lid_bc, dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), u, v, ny, nx, u_lid);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
 int cfd_apply_ibm2d_f32(float *u, float *v, const double *ibm_mask, int n, double force_strength,
                         void *stream) {
     CFD_REQUIRE(u && v && ibm_mask && n >= 0, "apply_ibm2d: bad arguments");
@@ -806,6 +846,14 @@ int cfd_vorticity2d_f32(const float *u, const float *v, const uint8_t *mask, flo
     CFD_SHAPE2D(ny, nx);
     hipLaunchKernelGGL(k_vorticity, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v, mask, w,
                        ny, nx, (float)(2.0 * dx), (float)(2.0 * dy));
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_numpy_powf_f32(const float *x, float y, float *out, size_t n, void *stream) {
+    CFD_REQUIRE(x && out, "numpy_powf: null pointer");
+    if (n == 0) return CFD_OK;
+    hipLaunchKernelGGL(k_numpy_powf, dim3(grid1d(n)), dim3(256), 0, as_stream(stream), x, y, out, n);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }

@@ -3,6 +3,26 @@
 #include "common.hpp"
 
 namespace cfd {
+// Kernel tuning knobs, set through the cfd_set_* entry points.  They are per
+// host thread (thread_local): a thread's settings apply to the solves it
+// launches and never to another thread's, so concurrent callers (e.g. the
+// ranks of an in-process slab group) cannot change each other's kernels.
+// Every thread starts from the process defaults (the CFD_* environment knobs,
+// read once); cfd_reset_tuning() returns the calling thread to them.
+struct Tuning {
+    // 3-D single sweep: variant 0 auto / 1 LDS / 2 cache, rows, planes per tile
+    int j3_variant = 0, j3_waves = 0, j3_zchunk = 0;
+    // 3-D temporal blocking: sweeps per pass (0 auto, 1 off), rows, z-chunk, prefetch
+    int tb_steps = 0, tb_rows = 0, tb_zchunk = 0, tb_prefetch = 0;
+    // 2-D Jacobi sweeps per pass: 0 auto, 1 off, 2..6, 8, 10, 12
+    int j2_blocking = 0;
+    // small-grid 2-D Jacobi: sweeps per launch (1..8), rows per wave, cells per lane
+    int j2s_k = 4, j2s_rw = 1, j2s_vec = 1;
+    // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per workgroup
+    int gs_rw = 2, gs_vec = 1, gs_wpb = 4;
+};
+Tuning &tuning();
+
 // poisson3d.hip
 int launch_fix_faces3d(const float *src, float *dst, const uint8_t *mask, int ny, int nx, int za,
                        int zb, int full_lo, int full_hi, hipStream_t s);

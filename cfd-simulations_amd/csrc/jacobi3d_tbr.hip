@@ -610,6 +610,7 @@ int num_cus() {
     return n;
 }
 thread_local int g_cu_reserve = 0;
+thread_local int g_last_shape[4] = {0, 0, 0, 0};  // K, row waves, rows per wave, z-chunk
 }  // namespace
 
 int tbr_cus() { return num_cus() - g_cu_reserve; }
@@ -657,6 +658,10 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
     a.nseg = nseg;
     a.ntile_y = ceil_div(a.ny - 2, best->rows());
     a.zchunk = best_zlen;
+    g_last_shape[0] = best->K;
+    g_last_shape[1] = best->nwr;
+    g_last_shape[2] = best->rpw;
+    g_last_shape[3] = best_zlen;
     const int blocks = a.nseg * a.ntile_y * ceil_div(L, best_zlen);
 #define CFD_TBR_L(KV, NW, RP, PR, PDV) \
     hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, PR, PDV, MODE>), dim3(blocks), dim3((NW + 1) * 64), 0, s, a)
@@ -725,3 +730,12 @@ int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int n
 }
 
 }  // namespace cfd
+
+extern "C" int cfd_get_last_tbr_shape(int *levels, int *row_waves, int *rows_per_wave, int *zchunk) {
+    CFD_REQUIRE(levels && row_waves && rows_per_wave && zchunk, "get_last_tbr_shape: null pointer");
+    *levels = cfd::g_last_shape[0];
+    *row_waves = cfd::g_last_shape[1];
+    *rows_per_wave = cfd::g_last_shape[2];
+    *zchunk = cfd::g_last_shape[3];
+    return CFD_OK;
+}

@@ -1,0 +1,131 @@
+// libm_powf.hpp -- device restatement of glibc's powf (2.35, x86_64), the
+// function NumPy calls for a float32 scalar `**` (npy_powf -> powf).
+//
+// Why: compute_supg_stabilization_fast evaluates |V| as
+// `(u[i,j]**2 + v[i,j]**2) ** 0.5` on float32 scalars (v5.py:155).  glibc's
+// powf is not correctly rounded: powf(x, 2) differs from x*x on 1 548 806 of
+// the 2^32 float inputs (its result is a double approximation with relative
+// error ~1.27 * 2^-26, rounded to float), so a correctly rounded u*u cannot
+// reproduce the reference bit for bit.  This is the published algorithm of
+// glibc's sysdeps/ieee754/flt-32/e_powf.c (from ARM's optimized-routines):
+// x = 2^k z, log2(x) = k + log2(c) + log1p(z/c - 1)/ln2 with a 16-entry table
+// of (1/c, log2 c) and a degree-5 polynomial; then 2^(y log2 x) = 2^(j/32) *
+// 2^r with a 32-entry table and a cubic, all in double, rounded once to float.
+// The tables are glibc's __powf_log2_data / __exp2f_data constants.
+//
+// Verified: the same code compiled for the host (gcc, -ffp-contract=off)
+// returns libm's powf bit for bit for every one of the 2^32 float x at
+// y = 2 and every non-negative x at y = 0.5 (the two exponents the reference
+// uses); the x86_64 FMA variant of libm agrees with the unfused form on all of
+// them too.  tests/test_gpu_parity.py checks this device copy against the
+// oracle's libm calls.  No multiply-add is fused here (-ffp-contract=off).
+#pragma once
+#include "common.hpp"
+
+namespace cfd {
+namespace libm {
+
+__device__ __constant__ const double kLog2InvC[16] = {
+    0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
+    0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
+    0x1.0953f419900a7p+0, 0x1p+0,               0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
+    0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
+__device__ __constant__ const double kLog2C[16] = {
+    -0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2,
+    -0x1.01d9bf3f2b631p-2, -0x1.97c1d1b3b7afp-3,  -0x1.2f9e393af3c9fp-3, -0x1.960cbbf788d5cp-4,
+    -0x1.a6f9db6475fcep-5, 0x0p+0,                0x1.338ca9f24f53dp-4,  0x1.476a9543891bap-3,
+    0x1.e840b4ac4e4d2p-3,  0x1.40645f0c6651cp-2,  0x1.88e9c2c1b9ff8p-2,  0x1.ce0a44eb17bccp-2};
+// tab[i] = bits(2^(i/32)) - (i << 47)
+__device__ __constant__ const unsigned long long kExp2Tab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+
+__device__ inline bool zeroinfnan(uint32_t i) { return 2u * i - 1u >= 2u * 0x7f800000u - 1u; }
+// 0: not an integer, 1: odd integer, 2: even integer
+__device__ inline int checkint(uint32_t iy) {
+    const int e = iy >> 23 & 0xff;
+    if (e < 0x7f) return 0;
+    if (e > 0x7f + 23) return 2;
+    if (iy & ((1u << (0x7f + 23 - e)) - 1)) return 0;
+    if (iy & (1u << (0x7f + 23 - e))) return 1;
+    return 2;
+}
+
+__device__ inline float powf(float x, float y) {
+    uint32_t sign_bias = 0;
+    uint32_t ix = __float_as_uint(x);
+    const uint32_t iy = __float_as_uint(y);
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u || zeroinfnan(iy)) {
+        // x < 0x1p-126, inf or nan; or y is 0, inf or nan
+        if (zeroinfnan(iy)) {
+            if (2u * iy == 0) return 1.0f;
+            if (ix == 0x3f800000u) return 1.0f;
+            if (2u * ix > 2u * 0x7f800000u || 2u * iy > 2u * 0x7f800000u) return x + y;
+            if (2u * ix == 2u * 0x3f800000u) return 1.0f;
+            if ((2u * ix < 2u * 0x3f800000u) == !(iy & 0x80000000u)) return 0.0f;  // |x|<1 && y==inf
+            return y * y;
+        }
+        if (zeroinfnan(ix)) {
+            float x2 = x * x;
+            if ((ix & 0x80000000u) && checkint(iy) == 1) x2 = -x2;
+            return (iy & 0x80000000u) ? 1.0f / x2 : x2;
+        }
+        if (ix & 0x80000000u) {  // finite x < 0
+            const int yint = checkint(iy);
+            if (yint == 0) return __builtin_nanf("");
+            if (yint == 1) sign_bias = 1u << 16;  // SIGN_BIAS = 1 << (EXP2F_TABLE_BITS + 11)
+            ix &= 0x7fffffffu;
+        }
+        if (ix < 0x00800000u) {  // subnormal x: normalise
+            ix = __float_as_uint(x * 0x1p23f);
+            ix &= 0x7fffffffu;
+            ix -= 23u << 23;
+        }
+    }
+    // log2 of x (POWF_SCALE_BITS = 0 on x86_64)
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (tmp >> 19) % 16;
+    const uint32_t top = tmp & 0xff800000u;
+    const uint32_t iz = ix - top;
+    const int k = (int32_t)top >> 23;
+    const double invc = kLog2InvC[i], logc = kLog2C[i];
+    const double z = (double)__uint_as_float(iz);
+    const double r = z * invc - 1.0;
+    const double y0 = logc + (double)k;
+    const double r2 = r * r;
+    double yy = 0x1.27616c9496e0bp-2 * r + -0x1.71969a075c67ap-2;
+    const double p = 0x1.ec70a6ca7baddp-2 * r + -0x1.7154748bef6c8p-1;
+    const double r4 = r2 * r2;
+    double q = 0x1.71547652ab82bp+0 * r + y0;
+    q = p * r2 + q;
+    yy = yy * r4 + q;
+    const double ylogx = (double)y * yy;
+    if (((unsigned long long)__double_as_longlong(ylogx) >> 47 & 0xffff) >=
+        ((unsigned long long)__double_as_longlong(126.0) >> 47)) {
+        if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -__builtin_inff() : __builtin_inff();
+        if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
+    }
+    // exp2 (EXP2F_TABLE_BITS = 5, shift 0x1.8p+52 / 32)
+    double kd = ylogx + 0x1.8p+47;
+    const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
+    kd -= 0x1.8p+47;
+    const double rr = ylogx - kd;
+    unsigned long long t = kExp2Tab[ki % 32];
+    t += (ki + sign_bias) << 47;
+    const double s = __longlong_as_double((long long)t);
+    const double zz = 0x1.c6af84b912394p-5 * rr + 0x1.ebfce50fac4f3p-3;
+    const double rr2 = rr * rr;
+    double e = 0x1.62e42ff0c52d6p-1 * rr + 1.0;
+    e = zz * rr2 + e;
+    e = e * s;
+    return (float)e;
+}
+
+}  // namespace libm
+}  // namespace cfd

@@ -535,7 +535,6 @@ static int jacobi2d_small_pass(int K, const T *in, T *out, const T *div, const u
     return CFD_OK;
 }
 
-static int g_j2_blocking = 0;  // sweeps per pass: 0 auto, 1 off, 2..6, 8, 10, 12
 // r01 at 8192^2 f64 (Gcell/s): K=2 368, 3 554, 4 752, 5 876, 6 1051, 8 1232,
 // 10 1228, 12 1155 (the pass turns latency-bound past 8 levels)
 constexpr int kDefaultLevels2d = 8;
@@ -588,15 +587,14 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
     const bool vec_ok = (nx % V == 0) && aligned16(src) && aligned16(phi) && aligned16(tmp);
     T *a = phi, *b = tmp;
     const int tk = timing_begin(s);
-    if (g_j2_blocking != 1 && vec_ok && resid_every <= 0 && iters >= 2 && ny >= 3) {
+    if (tuning().j2_blocking != 1 && vec_ok && resid_every <= 0 && iters >= 2 && ny >= 3) {
         // temporally blocked: passes of K sweeps, the remainder last
         // small grids (auto depth 2) take the preloaded kernel, 4 sweeps a pass
-        const bool small = g_j2_blocking == 0 && auto_levels2d<T>(ny, nx) != kDefaultLevels2d;
-        static const int ks = [] { const char *e = getenv("CFD_J2_SMALL_K"); return e ? atoi(e) : 4; }();
-        // the preloaded kernel's shape: output rows per wave (1 or 2), cells per lane (1 or 16 B)
-        static const int srw = [] { const char *e = getenv("CFD_J2_SMALL_RW"); return e ? atoi(e) : 1; }();
-        static const int svec = [] { const char *e = getenv("CFD_J2_SMALL_VEC"); return e ? atoi(e) : 1; }();
-        const int K = small ? ks : g_j2_blocking >= 2 ? g_j2_blocking : auto_levels2d<T>(ny, nx);
+        const bool small = tuning().j2_blocking == 0 && auto_levels2d<T>(ny, nx) != kDefaultLevels2d;
+        // the preloaded kernel's shape: sweeps per launch (1..8), output rows per
+        // wave (1 or 2), cells per lane (1 or 16 B) -- Tuning, cfd_set_small2d_shape
+        const int ks = tuning().j2s_k, srw = tuning().j2s_rw, svec = tuning().j2s_vec;
+        const int K = small ? ks : tuning().j2_blocking >= 2 ? tuning().j2_blocking : auto_levels2d<T>(ny, nx);
         int done = 0;
         while (done < iters) {
             int k = iters - done < K ? iters - done : K;
@@ -909,7 +907,10 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
         const float pv = rd ? *reinterpret_cast<volatile float *>(&slots[(size_t)sl * niters + it - back]) : 0.f;
         const float p1 = wave_max(ln < kGsSlots ? pv : 0.f);
         const float p2 = wave_max(ln < kGsSlots ? 0.f : pv);
-        stopped = (it > 0 && p1 < tol) || (NI == 2 && it > 1 && p2 < tol);
+        // (a single-iteration launch is the odd last one: it must also skip
+        // when the stop fell on the first iteration of the pair before it, or
+        // it would overwrite that pair's input, which the rollback re-reads)
+        stopped = (it > 0 && p1 < tol) || (it > 1 && p2 < tol);
         // grid-uniform (every lane read the same words): a scalar branch, so the
         // level arrays below need no exec-masked copies (584 v_mov without it)
         stopped = __builtin_amdgcn_readfirstlane((int)stopped) != 0;
@@ -1050,9 +1051,7 @@ static void rbgs2d_small_launch(int NI, const float *in, float *out, const float
                                 int niters, hipStream_t s) {
     // shape: output rows per wave (1 or 2) and cells per lane (1 or 4); r01 at
     // 600 x 180, us per iteration: (1, 2) 2.36, (1, 1) 2.42, (4, 2) 3.38
-    static const int rw = [] { const char *e = getenv("CFD_GS_SMALL_RW"); return e && atoi(e) == 1 ? 1 : 2; }();
-    static const int vec = [] { const char *e = getenv("CFD_GS_SMALL_VEC"); return e && atoi(e) == 4 ? 4 : 1; }();
-    static const int wpb = [] { const char *e = getenv("CFD_GS_SMALL_WPB"); return e && atoi(e) == 16 ? 16 : 4; }();
+    const int rw = tuning().gs_rw, vec = tuning().gs_vec, wpb = tuning().gs_wpb;
 #define CFD_GSS_W(M, N, V, R, W)                                                                     \
     do {                                                                                             \
         constexpr int HL_ = (2 * N + V - 1) / V;                                                     \
@@ -1199,12 +1198,12 @@ int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rh
                                   iters, resid_every, resid_out, as_stream(stream));
 }
 
-int cfd_get_jacobi2d_levels(void) { return g_j2_blocking >= 2 ? g_j2_blocking : kDefaultLevels2d; }
+int cfd_get_jacobi2d_levels(void) { return tuning().j2_blocking >= 2 ? tuning().j2_blocking : kDefaultLevels2d; }
 
 int cfd_set_jacobi2d_blocking(int steps) {
     CFD_REQUIRE((steps >= 0 && steps <= 6) || steps == 8 || steps == 10 || steps == 12,
                 "blocking steps must be 0 (auto), 1 (off), 2..6, 8, 10 or 12");
-    g_j2_blocking = steps;
+    tuning().j2_blocking = steps;
     return CFD_OK;
 }
 
@@ -1231,7 +1230,7 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
     if (ny < 3 || nx < 3 || iterations == 0) return CFD_OK;
     const bool vec_ok = (nx % 4 == 0) && aligned16(phi) && aligned16(div);
     const int tk = timing_begin(s);
-    if (phi_tmp && g_j2_blocking != 1 && vec_ok && aligned16(phi_tmp)) {
+    if (phi_tmp && tuning().j2_blocking != 1 && vec_ok && aligned16(phi_tmp)) {
         // fused: one out-of-place pass per iteration (both colours), ping-pong
         if ((rc = fix_edge_rows<float>(phi, phi_tmp, nullptr, ny, nx, s))) return rc;
         float *a = phi, *b = phi_tmp;

@@ -60,32 +60,22 @@ int launch_fix_faces3d(const float *src, float *dst, const uint8_t *mask, int ny
     return CFD_OK;
 }
 
-struct J3Config {
-    int variant = 0;  // 0 auto, 1 LDS, 2 cache
-    int waves = 0;    // rows per workgroup (0 = auto)
-    int zchunk = 0;   // planes per workgroup (0 = auto)
-    int tb_steps = 0; // sweeps fused per pass: 0 auto, 1 off, 2..4
-    int tb_rows = 0;  // output rows per temporally blocked tile (0 = auto)
-    int tb_zchunk = 0;
-    int tb_prefetch = 0;  // 0 auto (2), 1, 2
-};
-static J3Config g_j3;
 // Jacobi sweeps per pass when tb_steps == 0 (r01 sweep at 1024^3: K=2 855,
 // K=3 1010-1030, K=4 1000 Gcell/s)
 constexpr int kDefaultLevels = 3;
 
 // defaults from the r01 tile sweep (1024^3): 13 output rows per tile, prefetch
 // 1 plane ahead; planes per tile chosen by jacobi3d_tb2_pass (0 = auto)
-int jacobi3d_tb_rows() { return g_j3.tb_rows ? g_j3.tb_rows : 13; }
-int jacobi3d_tb_zchunk() { return g_j3.tb_zchunk; }
-bool jacobi3d_tb_enabled() { return g_j3.tb_steps != 1; }
-int jacobi3d_tb_levels() { return g_j3.tb_steps >= 2 ? g_j3.tb_steps : kDefaultLevels; }
+int jacobi3d_tb_rows() { return tuning().tb_rows ? tuning().tb_rows : 13; }
+int jacobi3d_tb_zchunk() { return tuning().tb_zchunk; }
+bool jacobi3d_tb_enabled() { return tuning().tb_steps != 1; }
+int jacobi3d_tb_levels() { return tuning().tb_steps >= 2 ? tuning().tb_steps : kDefaultLevels; }
 bool rbgs3d_fused_ok(const float *phi, const float *phi_tmp, const float *div, const uint8_t *mask,
                      int nx) {
     return phi_tmp && jacobi3d_tb_enabled() && !mask && nx % 4 == 0 && aligned16(phi) &&
            aligned16(phi_tmp) && aligned16(div);
 }
-int jacobi3d_tb_prefetch() { return g_j3.tb_prefetch == 2 ? 2 : 1; }
+int jacobi3d_tb_prefetch() { return tuning().tb_prefetch == 2 ? 2 : 1; }
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
@@ -307,11 +297,11 @@ int jacobi3d_sweep(const float *in, float *out, const float *div, const uint8_t 
         return CFD_OK;
     }
     // defaults from the r01 tile sweep (1024^3): LDS tile, 16 rows, 64 planes
-    int variant = g_j3.variant ? g_j3.variant : 1;
-    int W = g_j3.waves ? g_j3.waves : 16;
+    int variant = tuning().j3_variant ? tuning().j3_variant : 1;
+    int W = tuning().j3_waves ? tuning().j3_waves : 16;
     const int nseg = ceil_div(nx, 256);
     const int L = ze - zb;
-    int zchunk = g_j3.zchunk;
+    int zchunk = tuning().j3_zchunk;
     if (zchunk <= 0) {
         // >= ~1024 workgroups when the grid allows, 64 planes per march otherwise
         const long tiles = (long)nseg * ceil_div(ny - 2, W);
@@ -445,7 +435,7 @@ RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double toler
 
 // Red-black GS iterations per fused pass: 2 when the blocking depth is set to
 // 4 levels (then a stop inside a pair is rolled back after the loop), else 1.
-int rbgs3d_iters_per_pass() { return g_j3.tb_steps == 4 ? 2 : 1; }
+int rbgs3d_iters_per_pass() { return tuning().tb_steps == 4 ? 2 : 1; }
 
 // One fused GS pass of `iters` (1, 2) iterations: the tuned 2-level kernel
 // when its rows are set explicitly (5, 13), the tall-tile kernel otherwise
@@ -453,9 +443,9 @@ int rbgs3d_iters_per_pass() { return g_j3.tb_steps == 4 ? 2 : 1; }
 int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
                       int iters, RbgsWs *ws, hipStream_t s, int lag) {
-    if (iters == 1 && !lag && (g_j3.tb_rows == 5 || g_j3.tb_rows == 13))
+    if (iters == 1 && !lag && (tuning().tb_rows == 5 || tuning().tb_rows == 13))
         return rbgs3d_tb_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, ws, s);
-    const int r = g_j3.tb_rows;
+    const int r = tuning().tb_rows;
     const bool shape_ok = iters == 1 ? (r == 16 || r == 18 || r == 20 || r == 28) : (r == 15 || r == 16);
     return rbgs3d_tbr_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, iters,
                            ws, 0, 0, shape_ok ? r : 0, s, lag);
@@ -471,7 +461,7 @@ int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, 
                           bool pre, hipStream_t s) {
     // the configured rows apply to passes of the configured depth; a shorter
     // remainder pass picks its own tile
-    const int rows = k == jacobi3d_tb_levels() ? g_j3.tb_rows : 0, zc = g_j3.tb_zchunk;
+    const int rows = k == jacobi3d_tb_levels() ? tuning().tb_rows : 0, zc = tuning().tb_zchunk;
     if (k == 1) return jacobi3d_sweep(in, out, src, nullptr, nz, ny, nx, zb, ze, h2, dt, pre, nullptr, s);
     if (k == 2) {
         if (rows == 5 || rows == 13)
@@ -495,7 +485,7 @@ extern "C" {
 
 int cfd_set_jacobi3d_prefetch(int planes) {
     CFD_REQUIRE(planes >= 0 && planes <= 2, "prefetch planes must be 0 (auto), 1 or 2");
-    g_j3.tb_prefetch = planes;
+    tuning().tb_prefetch = planes;
     return CFD_OK;
 }
 
@@ -506,9 +496,9 @@ int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
                 "blocking rows must be 0 (auto), 5, 13, 16, 18, 20, 28 (2 levels), 11, 16, 17, 18 (3), "
                 "9, 15, 16 (4)");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
-    g_j3.tb_steps = steps;
-    g_j3.tb_rows = rows;
-    g_j3.tb_zchunk = zchunk;
+    tuning().tb_steps = steps;
+    tuning().tb_rows = rows;
+    tuning().tb_zchunk = zchunk;
     return CFD_OK;
 }
 
@@ -519,9 +509,9 @@ int cfd_set_jacobi3d_config(int variant, int waves, int zchunk) {
     CFD_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8 || waves == 16,
                 "waves must be 0,1,2,4,8,16");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
-    g_j3.variant = variant;
-    g_j3.waves = waves;
-    g_j3.zchunk = zchunk;
+    tuning().j3_variant = variant;
+    tuning().j3_waves = waves;
+    tuning().j3_zchunk = zchunk;
     return CFD_OK;
 }
 

@@ -132,6 +132,7 @@ class OptimizedTurbulentSolver:
         self.device = torch.device(config.device)
         if self.device.type != "cuda":
             raise TypeError("OptimizedTurbulentSolver runs on the HIP device only")
+        self._has_ibm = True  # immersed-boundary forcing (the cylinder); the cavity has none
         self.setup_grid()
         self.setup_boundary_masks()
         self.initialize_fields()
@@ -229,10 +230,25 @@ class OptimizedTurbulentSolver:
 
     @property
     def diagnostics(self):
-        """Last step's log values (v5.py:410,415,422,429) when log_diagnostics."""
+        """The last step's log values (v5.py:410, 415, 422, 428-432), the same
+        numbers the reference prints: max|div u*| before the pressure solve,
+        max|grad phi|, max|div u| after the cleaning, nanmax|vorticity| (the
+        first four need log_diagnostics=True) and the mean kinetic energy."""
         d = self._scal[1:5].cpu().numpy()
+        n = len(self._energy_steps)
+        e = float(self._energy[n - 1].item()) if n else float("nan")
         return {"pre_div_max": float(d[0]), "grad_max": float(d[1]), "post_div_max": float(d[2]),
-                "vorticity_max": float(d[3])}
+                "vorticity_max": float(d[3]), "energy_mean": e}
+
+    def log_lines(self):
+        """The reference's five per-step INFO lines (v5.py:410-435) for the
+        last step, formatted as it formats them (log_diagnostics=True)."""
+        d, k = self.diagnostics, self.step - 1
+        return [f"Step {k}: Pre-pressure divergence = {d['pre_div_max']:.3f}",
+                f"Step {k}: Max pressure gradient = {d['grad_max']:.3f}",
+                f"Step {k}: Post-pressure divergence = {d['post_div_max']:.3f}",
+                f"Step {k}: Max vorticity = {d['vorticity_max']:.3f}",
+                f"Step {k}: Mean kinetic energy = {d['energy_mean']:.3f}"]
 
     def _energy_slot(self):
         k = len(self._energy_steps)
@@ -257,7 +273,8 @@ class OptimizedTurbulentSolver:
             self.tau_supg.zero_()
         self.apply_boundary_conditions(self.u_star, self.v_star)
         force_strength = min(1.0, self.step / cfg.initial_steps)
-        K.apply_ibm_fast(self.u_star, self.v_star, self.ibm_mask, force_strength)
+        if self._has_ibm:
+            K.apply_ibm_fast(self.u_star, self.v_star, self.ibm_mask, force_strength)
         call("cfd_divergence2d_f32", ptr(self.u_star), ptr(self.v_star), ptr(self.div_u_star), cfg.ny,
              cfg.nx, float(cfg.dx), float(cfg.dy), ptr(self._scal[1:2]) if diag else None, s)
         self.solve_pressure_fast(self.div_u_star)
@@ -271,7 +288,8 @@ class OptimizedTurbulentSolver:
             call("cfd_divergence2d_f32", ptr(self.u_star), ptr(self.v_star), ptr(self.div_u_star),
                  cfg.ny, cfg.nx, float(cfg.dx), float(cfg.dy), None, s)
         self.apply_boundary_conditions(self.u, self.v)
-        K.apply_ibm_fast(self.u, self.v, self.ibm_mask, force_strength)
+        if self._has_ibm:
+            K.apply_ibm_fast(self.u, self.v, self.ibm_mask, force_strength)
         if diag:
             call("cfd_vorticity_absmax2d_f32", ptr(self.u), ptr(self.v), ptr(self._mask_u8), cfg.ny,
                  cfg.nx, float(cfg.dx), float(cfg.dy), ptr(self._scal[4:5]), s)
@@ -285,14 +303,112 @@ class OptimizedTurbulentSolver:
 
     # ------------------------------------------------------------ output
     def save_snapshot(self, path, step: int, current_time: float):
-        """save_data_to_hdf5 layout (v5.py:454-470) as .npz: group step_%06d
-        with u, v, vorticity, X, Y and the time attribute; phi is added so
-        a run can restart exactly (the reference does not store it)."""
+        """save_data_to_hdf5 layout (v5.py:454-470) as .npz (h5py is absent):
+        group step_%06d with u, v, vorticity, X, Y and the time attribute.
+        Like the reference's file (opened in append mode, a group written
+        once), an existing snapshot file keeps its groups and gains this one.
+        phi and the step counter are added (the reference stores neither) so
+        that load_snapshot restarts the run exactly."""
         g = f"step_{step:06d}"
-        np.savez_compressed(path, **{f"{g}/u": self.u.cpu().numpy(), f"{g}/v": self.v.cpu().numpy(),
-                                     f"{g}/vorticity": self.compute_vorticity().cpu().numpy(),
-                                     f"{g}/X": self.X, f"{g}/Y": self.Y, f"{g}/phi": self.phi.cpu().numpy(),
-                                     f"{g}/time": np.float64(current_time)})
+        groups = {}
+        if os.path.exists(path):
+            with np.load(path, allow_pickle=False) as old:
+                groups = {k: old[k] for k in old.files}
+        if f"{g}/u" not in groups:  # `if group_name not in f` (v5.py:458)
+            groups.update({f"{g}/u": self.u.cpu().numpy(), f"{g}/v": self.v.cpu().numpy(),
+                           f"{g}/vorticity": self.compute_vorticity().cpu().numpy(),
+                           f"{g}/X": self.X, f"{g}/Y": self.Y, f"{g}/phi": self.phi.cpu().numpy(),
+                           f"{g}/time": np.float64(current_time), f"{g}/solver_step": np.int64(self.step)})
+        tmp = str(path) + ".tmp.npz"
+        np.savez_compressed(tmp, **groups)
+        os.replace(tmp, path)
+
+    def load_snapshot(self, path, step=None):
+        """Restart from a save_snapshot file: group step_%06d (the latest
+        when ``step`` is None) gives u, v, phi and the step counter; returns
+        the stored time.  The next time_step() then equals the uninterrupted
+        run's bit for bit: a step reads only u, v and the counter (phi is
+        zero-filled before each solve, v5.py:331/337)."""
+        with np.load(path, allow_pickle=False) as f:
+            steps = sorted({int(k.split("/")[0][5:]) for k in f.files if k.startswith("step_")})
+            if not steps:
+                raise ValueError(f"{path}: no step_%06d groups")
+            g = f"step_{(steps[-1] if step is None else int(step)):06d}"
+            if f"{g}/u" not in f.files:
+                raise KeyError(f"{path}: no group {g} (have {steps})")
+            shape = (self.config.ny, self.config.nx)
+            if f[f"{g}/u"].shape != shape:
+                raise ValueError(f"{path}: {g} holds a {f[f'{g}/u'].shape} grid, the solver {shape}")
+            self.u.copy_(torch.from_numpy(f[f"{g}/u"]))
+            self.v.copy_(torch.from_numpy(f[f"{g}/v"]))
+            self.phi.copy_(torch.from_numpy(f[f"{g}/phi"]))
+            self.step = int(f[f"{g}/solver_step"]) if f"{g}/solver_step" in f.files else int(g[5:])
+            return float(f[f"{g}/time"])
+
+
+# ------------------------------------------------------ lid-driven cavity
+@dataclass
+class LidDrivenCavityConfig(OptimizedTurbulentConfig):
+    """BASELINE.json config 1: the 2-D lid-driven cavity, 128 x 128, Re = 100,
+    500 Jacobi iterations per pressure solve.  The reference has no
+    incompressible cavity (its SWA cavity is compressible Euler,
+    SWA/cavity_flow_v1.py:39-69), so this is the v5 projection step
+    (v5.py:375-441, every kernel and quirk unchanged) on the unit square with
+    cavity walls instead of the cylinder channel's inlet / outlet / IBM:
+    nu = 1/Re = 0.01, artificial viscosity 1e-3, the
+    NumPy Jacobi branch (use_fast_pressure=False), fluid at rest initially."""
+    x_max: float = 1.0
+    y_max: float = 1.0
+    nx: int = 128
+    ny: int = 128
+    Re: float = 100.0
+    artificial_viscosity: float = 0.001
+    pressure_iterations: int = 500
+    use_fast_pressure: bool = False
+    lid_velocity: float = 1.0
+    output_dir: str = "cavity_re_100"
+    hdf5_file: str = "cavity_re_100.h5"
+
+
+def host_lid_bc(u, v, u_lid):
+    """The cavity walls on host arrays (what cfd_apply_lid_bc2d_f32 does):
+    no-slip left / right / bottom, the lid u = u_lid on the top row, written
+    last so it owns the top corners (the assignment pattern of v5.py:349-360)."""
+    u[:, 0] = 0
+    v[:, 0] = 0
+    u[:, -1] = 0
+    v[:, -1] = 0
+    u[0, :] = 0
+    v[0, :] = 0
+    u[-1, :] = np.float32(u_lid)
+    v[-1, :] = 0
+
+
+class LidDrivenCavitySolver(OptimizedTurbulentSolver):
+    """The v5 time step (OptimizedTurbulentSolver.time_step) on the lid-driven
+    cavity: no solid cells (no mask, no IBM forcing), cavity walls as the
+    boundary conditions, zero initial velocity."""
+
+    def __init__(self, config: LidDrivenCavityConfig):
+        super().__init__(config)
+        self._has_ibm = False
+
+    def setup_boundary_masks(self):
+        cfg = self.config
+        self.dist = None
+        self.cylinder_mask_host = np.zeros((cfg.ny, cfg.nx), bool)
+        self.ibm_mask_host = np.zeros((cfg.ny, cfg.nx), np.float64)
+        self.cylinder_mask = torch.from_numpy(self.cylinder_mask_host).to(self.device)
+        self._mask_u8 = None  # no solid cells: the sweeps skip the mask read
+        self.ibm_mask = torch.from_numpy(self.ibm_mask_host).to(self.device)
+
+    def initialize_potential_flow(self):
+        self.u.zero_()
+        self.v.zero_()
+
+    def apply_boundary_conditions(self, u, v):
+        call("cfd_apply_lid_bc2d_f32", ptr(u), ptr(v), self.config.ny, self.config.nx,
+             float(np.float32(self.config.lid_velocity)), stream_handle())
 
 
 def monitor_simulation_health(solver: OptimizedTurbulentSolver, step: int) -> bool:

@@ -159,6 +159,11 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
  * y: device float64 (ny) grid coordinates (np.linspace, v5.py:272). */
 int cfd_apply_bc2d_f32(float *u, float *v, const double *y, int ny, int nx, double y_max,
                        double v_inf, int step, void *stream);
+/* Lid-driven cavity walls (BASELINE config 1, the build's own: the reference
+ * has no incompressible cavity): u = v = 0 on the left, right and bottom walls,
+ * u = u_lid, v = 0 on the top row (the lid owns the top corners); the
+ * assignment pattern of v5.py:349-360. */
+int cfd_apply_lid_bc2d_f32(float *u, float *v, int ny, int nx, float u_lid, void *stream);
 /* apply_ibm_fast, v5.py:228-237: f *= (1 - ibm_mask*force_strength) where ibm_mask > 0,
  * evaluated in float64 like the reference's float64 mask. */
 int cfd_apply_ibm2d_f32(float *u, float *v, const double *ibm_mask, int n, double force_strength,
@@ -178,6 +183,10 @@ int cfd_vorticity_absmax2d_f32(const float *u, const float *v, const uint8_t *ma
 /* compute_vorticity, v5.py:365-373 (masked cells NaN, boundary ring 0). */
 int cfd_vorticity2d_f32(const float *u, const float *v, const uint8_t *mask, float *w, int ny,
                         int nx, double dx, double dy, void *stream);
+/* out[i] = NumPy's float32 scalar x[i] ** y, i.e. glibc powf (not correctly
+ * rounded): the device restatement the SUPG tau uses for the reference's
+ * `(u**2 + v**2) ** 0.5` (v5.py:155).  A parity hook. */
+int cfd_numpy_powf_f32(const float *x, float y, float *out, size_t n, void *stream);
 /* count of non-finite values in a and b (v5.py:601), into a device int. */
 int cfd_nonfinite_count_f32(const float *a, const float *b, size_t n, int *out, void *stream);
 
@@ -265,6 +274,17 @@ int cfd_rbgs_finish(void *ws, float *phi, const float *phi_tmp, size_t n, int *i
                     void *stream);
 
 /* ------------------------------------------------------------- tuning */
+/* The tuning knobs below are PER HOST THREAD: a cfd_set_* call changes the
+ * kernels of the solves the calling thread launches, never another thread's.
+ * Every thread starts from the process defaults (auto shapes; the CFD_*
+ * environment knobs, read once).  cfd_reset_tuning() returns the calling
+ * thread to those defaults. */
+int cfd_reset_tuning(void);
+/* Small-grid 2-D kernels (the v5 cylinder, 600 x 180): Jacobi sweeps per
+ * launch j2_k (1..8), output rows per wave j2_rw (1, 2), cells per lane j2_vec
+ * (1, or 4 = 16 bytes); red-black GS rows per wave gs_rw (1, 2), cells per lane
+ * gs_vec (1, 4), waves per workgroup gs_wpb (4, 16).  0 = the default. */
+int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec, int gs_wpb);
 /* Select the 3-D Jacobi kernel variant (bench / tile sweep):
  * variant 0 = auto, 1 = LDS plane tile, 2 = cache (no LDS); waves = rows per
  * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */
@@ -280,6 +300,12 @@ int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk);
 int cfd_get_jacobi3d_levels(void);
 /* Prefetch distance of the blocked kernel in planes (0 = auto = 1, 1, 2). */
 int cfd_set_jacobi3d_prefetch(int planes);
+
+/* The tile shape of the calling thread's last tall-tile launch (the fused
+ * Jacobi / red-black GS passes, jacobi3d_tbr): levels per pass, row waves,
+ * rows per row wave (output rows = waves * rows + 2 - 2 * levels) and planes
+ * per z-chunk; zeros before the first.  For tests that pin a shape. */
+int cfd_get_last_tbr_shape(int *levels, int *row_waves, int *rows_per_wave, int *zchunk);
 
 /* Sweep timing (bench harness): while enabled, every solve records a HIP
  * event pair on its stream around its sweep launches.  cfd_timing_read

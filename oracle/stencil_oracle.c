@@ -23,6 +23,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define IDX(i, j) ((size_t)(i) * (size_t)nx + (size_t)(j))
 
@@ -123,9 +126,9 @@ void oracle_jacobi3d_f32(const float *div, const uint8_t *mask, float *phi,
  * dt is np.float32 so dt_inv = 1.0/dt is float32.  Colour c visits
  * j = 1 + (i + c) % 2 step 2, i.e. (i+j) odd first.  Masked cells are skipped.
  * Returns the number of iterations executed (the break at v5.py:224-225).   */
-int oracle_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask,
-                      int ny, int nx, double dx, double dy, float dt,
-                      int iters, double tol) {
+int oracle_rbgs2d_f32_maxc(float *phi, const float *div, const uint8_t *mask,
+                           int ny, int nx, double dx, double dy, float dt,
+                           int iters, double tol, float *maxc) {
     const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy);
     const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv));
     const float cx = (float)dx2_inv, cy = (float)dy2_inv, cd = (float)denom_inv;
@@ -146,9 +149,17 @@ int oracle_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask,
                     if (change > max_change) max_change = change;
                     phi[IDX(i, j)] = pn;
                 }
+        if (maxc) maxc[it] = max_change;
         if (max_change < ftol) return it + 1;
     }
     return it;
+}
+
+/* the same, without the per-iteration max|change| history */
+int oracle_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask,
+                      int ny, int nx, double dx, double dy, float dt,
+                      int iters, double tol) {
+    return oracle_rbgs2d_f32_maxc(phi, div, mask, ny, nx, dx, dy, dt, iters, tol, NULL);
 }
 
 /* 3-D red-black generalisation of a3 (the build's own): colour c updates
@@ -185,6 +196,103 @@ int oracle_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask,
     return it;
 }
 
+/* ---- multi-threaded restatements (OpenMP) -----------------------------
+ * The same arithmetic as oracle_jacobi3d_f32 / oracle_rbgs3d_f32, with the
+ * planes of a sweep (Jacobi) or of one colour (red-black GS) split over the
+ * host's threads.  Bit-identical to the serial forms: a Jacobi cell reads
+ * only the previous sweep, a red-black cell of one colour reads only cells of
+ * the other colour, and max|change| is a max (order-free).  They make the
+ * full-size parity checks (1024^3) take seconds, and serve as the all-core
+ * CPU baseline.                                                             */
+int oracle_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+void oracle_jacobi3d_f32_mt(const float *div, const uint8_t *mask, float *phi,
+                            int nz, int ny, int nx, double h, float dt, int iters) {
+    size_t plane = (size_t)ny * nx, n = plane * nz;
+    float *rhs = (float *)malloc(n * sizeof(float));
+    float *nw = (float *)malloc(n * sizeof(float));
+    const float h2 = (float)(h * h);
+    const float sixth = 1.0f / 6.0f;
+#pragma omp parallel for schedule(static)
+    for (int z = 0; z < nz; ++z)
+        for (size_t k = (size_t)z * plane; k < (size_t)(z + 1) * plane; ++k) {
+            rhs[k] = (h2 * div[k]) / dt;
+            nw[k] = phi[k];
+        }
+    for (int it = 0; it < iters; ++it) {
+#pragma omp parallel for schedule(static)
+        for (int z = 1; z < nz - 1; ++z)
+            for (int i = 1; i < ny - 1; ++i)
+                for (int j = 1; j < nx - 1; ++j) {
+                    size_t c = (size_t)z * plane + IDX(i, j);
+                    if (mask && mask[c]) { nw[c] = 0.0f; continue; }
+                    float s = phi[c + 1] + phi[c - 1];
+                    s = s + phi[c + nx];
+                    s = s + phi[c - nx];
+                    s = s + phi[c + plane];
+                    s = s + phi[c - plane];
+                    nw[c] = sixth * (s - rhs[c]);
+                }
+        if (mask && it == 0)  /* masked face cells: phi_new[mask] = 0 hits them too */
+#pragma omp parallel for schedule(static)
+            for (int z = 0; z < nz; ++z)
+                for (size_t k = (size_t)z * plane; k < (size_t)(z + 1) * plane; ++k)
+                    if (mask[k]) nw[k] = 0.0f;
+        float *t = phi;  /* swap by copy-back: phi <- nw (faces equal in both) */
+#pragma omp parallel for schedule(static)
+        for (int z = 0; z < nz; ++z)
+            memcpy(t + (size_t)z * plane, nw + (size_t)z * plane, plane * sizeof(float));
+    }
+    free(rhs);
+    free(nw);
+}
+
+int oracle_rbgs3d_f32_mt(float *phi, const float *div, const uint8_t *mask,
+                         int nz, int ny, int nx, double dx, double dy, double dz,
+                         float dt, int iters, double tol) {
+    size_t plane = (size_t)ny * nx;
+    const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy), dz2_inv = 1.0 / (dz * dz);
+    const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv + dz2_inv));
+    const float cx = (float)dx2_inv, cy = (float)dy2_inv, cz = (float)dz2_inv, cd = (float)denom_inv;
+    const float dt_inv = 1.0f / dt;
+    const float ftol = (float)tol;
+    int it;
+    for (it = 0; it < iters; ++it) {
+        float max_change = 0.0f;
+        for (int color = 0; color < 2; ++color) {
+#pragma omp parallel
+            {
+                float mloc = 0.0f;
+#pragma omp for schedule(static)
+                for (int z = 1; z < nz - 1; ++z)
+                    for (int i = 1; i < ny - 1; ++i)
+                        for (int j = 1 + (z + i + color) % 2; j < nx - 1; j += 2) {
+                            size_t c = (size_t)z * plane + IDX(i, j);
+                            if (mask && mask[c]) continue;
+                            float rhs = -div[c] * dt_inv;
+                            float a = cx * (phi[c + 1] + phi[c - 1]);
+                            float b = cy * (phi[c + nx] + phi[c - nx]);
+                            float e = cz * (phi[c + plane] + phi[c - plane]);
+                            float pn = (((a + b) + e) - rhs) * cd;
+                            float change = fabsf(pn - phi[c]);
+                            if (change > mloc) mloc = change;
+                            phi[c] = pn;
+                        }
+#pragma omp critical
+                if (mloc > max_change) max_change = mloc;
+            }
+        }
+        if (max_change < ftol) return it + 1;
+    }
+    return it;
+}
+
 /* ---- a6: compute_supg_stabilization_fast, v5.py:149-162 --------------- */
 static float supg_tau(float u, float v, float nu, double h, float dt) {
     /* NumPy float32 scalar `u**2` and `** 0.5` both go through libm powf,
@@ -197,6 +305,12 @@ static float supg_tau(float u, float v, float nu, double h, float dt) {
         return ((float)h / (2.0f * vm)) * lim;
     }
     return dt / 2.0f;
+}
+
+/* libm powf elementwise (NumPy float32 scalar `**`): the checker for the
+ * library's device restatement of glibc powf (cfd_numpy_powf_f32). */
+void oracle_powf_f32(const float *x, float y, float *out, size_t n) {
+    for (size_t k = 0; k < n; ++k) out[k] = powf(x[k], y);
 }
 
 /* ---- a7/a8/a9/a10: predictor, v5.py:112-176 and :388-403 ---------------

@@ -227,6 +227,134 @@ def gen_steps(ref) -> None:
         print("wrote", name)
 
 
+def _recorders(ref, solver):
+    """Wrap the reference's module-level kernels and compute_vorticity so one
+    time_step() call exposes the values its log lines print (v5.py:410, 415,
+    422, 428-432) at full precision: max|div_u_star|, max|grad phi|, max|post
+    div| and nanmax|vorticity|.  The wrappers only record what the reference
+    returns; time_step() itself runs unchanged."""
+    rec = {"div": [], "grad": [], "vort": []}
+    div0, grad0 = ref.compute_divergence_fast, ref.compute_gradient_fast
+    vort0 = solver.compute_vorticity
+
+    def div_w(u, v, dx, dy):
+        out = div0(u, v, dx, dy)
+        rec["div"].append(np.max(np.abs(out)))
+        return out
+
+    def grad_w(phi, dx, dy):
+        gx, gy = grad0(phi, dx, dy)
+        rec["grad"].append(np.max(np.abs(np.sqrt(gx ** 2 + gy ** 2))))
+        return gx, gy
+
+    def vort_w():
+        w = vort0()
+        rec["vort"].append(np.nanmax(np.abs(w)))
+        return w
+
+    ref.compute_divergence_fast, ref.compute_gradient_fast = div_w, grad_w
+    solver.compute_vorticity = vort_w
+
+    def restore():
+        ref.compute_divergence_fast, ref.compute_gradient_fast = div0, grad0
+        del solver.compute_vorticity
+    return rec, restore
+
+
+def gen_diagnostics(ref) -> None:
+    """The per-step log values of the two 3-step runs of gen_steps, recorded
+    at full precision from the reference's own calls (see _recorders), plus
+    the log lines themselves (3 decimals, as the reference prints them)."""
+    import logging
+    for fast in (True, False):
+        cfg = make_cfg(ref, nx=120, ny=36, pressure_iterations=200, use_fast_pressure=fast)
+        with _quiet_cwd():
+            solver = ref.OptimizedTurbulentSolver(cfg)
+        lines = []
+
+        class Grab(logging.Handler):
+            def emit(self, record):
+                lines.append(record.getMessage())
+        h = Grab()
+        ref.logger.addHandler(h)
+        ref.logger.setLevel(logging.INFO)
+        rec, restore = _recorders(ref, solver)
+        try:
+            for _ in range(3):
+                solver.time_step()
+        finally:
+            restore()
+            ref.logger.removeHandler(h)
+        # per step, compute_divergence_fast runs 4 times (pre-pressure, twice
+        # inside clean_divergence_fast, post) and compute_gradient_fast 3 times
+        # (the projection, then twice inside clean_divergence_fast)
+        assert len(rec["div"]) == 12 and len(rec["grad"]) == 9 and len(rec["vort"]) == 3
+        out = {"pre_div_max": np.array(rec["div"][0::4], np.float32),
+               "post_div_max": np.array(rec["div"][3::4], np.float32),
+               "grad_max": np.array(rec["grad"][0::3], np.float32),
+               "vorticity_max": np.array(rec["vort"], np.float32),
+               "energy": np.array([e for _, e in solver.energy_history], np.float32),
+               "log_lines": np.array(lines)}
+        name = f"diag_v5_120x36_n3_{'gs' if fast else 'jacobi'}.npz"
+        np.savez_compressed(OUT / name, **out)
+        print("wrote", name, len(lines), "log lines")
+
+
+def gen_steps_late(ref) -> None:
+    """Two time_step() calls from the potential-flow state with the step
+    counter set to 1000 and to 1500: the CFL / viscous dt branch
+    (v5.py:322-326), the saturated IBM force (v5.py:406) and the full inlet
+    perturbation ramp (v5.py:351-352), for both pressure branches."""
+    for fast in (True, False):
+        rec = {}
+        for start in (1000, 1500):
+            cfg = make_cfg(ref, nx=120, ny=36, pressure_iterations=200, use_fast_pressure=fast)
+            with _quiet_cwd():
+                solver = ref.OptimizedTurbulentSolver(cfg)
+            solver.step = start
+            for s in range(2):
+                dt = solver.time_step()
+                k = f"s{start}_{s + 1}"
+                rec[f"dt_{k}"] = np.float32(dt)
+                rec[f"u_{k}"] = solver.u.copy()
+                rec[f"v_{k}"] = solver.v.copy()
+                rec[f"phi_{k}"] = solver.phi.copy()
+                rec[f"u_star_{k}"] = solver.u_star.copy()
+                rec[f"div_{k}"] = solver.div_u_star.copy()
+            rec[f"energy_s{start}"] = np.array([e for _, e in solver.energy_history], np.float64)
+        name = f"step_v5_120x36_late_{'gs' if fast else 'jacobi'}.npz"
+        np.savez_compressed(OUT / name, **rec)
+        print("wrote", name)
+
+
+def gen_health(ref) -> None:
+    """monitor_simulation_health (v5.py:599-613) on crafted states: healthy,
+    non-finite u / v, over-speed, and a divergence between the two
+    thresholds (20 up to step 1000, 2 after), each at steps 500 and 1500."""
+    cfg = make_cfg(ref, nx=120, ny=36)
+    with _quiet_cwd():
+        solver = ref.OptimizedTurbulentSolver(cfg)
+    rng = np.random.default_rng(5)
+    u0, v0 = solver.u.copy(), solver.v.copy()
+    noisy_u = (u0 + rng.uniform(-0.3, 0.3, u0.shape)).astype(np.float32)
+    cases = {"healthy": (u0, v0), "nan_u": (u0.copy(), v0), "inf_v": (u0, v0.copy()),
+             "fast_u": (u0.copy(), v0), "at_limit": (u0.copy(), v0), "divergent": (noisy_u, v0)}
+    cases["nan_u"][0][7, 9] = np.nan
+    cases["inf_v"][1][3, 50] = -np.inf
+    cases["fast_u"][0][10, 20] = np.float32(5.25)
+    cases["at_limit"][0][10, 20] = np.float32(5.0)
+    out = {}
+    for name, (u, v) in cases.items():
+        solver.u, solver.v = u, v
+        div_max = np.max(np.abs(ref.compute_divergence_fast(u, v, cfg.dx, cfg.dy)))
+        out[f"{name}_u"], out[f"{name}_v"] = u, v
+        out[f"{name}_div_max"] = np.float32(div_max)
+        for step in (500, 1500):
+            out[f"{name}_ok_{step}"] = np.bool_(ref.monitor_simulation_health(solver, step))
+    np.savez_compressed(OUT / "health_v5_120x36.npz", **out)
+    print("wrote health_v5_120x36.npz", {k: bool(v) for k, v in out.items() if "_ok_" in k})
+
+
 def main() -> None:
     if not REF_FILE.exists():
         raise SystemExit(f"reference not found at {REF_FILE}; fixtures are generated in the build container only")
@@ -236,6 +364,9 @@ def main() -> None:
     gen_rbgs(ref)
     gen_predictor(ref)
     gen_steps(ref)
+    gen_diagnostics(ref)
+    gen_steps_late(ref)
+    gen_health(ref)
 
 
 if __name__ == "__main__":

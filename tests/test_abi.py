@@ -87,3 +87,39 @@ def test_slab_cu_partition_rejects_unbalanced_requests(ncu, reserve):
     xm = (ctypes.c_uint32 * words)()
     with pytest.raises(_lib.CfdError, match="slab_cu_partition"):
         _lib.call("cfd_slab_cu_partition", ncu, reserve, ctypes.addressof(cm), ctypes.addressof(xm), words)
+
+
+def test_tuning_knobs_are_per_thread():
+    """cfd_set_* changes only the calling thread's kernels (thread_local
+    tuning): another thread keeps the defaults, and cfd_reset_tuning restores
+    them (host-only calls, no GPU)."""
+    import threading
+    L = _lib.lib()
+    _lib.call("cfd_reset_tuning")
+    base3, base2 = L.cfd_get_jacobi3d_levels(), L.cfd_get_jacobi2d_levels()
+    _lib.call("cfd_set_jacobi3d_blocking", 4, 0, 0)
+    _lib.call("cfd_set_jacobi2d_blocking", 5)
+    seen = {}
+
+    def other():
+        seen["j3"], seen["j2"] = L.cfd_get_jacobi3d_levels(), L.cfd_get_jacobi2d_levels()
+        _lib.call("cfd_set_jacobi3d_blocking", 2, 0, 0)  # must not leak back
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    try:
+        assert seen == {"j3": base3, "j2": base2}
+        assert L.cfd_get_jacobi3d_levels() == 4 and L.cfd_get_jacobi2d_levels() == 5
+    finally:
+        _lib.call("cfd_reset_tuning")
+    assert (L.cfd_get_jacobi3d_levels(), L.cfd_get_jacobi2d_levels()) == (base3, base2)
+
+
+@pytest.mark.parametrize("args", [(9, 0, 0, 0, 0, 0), (-1, 0, 0, 0, 0, 0), (0, 3, 0, 0, 0, 0), (0, 0, 2, 0, 0, 0),
+                                  (0, 0, 0, 0, 3, 0), (0, 0, 0, 0, 0, 8)])
+def test_small2d_shape_validated(args):
+    """Out-of-range small-grid shapes are rejected (the r01 env knob took any
+    K and could count sweeps it never ran)."""
+    with pytest.raises(_lib.CfdError, match="small-grid"):
+        _lib.call("cfd_set_small2d_shape", *args)

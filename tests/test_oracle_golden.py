@@ -128,3 +128,109 @@ def test_rbgs3d_reduces_to_2d_template_on_thin_grid():
     assert n3 == 5
     assert np.isfinite(phi3).all()
     assert np.array_equal(phi3[0], 0 * phi3[0]) and np.array_equal(phi3[2], 0 * phi3[2])
+
+
+@pytest.mark.parametrize("branch", ["gs", "jacobi"])
+def test_oracle_diagnostics_match_reference_log_values(golden, branch):
+    """The per-step log values (v5.py:410, 415, 422, 428-432), recorded at full
+    precision from the reference's own calls, and its printed log lines."""
+    d = golden(f"step_v5_120x36_n3_{branch}.npz")
+    g = golden(f"diag_v5_120x36_n3_{branch}.npz")
+    c = _cfg(nx=120, ny=36, pressure_iterations=200, use_fast_pressure=(branch == "gs"))
+    _, y, _, _ = host_grid(c)
+    s = oracle.OracleSolver(c, d["u0"], d["v0"], d["cylinder_mask"], d["ibm_mask"], y)
+    lines = []
+    for k in range(3):
+        s.time_step()
+        for key in ("pre_div_max", "grad_max", "post_div_max", "vorticity_max"):
+            assert np.float32(s.diagnostics[key]) == g[key][k], (key, k)
+        e = s.energy_history[-1][1]
+        lines += [f"Step {k}: Pre-pressure divergence = {s.diagnostics['pre_div_max']:.3f}",
+                  f"Step {k}: Max pressure gradient = {s.diagnostics['grad_max']:.3f}",
+                  f"Step {k}: Post-pressure divergence = {s.diagnostics['post_div_max']:.3f}",
+                  f"Step {k}: Max vorticity = {s.diagnostics['vorticity_max']:.3f}",
+                  f"Step {k}: Mean kinetic energy = {e:.3f}"]
+    assert lines == [str(x) for x in g["log_lines"]]
+
+
+@pytest.mark.parametrize("branch", ["gs", "jacobi"])
+@pytest.mark.parametrize("start", [1000, 1500])
+def test_oracle_late_steps_bitexact(golden, branch, start):
+    """time_step() with the step counter at 1000 / 1500: the CFL / viscous dt
+    (v5.py:322-326), the saturated IBM force (:406), the full inlet ramp (:351)."""
+    d = golden(f"step_v5_120x36_n3_{branch}.npz")
+    g = golden(f"step_v5_120x36_late_{branch}.npz")
+    c = _cfg(nx=120, ny=36, pressure_iterations=200, use_fast_pressure=(branch == "gs"))
+    _, y, _, _ = host_grid(c)
+    s = oracle.OracleSolver(c, d["u0"], d["v0"], d["cylinder_mask"], d["ibm_mask"], y)
+    s.step = start
+    for k in (1, 2):
+        dt = s.time_step()
+        key = f"s{start}_{k}"
+        assert np.float32(dt) == g[f"dt_{key}"] and g[f"dt_{key}"] != np.float32(2e-5)
+        for f, a in (("u", s.u), ("v", s.v), ("phi", s.phi), ("u_star", s.u_star), ("div", s.div_u_star)):
+            assert np.array_equal(a, g[f"{f}_{key}"]), (f, k)
+    assert np.array_equal(np.array([v for _, v in s.energy_history]), g[f"energy_s{start}"])
+
+
+def test_oracle_health_monitor_matches_reference(golden):
+    """monitor_simulation_health (v5.py:599-613) on the crafted states."""
+    g = golden("health_v5_120x36.npz")
+    c = _cfg(nx=120, ny=36)
+    names = sorted({k.rsplit("_ok_", 1)[0] for k in g.files if "_ok_" in k})
+    assert {"healthy", "nan_u", "inf_v", "fast_u", "at_limit", "divergent"} <= set(names)
+    for n in names:
+        assert np.max(np.abs(oracle.divergence2d(g[f"{n}_u"], g[f"{n}_v"], dx=c.dx, dy=c.dy))) == g[f"{n}_div_max"] \
+            or not np.isfinite(g[f"{n}_div_max"])
+        for step in (500, 1500):
+            assert oracle.monitor_simulation_health(g[f"{n}_u"], g[f"{n}_v"], c, step) == bool(g[f"{n}_ok_{step}"]), \
+                (n, step)
+
+
+def test_oracle_powf_is_numpy_scalar_power():
+    """The oracle's libm powf is what NumPy's float32 scalar ``**`` computes
+    (the arithmetic of v5.py:155 under the stubbed reference), including the
+    inputs where it is not the correctly rounded square / square root."""
+    rng = np.random.default_rng(17)
+    x = np.concatenate([rng.standard_normal(3000), rng.uniform(0, 50, 3000) ** 2]).astype(np.float32)
+    for y, xs in ((2.0, x), (0.5, np.abs(x))):
+        got = oracle.numpy_powf(xs, y)
+        ref = np.array([np.float32(a) ** y for a in xs], np.float32)
+        assert np.array_equal(got, ref)
+    sq = oracle.numpy_powf(x, 2.0)
+    assert (sq != x * x).sum() > 0  # powf is not x*x everywhere: why the device port exists
+
+
+def test_oracle_mt_forms_bitexact():
+    """The OpenMP restatements (full-size parity checks, all-core CPU
+    baseline) equal the serial ones bit for bit."""
+    rng = np.random.default_rng(23)
+    div = rng.standard_normal((17, 21, 36)).astype(np.float32)
+    p0 = rng.standard_normal(div.shape).astype(np.float32)
+    m = rng.random(div.shape) < 0.1
+    for mask in (None, m):
+        a = oracle.jacobi3d(div, p0, h=0.05, dt=np.float32(1e-3), iters=6, mask=mask)
+        b = oracle.jacobi3d(div, p0, h=0.05, dt=np.float32(1e-3), iters=6, mask=mask, mt=True)
+        assert np.array_equal(a, b)
+        a, na = oracle.rbgs3d(div, p0, dx=.05, dy=.06, dz=.07, dt=np.float32(1e-3), iters=6, tol=1e-8, mask=mask)
+        b, nb = oracle.rbgs3d(div, p0, dx=.05, dy=.06, dz=.07, dt=np.float32(1e-3), iters=6, tol=1e-8, mask=mask,
+                              mt=True)
+        assert np.array_equal(a, b) and na == nb
+
+
+def test_cavity_cpu_numpy_path_equals_oracle():
+    """BASELINE config 1 on the CPU (no GPU): the lid-driven cavity step with
+    the reference's NumPy Jacobi form (the path bench.py times as the cavity's
+    cpu_baseline) equals the C-oracle step bit for bit; the walls hold."""
+    from cfd_simulations_amd.solver import LidDrivenCavityConfig
+    c = LidDrivenCavityConfig()
+    assert (c.nx, c.ny, c.pressure_iterations, c.use_fast_pressure) == (128, 128, 500, False)
+    assert c.nu == np.float32(0.01) and c.artificial_viscosity == np.float32(1e-3)
+    a, b = oracle.OracleCavitySolver(c), oracle.OracleCavitySolver(c, numpy_jacobi=True)
+    for _ in range(2):
+        assert a.time_step() == b.time_step()
+    for f in ("u", "v", "phi", "u_star", "div_u_star"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert (a.u[-1] == 1.0).all() and (a.u[:-1, 0] == 0).all() and (a.u[:-1, -1] == 0).all()
+    assert (a.u[0] == 0).all() and (a.v[[0, -1]] == 0).all()
+    assert np.abs(a.u[1:-1, 1:-1]).max() > 0  # the lid drives the interior
