@@ -220,8 +220,13 @@ def main():
             rhs = None if ARGS.no_rhs_ws else torch.empty_like(div)
 
             def step():
-                phi.zero_()
-                K.solve_pressure_jacobi3d(phi, div, h, dt, None, iters, phi_tmp=tmp, rhs_ws=rhs)
+                if rhs is None:
+                    phi.zero_()
+                    K.solve_pressure_jacobi3d(phi, div, h, dt, None, iters, phi_tmp=tmp, rhs_ws=None)
+                else:
+                    # phi = zeros + the sweeps (v5.py:337-346) in one call: the first
+                    # pass starts from the zeros and forms the RHS workspace
+                    K.solve_pressure_jacobi3d_zero(phi, div, h, dt, iters, phi_tmp=tmp, rhs_ws=rhs)
         else:
             comm = S.RcclComm(rank, world)
             sj = S.SlabJacobi3D(plan, ny, nx, h, dt, comm, device=dev, rhs_workspace=not ARGS.no_rhs_ws)

@@ -32,6 +32,7 @@ PROTOTYPES = {
     "cfd_jacobi2d_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
     "cfd_jacobi3d_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_double, c_float, c_int, c_int, P,
                                  P]),
+    "cfd_jacobi3d_zero_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_double, c_float, c_int, P]),
     "cfd_rbgs_workspace_bytes": (c_size_t, [c_int]),
     "cfd_rbgs2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_float, c_int, c_double,
                                P, P, P, P]),

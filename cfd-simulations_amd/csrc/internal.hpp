@@ -55,6 +55,10 @@ void set_cu_reserve(int n);
 int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float *div, int nz,
                       int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2,
                       float dt, int zchunk, bool pre, hipStream_t s);
+// first pass of a solve: forms the rhs workspace (and starts from phi = 0 when zero)
+int jacobi3d_tbr_first_pass(int K, float *out, const float *div, float *rhs_out, const float *in,
+                            int nz, int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi,
+                            float h2, float dt, int zchunk, bool zero, hipStream_t s);
 // red-black GS workspace (declared below) passes on tall tiles
 struct RbgsWs;
 struct RbgsConsts;

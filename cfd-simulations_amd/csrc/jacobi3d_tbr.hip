@@ -78,7 +78,15 @@ struct TbrArgs {
     int npairs;      // GS rollback: pair passes the solve scheduled
     const int *count;  // GS rollback: iterations done (device)
     int lag;         // GS: the stop test reads maxc[it-1-lag], maxc[it-2-lag] (see rbgs3d_tbr_pass)
+    float *rhs_out;  // first pass (F & kFirstRhs): the rhs of the owned cells goes here
 };
+// First-pass flags (template F of jacobi3d_tbr, Jacobi on the LDS-DMA path):
+// kFirstRhs: `div` is raw; the row waves form f32(h*h)*div/dt once per cell
+// (the bits k_rhs_f32 and the in-register form give) and store it to rhs_out
+// for the later passes, replacing the separate RHS prologue;
+// kFirstZero: level 0 is phi = 0 (v5.py:337's zero fill): nothing is read
+// from `in`, so the pass can write either buffer and no memset is needed.
+enum { kFirstRhs = 1, kFirstZero = 2 };
 
 // One level on the float4 of cells x .. x+3.  Jacobi: every interior cell.
 // Red-black GS: the cells of colour `par` parity (v5.py:213-219 generalised:
@@ -144,7 +152,7 @@ __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S
 // The halo wave of jacobi3d_tbr (see there): loads the two outermost level-0
 // rows and the 4-float x-halo chunks of every row, and computes levels
 // 1..K-1 of the chunks, in lock step (two barriers per step) with the row waves.
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE>
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F>
 __device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0, int z1, int y0, int xs) {
     constexpr int NR = NWR * RPW + 2;
     constexpr int RS = 264;
@@ -178,19 +186,21 @@ __device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0,
     const int hx = side ? xs + 256 : xs - 4;
     const size_t hofs = (size_t)(hon ? yr : 0) * nx + (hon ? hx : 0);
     const int col = side ? 260 : 0;
+    constexpr bool ZERO = (F & kFirstZero) != 0;  // level 0 = 0: no phi loads
     auto ldh = [&](const float *base, int p) {
         return (hon && p >= 0 && p <= nz - 1) ? ldg4(base + (size_t)p * plane + hofs) : z4;
     };
-    auto ldlo = [&](int p) { return (elo && p >= 0 && p <= nz - 1) ? ldg4(P(p) + olo) : z4; };
-    auto ldhi = [&](int p) { return (ehi && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ohi) : z4; };
+    auto ldhp = [&](int p) { return ZERO ? z4 : ldh(a.in, p); };
+    auto ldlo = [&](int p) { return (!ZERO && elo && p >= 0 && p <= nz - 1) ? ldg4(P(p) + olo) : z4; };
+    auto ldhi = [&](int p) { return (!ZERO && ehi && p >= 0 && p <= nz - 1) ? ldg4(P(p) + ohi) : z4; };
     float4 lo = ldlo(zs), hi = ldhi(zs);
     float4 H[K][3];
     float4 Hr[K];
 #pragma unroll
     for (int l = 0; l < K; ++l) H[l][0] = H[l][1] = H[l][2] = z4;
-    H[0][0] = ldh(a.in, zs - 1);
-    H[0][1] = ldh(a.in, zs);
-    H[0][2] = ldh(a.in, zs + 1);
+    H[0][0] = ldhp(zs - 1);
+    H[0][1] = ldhp(zs);
+    H[0][2] = ldhp(zs + 1);
 #pragma unroll
     for (int i = 0; i < K; ++i) Hr[i] = ldh(a.div, zs - i);
     float4 Lq[PD], Uq[PD], Hq[PD], Rn[PD];
@@ -198,13 +208,13 @@ __device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0,
     for (int i = 0; i + 1 < PD; ++i) {
         Lq[i] = ldlo(zs + 1 + i);
         Uq[i] = ldhi(zs + 1 + i);
-        Hq[i] = ldh(a.in, zs + 2 + i);
+        Hq[i] = ldhp(zs + 2 + i);
         Rn[i] = ldh(a.div, zs + 1 + i);
     }
     for (int z = zs; z <= zl; ++z) {
         Lq[PD - 1] = ldlo(z + PD);
         Uq[PD - 1] = ldhi(z + PD);
-        Hq[PD - 1] = ldh(a.in, z + 1 + PD);
+        Hq[PD - 1] = ldhp(z + 1 + PD);
         Rn[PD - 1] = ldh(a.div, z + PD);
         // phase W
         if (elo) sts4(T(0, 0) + 4 + 4 * lane, lo);
@@ -261,7 +271,7 @@ __device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0,
 // 139 KB of LDS -- was measured at 1007 against 1131 Gcell/s for this one.)
 // MODE kRbgs: K/2 red-black iterations per pass (level l = colour (l-1)&1);
 // see rbgs3d_tbr_pass for the stop rule and the rollback.
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE>
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F = 0>
 __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     constexpr int NR = NWR * RPW + 2;  // level-0 rows per tile
     constexpr int W = NR - 2 * K;      // output rows
@@ -294,6 +304,19 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     };
 
     static_assert(MODE == kJacobi || (K % 2 == 0 && !PRE), "GS: whole iterations, raw div");
+    static_assert(F == 0 || (MODE == kJacobi && !PRE && DMA), "first pass: Jacobi, raw div, DMA path");
+    constexpr bool ZERO = (F & kFirstZero) != 0, RHSW = (F & kFirstRhs) != 0;
+    constexpr bool PREL = PRE || RHSW;  // the row waves' queues hold the rhs
+    // the rhs from raw div (RHSW), the same bits as k_rhs_f32
+    auto torhs = [&](float4 d) {
+        if constexpr (RHSW) {
+            d.x = (a.h2 * d.x) / a.dt;
+            d.y = (a.h2 * d.y) / a.dt;
+            d.z = (a.h2 * d.z) / a.dt;
+            d.w = (a.h2 * d.w) / a.dt;
+        }
+        return d;
+    };
     constexpr int NIT = MODE == kRbgs ? K / 2 : 1;  // GS iterations per pass
     if (MODE == kRbgs) {
         if (a.rollback) {
@@ -360,14 +383,14 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             for (int j = 0; j < RPW; ++j) {
 #pragma unroll
                 for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = z4;
-                V[j][0] = ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]);
-                V[j][1] = ldb4(plane_rsrc(a.in, zs, nz, plane), bo[j]);
+                V[j][0] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]);
+                V[j][1] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs, nz, plane), bo[j]);
                 V[j][2] = z4;
                 Rq[j][0] = z4;
 #pragma unroll
-                for (int i = 1; i < K; ++i) Rq[j][i] = ldb4(plane_rsrc(a.div, zs - i, nz, plane), bo[j]);
+                for (int i = 1; i < K; ++i) Rq[j][i] = torhs(ldb4(plane_rsrc(a.div, zs - i, nz, plane), bo[j]));
                 // read at step zs (even): plane zs + 1 and rhs zs in the odd buffers
-                dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], st_p1 + (rr[j] - 1) * 256);
+                if (!ZERO) dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], st_p1 + (rr[j] - 1) * 256);
                 dma_row(plane_rsrc4(a.div, zs, nz, plane), bo[j], st_r1 + (rr[j] - 1) * 256);
             }
             auto step = [&](int z, auto parc) {
@@ -381,7 +404,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     const v4i32 rd = plane_rsrc4(a.div, z + 1, nz, plane);
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
-                        dma_row(rp, bo[j], pw + (rr[j] - 1) * 256);
+                        if (!ZERO) dma_row(rp, bo[j], pw + (rr[j] - 1) * 256);
                         dma_row(rd, bo[j], rw + (rr[j] - 1) * 256);
                     }
                 }
@@ -395,14 +418,24 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 }
                 // the previous step's DMAs have landed once at most this step's
                 // 2 * RPW remain in flight (they are issued in order)
-                wait_vmcnt<2 * RPW>();
+                wait_vmcnt<(ZERO ? 1 : 2) * RPW>();
                 lds_barrier();
 #pragma unroll
                 for (int j = 0; j < RPW; ++j) {
-                    V[j][2] = lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
+                    V[j][2] = ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
 #pragma unroll
                     for (int i = K - 1; i > 0; --i) Rq[j][i] = Rq[j][i - 1];
-                    Rq[j][0] = lds4(rdr + (rr[j] - 1) * 256 + 4 * lane);
+                    Rq[j][0] = torhs(lds4(rdr + (rr[j] - 1) * 256 + 4 * lane));
+                    if constexpr (RHSW) {
+                        // the rhs of plane z for the later passes: owned planes and
+                        // rows only (so[j] = kOob elsewhere), every x of the row
+                        const bool own = z >= z0 && z < z1;
+                        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+                            a.rhs_out + (size_t)(own ? z : 0) * plane, (short)0,
+                            own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
+                        const gv4f rv = {Rq[j][0].x, Rq[j][0].y, Rq[j][0].z, Rq[j][0].w};
+                        __builtin_amdgcn_raw_buffer_store_b128(rv, ro, (int)so[j], 0, 0);
+                    }
                 }
                 // phase R: level l of plane p = z - l + 1
 #pragma unroll
@@ -427,7 +460,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
                                 const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
                                 const int y = y0 - K + r;
-                                v = level4<MODE, PRE>(c, wl, er, N, S, U, D, Rq[j][l - 1], x, nx,
+                                v = level4<MODE, PREL>(c, wl, er, N, S, U, D, Rq[j][l - 1], x, nx,
                                                       irow[j] && !fx, a,
                                                       (a.zoff + p + y + 1 + ((l - 1) & 1)) & 1,
                                                       orow[j] && p >= z0 && p < z1, chg[(l - 1) / 2]);
@@ -574,7 +607,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     } else {
         // the halo wave in its own (not inlined) function, so that its
         // registers are allocated apart from the row waves'
-        tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE>(a, smem, z0, z1, y0, xs);
+        tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F>(a, smem, z0, z1, y0, xs);
     }
     if (MODE == kRbgs && a.maxc) {
         __shared__ float red[NIT][NWR + 1];
@@ -624,9 +657,14 @@ void set_cu_reserve(int n) { g_cu_reserve = n; }
 // (2.48 ms per pass) beat 18-row tiles in 9 rounds of 103 planes (2.62 ms)
 // and in 5 rounds of 205 planes (2.79 ms); the model orders them the same.
 // Pick the shape and z-chunk (see above) and launch.
+// first: 0, or the kFirst* flags of a Jacobi first pass (K = 2, 3 auto shapes).
 template <int MODE>
-static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStream_t s) {
+static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStream_t s, int first = 0) {
     const int pd = jacobi3d_tb_prefetch();
+    if (first && (MODE != kJacobi || pre || pd != 1 || rows != 0 || (K != 2 && K != 3))) {
+        set_error("jacobi3d_tbr: a first pass needs Jacobi, raw div, prefetch 1, auto tiles, 2 or 3 levels");
+        return CFD_E_INVALID;
+    }
     const int L = a.ze - a.zb;
     const int nseg = ceil_div(a.nx, 256);
     const int ncu = tbr_cus();
@@ -675,18 +713,36 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
             if (pre) CFD_TBR_L(KV, NW, RP, true, 1); else CFD_TBR_L(KV, NW, RP, false, 1);      \
         }                                                                                     \
     } while (0)
+    // shapes with a first-pass variant (all on the LDS-DMA path)
+#define CFD_TBRF(KV, NW, RP)                                                                 \
+    do {                                                                                     \
+        if constexpr (MODE == kJacobi) {                                                     \
+            if (first == (kFirstRhs | kFirstZero)) {                                         \
+                hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, false, 1, MODE, kFirstRhs | kFirstZero>), \
+                                   dim3(blocks), dim3((NW + 1) * 64), 0, s, a);              \
+                break;                                                                       \
+            }                                                                                \
+            if (first == kFirstRhs) {                                                        \
+                hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, false, 1, MODE, kFirstRhs>),     \
+                                   dim3(blocks), dim3((NW + 1) * 64), 0, s, a);              \
+                break;                                                                       \
+            }                                                                                \
+        }                                                                                    \
+        CFD_TBR(KV, NW, RP);                                                                 \
+    } while (0)
     const int code = best->K * 100 + best->nwr * 10 + best->rpw;
     switch (code) {
-        case 3 * 100 + 11 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBR(3, 11, 2); break;
-        case 3 * 100 + 10 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBR(3, 10, 2); break;
+        case 3 * 100 + 11 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBRF(3, 11, 2); break;
+        case 3 * 100 + 10 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBRF(3, 10, 2); break;
         case 3 * 100 + 7 * 10 + 3: if constexpr (MODE == kJacobi) CFD_TBR(3, 7, 3); break;
         case 4 * 100 + 7 * 10 + 3: CFD_TBR(4, 7, 3); break;
         case 4 * 100 + 11 * 10 + 2: CFD_TBR(4, 11, 2); break;
-        case 2 * 100 + 11 * 10 + 2: CFD_TBR(2, 11, 2); break;
-        case 2 * 100 + 10 * 10 + 2: CFD_TBR(2, 10, 2); break;
-        case 2 * 100 + 9 * 10 + 2: CFD_TBR(2, 9, 2); break;
+        case 2 * 100 + 11 * 10 + 2: CFD_TBRF(2, 11, 2); break;
+        case 2 * 100 + 10 * 10 + 2: CFD_TBRF(2, 10, 2); break;
+        case 2 * 100 + 9 * 10 + 2: CFD_TBRF(2, 9, 2); break;
         default: CFD_TBR(2, 10, 3); break;
     }
+#undef CFD_TBRF
 #undef CFD_TBR
 #undef CFD_TBR_L
     CFD_LAUNCH_CHECK();
@@ -702,6 +758,20 @@ int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float 
     a.nz = nz; a.ny = ny; a.nx = nx; a.zb = zb; a.ze = ze;
     a.fixed_lo = fixed_lo; a.fixed_hi = fixed_hi; a.h2 = h2; a.dt = dt;
     return tbr_launch<kJacobi>(a, K, rows, zchunk, pre, s);
+}
+
+// The first pass of a solve (K = 2, 3): raw div in, f32(h*h)*div/dt of the
+// owned cells out to rhs_out for the later passes; zero != 0: level 0 is
+// phi = 0 and `out` is the only array of phi touched (any of the pair).
+int jacobi3d_tbr_first_pass(int K, float *out, const float *div, float *rhs_out, const float *in,
+                            int nz, int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi,
+                            float h2, float dt, int zchunk, bool zero, hipStream_t s) {
+    if (ze <= zb || ny < 3) return CFD_OK;
+    TbrArgs a{};
+    a.in = zero ? out : in; a.out = out; a.div = div; a.rhs_out = rhs_out;
+    a.nz = nz; a.ny = ny; a.nx = nx; a.zb = zb; a.ze = ze;
+    a.fixed_lo = fixed_lo; a.fixed_hi = fixed_hi; a.h2 = h2; a.dt = dt;
+    return tbr_launch<kJacobi>(a, K, 0, zchunk, false, s, kFirstRhs | (zero ? kFirstZero : 0));
 }
 
 // Red-black GS passes on tall tiles: `iters` (1 or 2) iterations from `it` on,

@@ -60,6 +60,37 @@ int launch_fix_faces3d(const float *src, float *dst, const uint8_t *mask, int ny
     return CFD_OK;
 }
 
+// Zero the Dirichlet faces the blocked passes never write (planes 0 and nz-1,
+// rows 0 and ny-1 of every plane) in both arrays of the ping-pong pair: the
+// boundary of phi = zeros (v5.py:337) for a solve that starts from zero.
+// This kernel does rows 0 and ny-1 of planes 1 .. nz-2 (grid-stride in y);
+// the two full planes are memsets.  float4: nx % 4 == 0, aligned arrays.
+__global__ void zero_rows3d(float *__restrict__ a, float *__restrict__ b, int nz, int ny, int nx) {
+    const size_t plane = (size_t)ny * nx;
+    const size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (4 * k >= 2 * (size_t)nx) return;
+    const size_t r = 4 * k < (size_t)nx ? 4 * k : (size_t)(ny - 2) * nx + 4 * k;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (size_t z = blockIdx.y + 1; z + 1 < (size_t)nz; z += gridDim.y) {
+        *reinterpret_cast<float4 *>(a + z * plane + r) = z4;
+        *reinterpret_cast<float4 *>(b + z * plane + r) = z4;
+    }
+}
+
+int launch_zero_faces3d(float *a, float *b, int nz, int ny, int nx, hipStream_t s) {
+    const size_t plane = (size_t)ny * nx;
+    for (float *p : {a, b}) {
+        CFD_CHECK_HIP(hipMemsetAsync(p, 0, plane * sizeof(float), s));
+        CFD_CHECK_HIP(hipMemsetAsync(p + (size_t)(nz - 1) * plane, 0, plane * sizeof(float), s));
+    }
+    if (nz > 2) {
+        hipLaunchKernelGGL(zero_rows3d, dim3(ceil_div(2 * nx / 4, 256), nz - 2 < 4096 ? nz - 2 : 4096),
+                           dim3(256), 0, s, a, b, nz, ny, nx);
+        CFD_LAUNCH_CHECK();
+    }
+    return CFD_OK;
+}
+
 // Jacobi sweeps per pass when tb_steps == 0 (r01 sweep at 1024^3: K=2 855,
 // K=3 1010-1030, K=4 1000 Gcell/s)
 constexpr int kDefaultLevels = 3;
@@ -477,6 +508,57 @@ int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, 
                              fixed_lo, fixed_hi, h2, dt, zc, pre, s);
 }
 
+// Whether a solve can start with a fused first pass (jacobi3d_tbr_first_pass:
+// the RHS workspace formed by the pass itself, and, from zero, no phi read):
+// the blocked path, a workspace, the LDS-DMA kernel (prefetch 1).
+static bool jacobi3d_first_ok(const float *rhs_ws, bool vec_ok, int nz, int ny, int iters) {
+    return rhs_ws && vec_ok && jacobi3d_tb_enabled() && jacobi3d_tb_prefetch() == 1 && nz >= 3 &&
+           ny >= 3 && iters >= 2 && aligned16(rhs_ws);
+}
+
+// The blocked solve with a fused first pass of k1 = 2 or 3 sweeps (k1 =
+// iters mod K when that is 2 or 3, so the passes of K that follow need no
+// shorter remainder pass), then passes of K, any remainder last.  zero: phi
+// starts as zeros (its boundary ring zeroed here in both arrays; nothing of
+// phi is read), and the first pass writes the array that makes the last
+// pass land in phi -- no zero fill, no RHS prologue, no final copy.  Else phi
+// holds the initial guess (faces copied to phi_tmp, the first pass reads phi).
+static int jacobi3d_blocked_solve(const float *div, float *phi, float *phi_tmp, float *rhs_ws,
+                                  int nz, int ny, int nx, float h2, float dt, int iters, bool zero,
+                                  hipStream_t s) {
+    int rc;
+    const int K = jacobi3d_tb_levels();
+    const int r = iters % K;
+    int k1 = (r == 2 || r == 3) ? r : (K < 3 ? K : 3);
+    if (k1 > iters) k1 = iters;
+    const int rest = iters - k1;
+    const int npass = 1 + (rest + K - 1) / K;
+    float *first_out = zero && npass % 2 == 1 ? phi : phi_tmp;
+    if (zero) {
+        if ((rc = launch_zero_faces3d(phi, phi_tmp, nz, ny, nx, s))) return rc;
+    } else if ((rc = launch_fix_faces3d(phi, phi_tmp, nullptr, ny, nx, 0, nz, 0, nz - 1, s))) {
+        return rc;
+    }
+    const int tk = timing_begin(s);
+    if ((rc = jacobi3d_tbr_first_pass(k1, first_out, div, rhs_ws, phi, nz, ny, nx, 1, nz - 1, 1, 1, h2,
+                                      dt, tuning().tb_zchunk, zero, s)))
+        return rc;
+    float *a = first_out, *b = first_out == phi ? phi_tmp : phi;
+    for (int done = k1; done < iters;) {
+        const int k = iters - done < K ? iters - done : K;
+        if ((rc = jacobi3d_blocked_pass(k, a, b, rhs_ws, nz, ny, nx, 1, nz - 1, 1, 1, h2, dt, true, s)))
+            return rc;
+        done += k;
+        float *t = a;
+        a = b;
+        b = t;
+    }
+    timing_end(tk, s, iters);
+    if (a != phi)
+        CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(float) * (size_t)nz * ny * nx, hipMemcpyDeviceToDevice, s));
+    return CFD_OK;
+}
+
 }  // namespace cfd
 
 using namespace cfd;
@@ -534,6 +616,10 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
     hipStream_t s = as_stream(stream);
     const size_t plane = (size_t)ny * nx;
     int rc;
+    const bool vec_ok0 = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(div);
+    if (!mask && resid_every <= 0 && jacobi3d_first_ok(rhs_ws, vec_ok0, nz, ny, iters))
+        return jacobi3d_blocked_solve(div, phi, phi_tmp, rhs_ws, nz, ny, nx, (float)(h * h), dt, iters,
+                                      false, s);
     // Dirichlet faces the sweep never writes (planes 0, nz-1; rows 0, ny-1)
     if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, 0, nz, 0, nz - 1, s))) return rc;
     const int nres = resid_every > 0 ? iters / resid_every : 0;
@@ -586,6 +672,21 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
     if (a != phi)
         CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(float) * plane * nz, hipMemcpyDeviceToDevice, s));
     return CFD_OK;
+}
+
+int cfd_jacobi3d_zero_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws, int nz,
+                          int ny, int nx, double h, float dt, int iters, void *stream) {
+    CFD_REQUIRE(div && phi && phi_tmp, "jacobi3d_zero: null array pointer");
+    CFD_REQUIRE(nz >= 1 && ny >= 1 && nx >= 1 && iters >= 0, "jacobi3d_zero: bad arguments");
+    hipStream_t s = as_stream(stream);
+    const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(div);
+    if (jacobi3d_first_ok(rhs_ws, vec_ok, nz, ny, iters))
+        return jacobi3d_blocked_solve(div, phi, phi_tmp, rhs_ws, nz, ny, nx, (float)(h * h), dt, iters,
+                                      true, s);
+    // other layouts: the zero fill, then the general solve
+    CFD_CHECK_HIP(hipMemsetAsync(phi, 0, sizeof(float) * (size_t)nz * ny * nx, s));
+    return cfd_jacobi3d_f32(div, phi, phi_tmp, rhs_ws, nullptr, nz, ny, nx, h, dt, iters, 0, nullptr,
+                            stream);
 }
 
 int cfd_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask, int nz, int ny, int nx,

@@ -21,6 +21,7 @@ __all__ = [
     "compute_laplacian_fast", "compute_divergence_fast", "compute_gradient_fast",
     "solve_pressure_gauss_seidel_fast", "solve_pressure_jacobi", "apply_ibm_fast",
     "clean_divergence_fast", "predictor_fused", "project_velocity", "solve_pressure_jacobi3d",
+    "solve_pressure_jacobi3d_zero",
     "solve_pressure_gauss_seidel3d",
 ]
 
@@ -160,6 +161,23 @@ def solve_pressure_jacobi3d(phi, div, h, dt, mask, iterations, phi_tmp=None, res
     call("cfd_jacobi3d_f32", ptr(_f32(div, "div")), ptr(_f32(phi, "phi")), ptr(tmp), ptr(rhs_ws), ptr(m),
          nz, ny, nx, float(h), float(np.float32(dt)), int(iterations), int(resid_every), ptr(resid_out),
          stream_handle())
+    return phi
+
+
+def solve_pressure_jacobi3d_zero(phi, div, h, dt, iterations, phi_tmp=None, rhs_ws=None):
+    """The Jacobi branch of solve_pressure_fast in 3-D, zero fill included
+    (v5.py:337-346): phi = zeros, then `iterations` sweeps.  With ``rhs_ws``
+    the first pass starts from the zeros itself (no fill, no RHS prologue, no
+    final copy; cfd_jacobi3d_zero_f32).  Returns phi."""
+    if phi.dim() != 3:
+        raise ValueError("expected (nz, ny, nx)")
+    nz, ny, nx = (int(s) for s in phi.shape)
+    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
+    for t, name in ((tmp, "phi_tmp"), (rhs_ws, "rhs_ws")):
+        if t is not None and (t.shape != phi.shape or t.dtype != torch.float32 or not t.is_contiguous()):
+            raise ValueError(f"{name} must be a contiguous float32 array of phi's shape")
+    call("cfd_jacobi3d_zero_f32", ptr(_f32(div, "div")), ptr(_f32(phi, "phi")), ptr(tmp), ptr(rhs_ws),
+         nz, ny, nx, float(h), float(np.float32(dt)), int(iterations), stream_handle())
     return phi
 
 

@@ -91,6 +91,16 @@ int cfd_jacobi3d_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws
                      const uint8_t *mask, int nz, int ny, int nx, double h, float dt, int iters,
                      int resid_every, float *resid_out, void *stream);
 
+/* The whole Jacobi branch of solve_pressure_fast in 3-D, v5.py:337-346:
+ * phi = zeros (v5.py:337), then iters sweeps of cfd_jacobi3d_f32 -- the same
+ * bits as a zero fill followed by cfd_jacobi3d_f32.  With rhs_ws (and nx % 4
+ * == 0, 16-byte aligned arrays, blocking on) the first pass starts from the
+ * zeros without reading phi, forms rhs_ws itself, and writes the array that
+ * makes the last pass land in phi: no fill, no RHS prologue, no final copy.
+ * phi's prior contents are ignored; phi_tmp is scratch. */
+int cfd_jacobi3d_zero_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws, int nz,
+                          int ny, int nx, double h, float dt, int iters, void *stream);
+
 /* Replaces solve_pressure_gauss_seidel_fast, v5.py:202-226 (the
  * use_fast_pressure=True branch, v5.py:330-335): red-black Gauss-Seidel in
  * place on phi; colour 0 = cells with (i+j) odd first; masked cells skipped;

@@ -248,3 +248,71 @@ def test_jacobi2d_small_shapes_bitexact(k, rw, vec):
     phi = torch.zeros_like(dev(div))
     K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), dev(mask), 37)
     assert np.array_equal(host(phi), ref)
+
+
+# ------------------------------------------- zero-start solve, fused first pass
+def test_jacobi3d_1024_zero_start_bitexact(div1024):
+    """cfd_jacobi3d_zero_f32 at the bench geometry: phi = zeros then 2..6 and
+    200 sweeps (the bench's step: a fused 2-sweep first pass that starts from
+    the zeros and forms the RHS workspace, then 66 passes of 3).  phi and the
+    workspace start as NaN garbage: the first pass must read neither."""
+    n = 1024
+    h, dt = 1.0 / (n - 1), np.float32(5e-5)
+    refs = {}
+    ref = np.zeros_like(div1024)
+    for it in range(1, 7):
+        ref = oracle.jacobi3d(div1024, ref, h=h, dt=dt, iters=1, mt=True)
+        refs[it] = ref
+    d = dev(div1024)
+    phi = torch.empty_like(d)
+    tmp = torch.empty_like(d)
+    rhs = torch.empty_like(d)
+    for iters in (2, 3, 4, 5, 6):
+        phi.fill_(float("nan"))
+        tmp.fill_(float("nan"))
+        rhs.fill_(float("nan"))
+        K.solve_pressure_jacobi3d_zero(phi, d, h, dt, iters, phi_tmp=tmp, rhs_ws=rhs)
+        assert np.array_equal(host(phi), refs[iters]), iters
+    del refs, ref
+    # the bench step itself: 200 sweeps, vs the general path (pinned above) on the same inputs
+    phi.fill_(float("nan"))
+    K.solve_pressure_jacobi3d_zero(phi, d, h, dt, 200, phi_tmp=tmp, rhs_ws=rhs)
+    want = torch.zeros_like(d)
+    K.solve_pressure_jacobi3d(want, d, h, dt, None, 200, phi_tmp=tmp, rhs_ws=None)
+    torch.cuda.synchronize()
+    assert torch.equal(phi, want)
+
+
+@pytest.mark.parametrize("levels", [0, 2, 4])
+@pytest.mark.parametrize("shape", [(17, 19, 260), (6, 40, 8), (3, 3, 4), (40, 5, 516)])
+def test_jacobi3d_zero_start_ragged_bitexact(levels, shape):
+    """Zero-start solves on ragged grids (two x-segments, y and z not tile
+    multiples, minimal 3-plane grids), every sweep count 1..10 (first passes
+    of 2 and 3, remainders of 1 and 2, both result parities), blocking depth
+    auto / 2 / 4, with and without the RHS workspace."""
+    call("cfd_set_jacobi3d_blocking", levels, 0, 0)
+    rng = np.random.default_rng(sum(shape))
+    div = rng.standard_normal(shape).astype(np.float32)
+    d = dev(div)
+    ref = np.zeros_like(div)
+    for iters in range(1, 11):
+        ref = oracle.jacobi3d(div, ref, h=0.03, dt=np.float32(1e-3), iters=1)
+        for rhs in (torch.full_like(d, float("nan")), None):
+            phi = torch.full_like(d, float("nan"))
+            tmp = torch.full_like(d, float("nan"))
+            K.solve_pressure_jacobi3d_zero(phi, d, 0.03, np.float32(1e-3), iters, phi_tmp=tmp, rhs_ws=rhs)
+            assert np.array_equal(host(phi), ref), (iters, rhs is None)
+
+
+def test_jacobi3d_first_pass_general_start_bitexact():
+    """The general solve with a workspace now forms it in its first pass (no
+    RHS prologue) from a non-zero initial guess: still the oracle's bits."""
+    rng = np.random.default_rng(5)
+    div = rng.standard_normal((21, 35, 264)).astype(np.float32)
+    phi0 = rng.standard_normal(div.shape).astype(np.float32)
+    for iters in (2, 3, 5, 7):
+        ref = oracle.jacobi3d(div, phi0, h=0.05, dt=np.float32(2e-3), iters=iters)
+        phi = dev(phi0)
+        rhs = torch.full_like(phi, float("nan"))
+        K.solve_pressure_jacobi3d(phi, dev(div), 0.05, np.float32(2e-3), None, iters, rhs_ws=rhs)
+        assert np.array_equal(host(phi), ref), iters
