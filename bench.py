@@ -19,6 +19,12 @@ stream around its launches.  `cpu_baseline` times the NumPy restatement of the
 reference's Jacobi branch (oracle/, bit-exact to v5.py:336-346) on a bounded
 sample of the same grid, on this host, at N=1 only.
 
+`--workload cavity2d_128` is config 1: the whole projection step of the
+lid-driven cavity (128^2, Re = 100, 500 Jacobi sweeps per pressure solve) per
+step; `value` counts the pressure cell-updates over the step's wall time, and
+the CPU baseline is the same step on the host (oracle.OracleCavitySolver with
+the reference's NumPy Jacobi form).
+
 `--workload rbgs3d_1024` is config 5: red-black Gauss-Seidel (the 3-D
 generalisation of v5.py:202-226) on the 1024^3 grid, one step = zero-fill +
 200 iterations at the reference's tolerance 1e-8 (stop rule evaluated on device
@@ -50,6 +56,9 @@ WORKLOADS = {
     "jacobi3d_channel": ((512, 1024, 1024), "f32", 200, 12),
     "jacobi2d_8192_f64": ((8192, 8192), "f64", 1000, 24),
     "rbgs3d_1024": ((1024, 1024, 1024), "f32", 200, 12),
+    # config 1: lid-driven cavity 128^2, Re = 100, 500 Jacobi sweeps per pressure
+    # solve; one step = one LidDrivenCavitySolver.time_step() (v5.py:375-441)
+    "cavity2d_128": ((128, 128), "f32", 500, 12),
 }
 GS_TOL = 1e-8  # OptimizedTurbulentConfig.pressure_tolerance (v5.py)
 
@@ -141,9 +150,78 @@ def cpu_baseline(shape, iters_total_hint, gs=False):
             "sample": desc + f"; {t:.2f} s; host has {os.cpu_count()} logical CPUs, NumPy uses 1"}
 
 
+def cavity_bench():
+    """Config 1 (single GPU): LidDrivenCavitySolver.time_step() repeated; the
+    pressure solve is the small-grid 2-D Jacobi kernel (4 sweeps per launch),
+    latency-bound at 128^2 (a pass moves 190 KB)."""
+    import torch
+    import _pkgpath
+    _pkgpath.load()
+    import oracle
+    from cfd_simulations_amd._lib import call
+    from cfd_simulations_amd.solver import LidDrivenCavityConfig, LidDrivenCavitySolver
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("the cavity workload (config 1) is single-GPU")
+    cfg = LidDrivenCavityConfig()
+    g = LidDrivenCavitySolver(cfg)
+    for _ in range(ARGS.warmup):
+        g.time_step()
+    torch.cuda.synchronize()
+    call("cfd_timing_enable", 1)
+    t0 = time.perf_counter()
+    for _ in range(ARGS.steps):
+        g.time_step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = ctypes.c_double()
+    nsw = ctypes.c_longlong()
+    call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(nsw), 1)
+    call("cfd_timing_enable", 0)
+    ny, nx = cfg.ny, cfg.nx
+    cells = (ny - 2) * (nx - 2)
+    iters = cfg.pressure_iterations
+    spl = 4  # jacobi2d_small: 4 sweeps per launch (Tuning::j2s_k)
+    launch_ms = ms.value / max(nsw.value, 1) * spl
+    alg = cells * 12
+    achieved = alg / (launch_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC, "value": round(cells * iters * ARGS.steps / elapsed / 1e9, 3),
+        "unit": "Gcell-updates/s", "n_gpus": 1, "steps": ARGS.steps, "warmup": ARGS.warmup,
+        "ms_per_step": round(elapsed / ARGS.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: lid-driven cavity from rest, lid u = 1 (no dataset)",
+        "config": {"workload": "cavity2d_128x128_re100_jacobi500", "grid": [ny, nx], "iters_per_step": iters,
+                   "step": "LidDrivenCavitySolver.time_step (predictor, BC, divergence, 500 Jacobi sweeps, "
+                           "projection, divergence cleaning, energy)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel": "jacobi2d_small<float, 1, 4> (latency-bound: 190 KB per pass)",
+                     "sweeps_per_launch": spl, "cells_per_launch": cells, "algorithmic_bytes_per_launch": alg,
+                     "avg_launch_ms": round(launch_ms, 5)},
+        "cpu_baseline": None,
+    }
+    if not ARGS.no_cpu_baseline:
+        o = oracle.OracleCavitySolver(cfg, numpy_jacobi=True)
+        n = 0
+        t0 = time.perf_counter()
+        while n < 10 or (time.perf_counter() - t0 < 5.0 and n < 400):
+            o.time_step()
+            n += 1
+        t = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": cells * iters * n / t / 1e9, "unit": "Gcell-updates/s", "cores": 1,
+                               "kind": "port", "ms_per_step": round(t / n * 1e3, 3),
+                               "sample": f"{n} steps of OracleCavitySolver(numpy_jacobi=True).time_step() "
+                                         f"(the same step, pressure in the reference's NumPy Jacobi form, "
+                                         f"v5.py:336-346); {t:.2f} s; NumPy uses 1 of {os.cpu_count()} "
+                                         f"logical CPUs"}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     global ARGS
     ARGS = parse()
+    if ARGS.workload == "cavity2d_128":
+        return cavity_bench()
     import torch
     import torch.distributed as dist
     import _pkgpath
