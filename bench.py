@@ -379,7 +379,12 @@ def main():
     levels = int(lib().cfd_get_jacobi3d_levels() if len(shape) == 3 else lib().cfd_get_jacobi2d_levels())
     # sweeps per launch: K Jacobi sweeps per blocked pass; the GS timing
     # counts iterations, and a fused GS pass is one (two with --tb 4)
-    spl = levels if blocked and not gs else (2 if gs and blocked and ARGS.tb == 4 else 1)
+    if not gs:
+        spl = levels if blocked else 1
+    elif use_slab:  # slab passes: one iteration, two with --tb 4
+        spl = 2 if blocked and ARGS.tb == 4 else 1
+    else:  # single GPU: --tb half-sweeps per pass (auto 3: one and a half iterations)
+        spl = (ARGS.tb if ARGS.tb >= 2 else 3) / 2 if blocked else 1
     launch_ms = sweep_ms * spl
     alg_bytes = cells_rank * bpc  # one pass moves bpc bytes per cell whatever it fuses
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
@@ -408,7 +413,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
                      "kernel": (("jacobi3d_tb2<MODE_RBGS>" if ARGS.tb_rows in (5, 13) else
-                                 f"jacobi3d_tbr<{2 * spl}, MODE_RBGS>") if blocked else "rbgs3d_color x2") if gs
+                                 f"jacobi3d_tbr<{int(2 * spl)}, MODE_RBGS>") if blocked else "rbgs3d_color x2") if gs
                      else (blocked_kernel_name(levels, ARGS.tb_rows) if blocked
                            else "jacobi3d_march") if len(shape) == 3
                      else (f"jacobi2d_tbk<{levels}>" if blocked else "jacobi2d_march"),

@@ -62,9 +62,11 @@ int jacobi3d_tbr_first_pass(int K, float *out, const float *div, float *rhs_out,
 // red-black GS workspace (declared below) passes on tall tiles
 struct RbgsWs;
 struct RbgsConsts;
+// (levels half-sweeps from half-sweep h0; rollback = half-sweeps per pass of
+// the solve, nhalf = its half-sweeps in all: see jacobi3d_tbr.hip)
 int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
-                    int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
-                    int iters, RbgsWs *ws, int rollback, int npairs, int rows, hipStream_t s,
+                    int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int h0,
+                    int levels, RbgsWs *ws, int rollback, int nhalf, int rows, hipStream_t s,
                     int lag = 0);
 // red-black GS workspace (cfd_rbgs_workspace_bytes): flags[0] = iterations,
 // flags[1] = iterations done, flags[2] = tolerance (float bits), float
@@ -78,8 +80,9 @@ struct RbgsWs {
 int launch_rbgs_init(RbgsWs *ws, int iterations, float tol, int *iters_done, hipStream_t s);
 // iterations done (flags[1], *iters_done) from the per-iteration maxima
 int launch_rbgs_count(RbgsWs *ws, int *iters_done, hipStream_t s);
-// phi <- phi_tmp when ceil(done / per_pass) is odd (phi_tmp NULL: nothing)
-int launch_rbgs_copy(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n, int per_pass,
+// phi <- phi_tmp when ceil(2 done / half_per_pass) is odd, i.e. when the pass
+// that completed the last iteration wrote phi_tmp (phi_tmp NULL: nothing)
+int launch_rbgs_copy(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n, int half_per_pass,
                      hipStream_t s);
 // after fused (out-of-place) iterations: phi <- phi_tmp when an odd number
 // ran, and *iters_done <- the count (both read on device: no host sync)
@@ -98,10 +101,14 @@ bool rbgs3d_fused_ok(const float *phi, const float *phi_tmp, const float *div, c
 int rbgs3d_colour_pass(int colour, float *phi, const float *div, const uint8_t *mask, int ny,
                        int nx, int z0, int z1, int zoff, const RbgsConsts &k, RbgsWs *ws, int it,
                        hipStream_t s);
-int rbgs3d_iters_per_pass();  // 1, or 2 (blocking depth 4)
+int rbgs3d_iters_per_pass();  // slab solves: 1, or 2 (blocking depth 4)
+int rbgs3d_half_per_pass();   // single-GPU solves: half-sweeps per pass, 2..4 (auto 3)
 int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
                       int iters, RbgsWs *ws, hipStream_t s, int lag = 0);
+int rbgs3d_half_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
+                     int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int h0,
+                     int levels, RbgsWs *ws, hipStream_t s, int lag);
 // one fused iteration (both colours) of planes [zb, ze) of `out` from `in`;
 // max|change| into ws->maxc[it], stop counter ws->flags[1]
 int rbgs3d_tb_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,

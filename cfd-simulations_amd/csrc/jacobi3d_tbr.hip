@@ -72,10 +72,10 @@ struct TbrArgs {
     float h2, dt;                      // Jacobi
     float cx, cy, cz, cd, dt_inv, tol; // red-black GS
     int zoff;        // global z of local plane 0 (colour parity)
-    int it;          // first GS iteration of this pass
+    int h0;          // GS: first half-sweep of this pass (iteration h0 / 2, colour h0 & 1)
     float *maxc;     // per-iteration max|change| (device), NULL: not accumulated
-    int rollback;    // GS: the conditional re-run of one iteration (see rbgs3d_rollback)
-    int npairs;      // GS rollback: pair passes the solve scheduled
+    int rollback;    // GS: 0, or the half-sweeps per pass P of the solve whose stop this undoes
+    int nhalf;       // GS rollback: half-sweeps the solve scheduled (2 x iterations)
     const int *count;  // GS rollback: iterations done (device)
     int lag;         // GS: the stop test reads maxc[it-1-lag], maxc[it-2-lag] (see rbgs3d_tbr_pass)
     float *rhs_out;  // first pass (F & kFirstRhs): the rhs of the owned cells goes here
@@ -98,30 +98,32 @@ __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S
                                 int par, bool own, float &chg) {
     if (!upd) return c;
     if (MODE == kRbgs) {
-        const float cv[4] = {c.x, c.y, c.z, c.w};
-        const float nv[4] = {N.x, N.y, N.z, N.w};
-        const float sv[4] = {S.x, S.y, S.z, S.w};
-        const float uv[4] = {U.x, U.y, U.z, U.w};
-        const float dv[4] = {D.x, D.y, D.z, D.w};
-        const float rv[4] = {d.x, d.y, d.z, d.w};
-        float o[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float E = k < 3 ? cv[k + 1] : er;
-            const float Wv = k > 0 ? cv[k - 1] : wl;
-            const int xk = x + k;
-            o[k] = cv[k];
-            if (xk != 0 && xk != nx - 1 && ((par + xk) & 1) == 0) {
-                const float rhs = -rv[k] * a.dt_inv;
-                const float p = a.cx * (E + Wv);
-                const float q = a.cy * (nv[k] + sv[k]);
-                const float r = a.cz * (uv[k] + dv[k]);
-                o[k] = (((p + q) + r) - rhs) * a.cd;
-                const float ch = fabsf(o[k] - cv[k]);
-                if (own && ch > chg) chg = ch;
+        // x % 4 == 0, so the colour updates cells k = par & 1 and k + 2 of the
+        // float4 (par is uniform over a row): those two only, as one float2
+        // pair through packed math, in the in-place kernel's operation order
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        auto pair = [&](v2f C, v2f E, v2f Wv, v2f Nv, v2f Sv, v2f Uv, v2f Dv, v2f Rv, int x0) {
+            const v2f rhs = -Rv * a.dt_inv;
+            const v2f p = a.cx * (E + Wv);
+            const v2f q = a.cy * (Nv + Sv);
+            const v2f r = a.cz * (Uv + Dv);
+            v2f o = (((p + q) + r) - rhs) * a.cd;
+            o.x = (x0 != 0 && x0 != nx - 1) ? o.x : C.x;  // the pair's cells x0, x0 + 2 >= 2
+            o.y = (x0 + 2 != nx - 1) ? o.y : C.y;
+            if (own) {  // fmaxf ignores a NaN change like the `ch > mx` test
+                chg = fmaxf(chg, fabsf(o.x - C.x));
+                chg = fmaxf(chg, fabsf(o.y - C.y));
             }
+            return o;
+        };
+        if (par & 1) {  // row-uniform: a scalar branch, no per-element selects
+            const v2f o = pair(v2f{c.y, c.w}, v2f{c.z, er}, v2f{c.x, c.z}, v2f{N.y, N.w}, v2f{S.y, S.w},
+                               v2f{U.y, U.w}, v2f{D.y, D.w}, v2f{d.y, d.w}, x + 1);
+            return make_float4(c.x, o.x, c.z, o.y);
         }
-        return make_float4(o[0], o[1], o[2], o[3]);
+        const v2f o = pair(v2f{c.x, c.z}, v2f{c.y, c.w}, v2f{wl, c.y}, v2f{N.x, N.z}, v2f{S.x, S.z},
+                           v2f{U.x, U.z}, v2f{D.x, D.z}, v2f{d.x, d.z}, x);
+        return make_float4(o.x, c.y, o.y, c.w);
     }
     const float h2 = a.h2, dt = a.dt;
     const float cv[4] = {c.x, c.y, c.z, c.w};
@@ -241,7 +243,7 @@ __device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0,
                     v = level4<MODE, PRE>(c, side ? inner : 0.f, side ? 0.f : inner, N, S,
                                           H[l - 1][2], H[l - 1][0], Hr[l - 1], hx, nx,
                                           hint && !fixedp(p), a,
-                                          (a.zoff + p + yr + 1 + ((l - 1) & 1)) & 1, false, dummy);
+                                          (a.zoff + p + yr + 1 + ((a.h0 + l - 1) & 1)) & 1, false, dummy);
                 }
                 H[l][0] = H[l][1];
                 H[l][1] = H[l][2];
@@ -269,14 +271,15 @@ __device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0,
 
 // (A double-buffered, one-barrier-per-step version of the (3, 11, 2) shape --
 // 139 KB of LDS -- was measured at 1007 against 1131 Gcell/s for this one.)
-// MODE kRbgs: K/2 red-black iterations per pass (level l = colour (l-1)&1);
-// see rbgs3d_tbr_pass for the stop rule and the rollback.
+// MODE kRbgs: K red-black half-sweeps per pass, level l = half-sweep h0+l-1
+// (colour (h0+l-1) & 1, iteration (h0+l-1) / 2), so a pass may start or end
+// inside an iteration; see rbgs3d_tbr_pass for the stop rule and the rollback.
 template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F = 0>
 __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     constexpr int NR = NWR * RPW + 2;  // level-0 rows per tile
     constexpr int W = NR - 2 * K;      // output rows
     constexpr int RS = 264;            // LDS row: 4 halo | 256 | 4 halo floats
-    static_assert(K >= 2 && K <= 4 && W >= 1, "bad shape");
+    static_assert(K >= 1 && K <= 4 && W >= 1, "bad shape");
     static_assert(2 * NR <= 64, "halo wave: one lane per (row, side)");
     constexpr int TOTAL = [] {
         int t = 0;
@@ -303,7 +306,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         return smem + base + (r - l) * RS;
     };
 
-    static_assert(MODE == kJacobi || (K % 2 == 0 && !PRE), "GS: whole iterations, raw div");
+    static_assert(MODE == kJacobi || !PRE, "GS: raw div");
     static_assert(F == 0 || (MODE == kJacobi && !PRE && DMA), "first pass: Jacobi, raw div, DMA path");
     constexpr bool ZERO = (F & kFirstZero) != 0, RHSW = (F & kFirstRhs) != 0;
     constexpr bool PREL = PRE || RHSW;  // the row waves' queues hold the rhs
@@ -317,27 +320,37 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         }
         return d;
     };
-    constexpr int NIT = MODE == kRbgs ? K / 2 : 1;  // GS iterations per pass
+    // GS iterations a pass touches: (h0 >> 1) + q, q < NIT (K = 3: one and a half)
+    constexpr int NIT = MODE == kRbgs ? (K + 2) / 2 : 1;
     if (MODE == kRbgs) {
         if (a.rollback) {
-            // re-run iteration 2m' alone when the stop fell after the first
-            // iteration of pair pass m' (whose output holds one too many)
-            const int c = *a.count;
-            if (!((c & 1) && (c - 1) / 2 < a.npairs)) return;
-            if (((c - 1) / 2) & 1) {
+            // The stop fell inside pass j* of a solve of P half-sweeps per pass
+            // when the 2c half-sweeps of its c iterations end inside it: re-run
+            // those of its half-sweeps that count (need = 2c - P j*) from the
+            // pass's input buffer, which no later (skipped) pass overwrote, into
+            // its output.  One launch per possible need; this one does K.
+            const int P = a.rollback, H = 2 * *a.count;
+            const int js = (H - 1) / P, need = H - P * js;
+            if (need != K || need >= P || P * js + P > a.nhalf) return;
+            a.h0 = P * js;
+            if (js & 1) {  // pass j* read phi_tmp
                 float *t_ = const_cast<float *>(a.in);
                 a.in = a.out;
                 a.out = t_;
             }
         } else {
-            const int d = 1 + a.lag;
-            if ((a.it >= d && a.maxc[a.it - d] < a.tol) || (a.it >= d + 1 && a.maxc[a.it - d - 1] < a.tol))
-                return;  // an earlier iteration met the tolerance (v5.py:224-225)
+            // skip when an iteration the previous pass completed met the
+            // tolerance (v5.py:224-225); with a lag, the pass before that
+            const int ic = a.h0 >> 1, d = 1 + a.lag;
+            if ((ic >= d && a.maxc[ic - d] < a.tol) || (ic >= d + 1 && a.maxc[ic - d - 1] < a.tol))
+                return;
         }
     }
     const int nz = a.nz, ny = a.ny, nx = a.nx;
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+    // wave index, uniform by construction: rows, row masks and colours derived
+    // from it stay scalar
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int t = xcd_swizzle(blockIdx.x, gridDim.x);
     const int seg = t % a.nseg;
     const int ty = (t / a.nseg) % a.ntile_y;
@@ -355,9 +368,18 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float chg[NIT];  // GS: max|change| of own cells per iteration
+    float chg[NIT];  // GS: max|change| of own cells per iteration (h0 >> 1) + q
 #pragma unroll
     for (int i = 0; i < NIT; ++i) chg[i] = 0.f;
+    // fold a level's max|change| into its iteration's slot: level l is
+    // iteration (h0 >> 1) + q(l), q(l) = ((h0 & 1) + l - 1) >> 1
+    auto fold = [&](int l, float lm) {
+        if constexpr (MODE == kRbgs) {
+            const int q = ((a.h0 & 1) + l - 1) >> 1;
+#pragma unroll
+            for (int i = 0; i < NIT; ++i) chg[i] = q == i ? fmaxf(chg[i], lm) : chg[i];
+        }
+    };
 
     if (wv < NWR) {
         if constexpr (DMA) {
@@ -460,10 +482,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
                                 const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
                                 const int y = y0 - K + r;
+                                float lm = 0.f;
                                 v = level4<MODE, PREL>(c, wl, er, N, S, U, D, Rq[j][l - 1], x, nx,
                                                       irow[j] && !fx, a,
-                                                      (a.zoff + p + y + 1 + ((l - 1) & 1)) & 1,
-                                                      orow[j] && p >= z0 && p < z1, chg[(l - 1) / 2]);
+                                                      (a.zoff + p + y + 1 + ((a.h0 + l - 1) & 1)) & 1,
+                                                      orow[j] && p >= z0 && p < z1, lm);
+                                fold(l, lm);
                             }
                             if (l < K) {
                                 Q[j][l][0] = Q[j][l][1];
@@ -572,10 +596,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
                                 const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
                                 const int y = y0 - K + r;
+                                float lm = 0.f;
                                 v = level4<MODE, PRE>(c, wl, er, N, S, Q[j][l - 1][2], Q[j][l - 1][0],
                                                       Rq[j][l - 1], x, nx, irow[j] && !fx, a,
-                                                      (a.zoff + p + y + 1 + ((l - 1) & 1)) & 1,
-                                                      orow[j] && p >= z0 && p < z1, chg[(l - 1) / 2]);
+                                                      (a.zoff + p + y + 1 + ((a.h0 + l - 1) & 1)) & 1,
+                                                      orow[j] && p >= z0 && p < z1, lm);
+                                fold(l, lm);
                             }
                             if (l < K) {
                                 Q[j][l][0] = Q[j][l][1];
@@ -612,7 +638,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     if (MODE == kRbgs && a.maxc) {
         __shared__ float red[NIT][NWR + 1];
 #pragma unroll
-        for (int i = 0; i < NIT; ++i) block_reduce_max_store(chg[i], a.maxc + a.it + i, red[i]);
+        for (int i = 0; i < NIT; ++i)  // the iterations this pass touched (workgroup-uniform)
+            if ((a.h0 >> 1) + i <= (a.h0 + K - 1) >> 1)
+                block_reduce_max_store(chg[i], a.maxc + (a.h0 >> 1) + i, red[i]);
     }
 }
 
@@ -628,9 +656,11 @@ struct TbrShape {
 // 1024^3: 20 rows 2.48 ms, 18 rows 2.51 ms, 28 rows 2.60 ms per iteration.
 // (2, 9, 2): 16-row GS tiles, 256 workgroups at 1024^2 -- one full round;
 // (2, 10, 2): 18-row, 228 workgroups, for the 240 CUs of a partitioned slab.
+// K = 3 shapes also serve the red-black GS (three half-sweeps, 1.5 iterations,
+// per pass: the r02 default); K = 1 only its rollback of one half-sweep.
 constexpr TbrShape kShapes[] = {{3, 11, 2, true}, {3, 10, 2, true}, {3, 7, 3, false},
-                                {4, 7, 3, true}, {4, 11, 2, false}, {2, 11, 2, true},
-                                {2, 10, 2, true}, {2, 10, 3, false}, {2, 9, 2, true}};
+                                {4, 7, 3, true}, {4, 11, 2, false}, {4, 10, 2, false}, {2, 11, 2, true},
+                                {2, 10, 2, true}, {2, 10, 3, false}, {2, 9, 2, true}, {1, 9, 2, true}};
 
 int num_cus() {
     static int n = 0;
@@ -732,11 +762,13 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
     } while (0)
     const int code = best->K * 100 + best->nwr * 10 + best->rpw;
     switch (code) {
-        case 3 * 100 + 11 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBRF(3, 11, 2); break;
-        case 3 * 100 + 10 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBRF(3, 10, 2); break;
+        case 3 * 100 + 11 * 10 + 2: CFD_TBRF(3, 11, 2); break;
+        case 3 * 100 + 10 * 10 + 2: CFD_TBRF(3, 10, 2); break;
+        case 1 * 100 + 9 * 10 + 2: if constexpr (MODE == kRbgs) CFD_TBR(1, 9, 2); break;
         case 3 * 100 + 7 * 10 + 3: if constexpr (MODE == kJacobi) CFD_TBR(3, 7, 3); break;
         case 4 * 100 + 7 * 10 + 3: CFD_TBR(4, 7, 3); break;
         case 4 * 100 + 11 * 10 + 2: CFD_TBR(4, 11, 2); break;
+        case 4 * 100 + 10 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBR(4, 10, 2); break;
         case 2 * 100 + 11 * 10 + 2: CFD_TBRF(2, 11, 2); break;
         case 2 * 100 + 10 * 10 + 2: CFD_TBRF(2, 10, 2); break;
         case 2 * 100 + 9 * 10 + 2: CFD_TBRF(2, 9, 2); break;
@@ -774,15 +806,19 @@ int jacobi3d_tbr_first_pass(int K, float *out, const float *div, float *rhs_out,
     return tbr_launch<kJacobi>(a, K, 0, zchunk, false, s, kFirstRhs | (zero ? kFirstZero : 0));
 }
 
-// Red-black GS passes on tall tiles: `iters` (1 or 2) iterations from `it` on,
-// planes [zb, ze) of `out` from `in`.  A pass is skipped on the device when
-// iteration it-1 or it-2 met the tolerance; max|change| of each iteration goes
-// to ws->maxc.  rollback != 0: the conditional re-run after a stop inside a
-// pair pass (in = phi, out = phi_tmp as passed to the solve; the kernel picks
-// the direction from the count in ws->flags[1], see rbgs_count).
+// Red-black GS passes on tall tiles: `levels` half-sweeps (1..4) from half-sweep
+// h0 on (iteration h0 / 2, colour h0 & 1), planes [zb, ze) of `out` from `in`.
+// A pass is skipped on the device when an iteration the previous pass
+// completed met the tolerance (maxc of iterations h0/2 - 1 and h0/2 - 2, or
+// `lag` earlier); each level's max|change| of owned cells goes to
+// ws->maxc[its iteration] (a pass that ends inside an iteration leaves the
+// rest to the next).  rollback = P != 0: the conditional re-run after a stop
+// inside a pass of a solve of P half-sweeps per pass and nhalf in all (in =
+// phi, out = phi_tmp as passed to the solve; the kernel reads the count in
+// ws->flags[1], see rbgs_count, and picks h0 and the direction itself).
 int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
-                    int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
-                    int iters, RbgsWs *ws, int rollback, int npairs, int rows, hipStream_t s,
+                    int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int h0,
+                    int levels, RbgsWs *ws, int rollback, int nhalf, int rows, hipStream_t s,
                     int lag) {
     if (ze <= zb || ny < 3) return CFD_OK;
     TbrArgs a{};
@@ -790,13 +826,13 @@ int rbgs3d_tbr_pass(const float *in, float *out, const float *div, int nz, int n
     a.nz = nz; a.ny = ny; a.nx = nx; a.zb = zb; a.ze = ze;
     a.fixed_lo = fixed_lo; a.fixed_hi = fixed_hi;
     a.cx = k.cx; a.cy = k.cy; a.cz = k.cz; a.cd = k.cd; a.dt_inv = k.dt_inv; a.tol = k.tol;
-    a.zoff = zoff; a.it = it;
+    a.zoff = zoff; a.h0 = h0;
     a.maxc = rollback ? nullptr : ws->maxc;
     a.rollback = rollback;
-    a.npairs = npairs;
+    a.nhalf = nhalf;
     a.count = &ws->flags[1];
     a.lag = lag;
-    return tbr_launch<kRbgs>(a, 2 * iters, rows, jacobi3d_tb_zchunk(), false, s);
+    return tbr_launch<kRbgs>(a, levels, rows, jacobi3d_tb_zchunk(), false, s);
 }
 
 }  // namespace cfd

@@ -690,11 +690,11 @@ int launch_rbgs_count(RbgsWs *ws, int *iters_done, hipStream_t s) {
 // The fused paths ping-pong phi / phi_tmp, one buffer per pass; where the
 // last iteration landed depends on the device-side stop, so the copy-back is
 // decided on device too (no host sync in the solve): after c iterations at
-// `per_pass` iterations per pass the result is in buffer ceil(c / per_pass) & 1.
+// `hpp` half-sweeps per pass the result is in buffer ceil(2c / hpp) & 1.
 __global__ void rbgs_copy(const RbgsWs *__restrict__ ws, float *__restrict__ phi,
-                          const float *__restrict__ tmp, size_t n, int per_pass) {
+                          const float *__restrict__ tmp, size_t n, int hpp) {
     const int c = ws->flags[1];
-    if (!(((c + per_pass - 1) / per_pass) & 1)) return;
+    if (!(((2 * c + hpp - 1) / hpp) & 1)) return;
     const size_t n4 = n / 4;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -703,13 +703,13 @@ __global__ void rbgs_copy(const RbgsWs *__restrict__ ws, float *__restrict__ phi
     for (size_t k = 4 * n4 + t0; k < n; k += stride) phi[k] = tmp[k];
 }
 
-int launch_rbgs_copy(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n, int per_pass,
+int launch_rbgs_copy(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t n, int hpp,
                      hipStream_t s) {
     if (!phi_tmp) return CFD_OK;
     long blocks = (long)((n / 4 + 255) / 256);
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(rbgs_copy, dim3(blocks), dim3(256), 0, s, ws, phi, phi_tmp, n, per_pass);
+    hipLaunchKernelGGL(rbgs_copy, dim3(blocks), dim3(256), 0, s, ws, phi, phi_tmp, n, hpp);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }
@@ -717,7 +717,7 @@ int launch_rbgs_copy(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t 
 int launch_rbgs_finish(RbgsWs *ws, float *phi, const float *phi_tmp, size_t n, int *iters_done,
                        hipStream_t s) {
     int rc = launch_rbgs_count(ws, iters_done, s);
-    return rc ? rc : launch_rbgs_copy(ws, phi, phi_tmp, n, 1, s);
+    return rc ? rc : launch_rbgs_copy(ws, phi, phi_tmp, n, 2, s);
 }
 
 // Fused red-black iteration, 2-D: the overlapped-segment row march of
@@ -1255,7 +1255,7 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
                                     npairs, iterations, s);
                 CFD_LAUNCH_CHECK();
             }
-            return launch_rbgs_copy(w, phi, phi_tmp, (size_t)ny * nx, 2, s);
+            return launch_rbgs_copy(w, phi, phi_tmp, (size_t)ny * nx, 4, s);
         }
         for (int it = 0; it < iterations; ++it) {
             if ((rc = rbgs2d_tb_pass(a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, s)))

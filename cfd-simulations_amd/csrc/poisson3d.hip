@@ -464,9 +464,14 @@ RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double toler
     return k;
 }
 
-// Red-black GS iterations per fused pass: 2 when the blocking depth is set to
-// 4 levels (then a stop inside a pair is rolled back after the loop), else 1.
+// Red-black GS iterations per fused pass of a slab solve: 2 when the blocking
+// depth is set to 4 levels (then a stop inside a pair is rolled back after the
+// loop), else 1.
 int rbgs3d_iters_per_pass() { return tuning().tb_steps == 4 ? 2 : 1; }
+// Half-sweeps (colour levels) per fused pass of a single-GPU solve: the
+// blocking depth, 2..4; auto = 3 (one and a half iterations per HBM pass, on
+// the 3-level tall tiles the Jacobi uses).
+int rbgs3d_half_per_pass() { return tuning().tb_steps >= 2 ? tuning().tb_steps : 3; }
 
 // One fused GS pass of `iters` (1, 2) iterations: the tuned 2-level kernel
 // when its rows are set explicitly (5, 13), the tall-tile kernel otherwise
@@ -476,9 +481,21 @@ int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int
                       int iters, RbgsWs *ws, hipStream_t s, int lag) {
     if (iters == 1 && !lag && (tuning().tb_rows == 5 || tuning().tb_rows == 13))
         return rbgs3d_tb_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, ws, s);
+    return rbgs3d_half_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, 2 * it,
+                            2 * iters, ws, s, lag);
+}
+
+// A fused GS pass of `levels` half-sweeps from half-sweep h0, on the tile rows
+// set for that depth (2: 16, 18, 20, 28; 3: 16, 18; 4: 15, 16), else auto.
+int rbgs3d_half_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
+                     int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int h0,
+                     int levels, RbgsWs *ws, hipStream_t s, int lag) {
     const int r = tuning().tb_rows;
-    const bool shape_ok = iters == 1 ? (r == 16 || r == 18 || r == 20 || r == 28) : (r == 15 || r == 16);
-    return rbgs3d_tbr_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, iters,
+    const bool shape_ok = levels == 2   ? (r == 16 || r == 18 || r == 20 || r == 28)
+                          : levels == 3 ? (r == 16 || r == 18)
+                          : levels == 4 ? (r == 15 || r == 16)
+                                        : false;
+    return rbgs3d_tbr_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, h0, levels,
                            ws, 0, 0, shape_ok ? r : 0, s, lag);
 }
 
@@ -573,10 +590,10 @@ int cfd_set_jacobi3d_prefetch(int planes) {
 
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
     CFD_REQUIRE(steps >= 0 && steps <= 4, "blocking steps must be 0 (auto), 1 (off) or 2..4");
-    CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13 || rows == 9 || rows == 11 || rows == 15 ||
+    CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13 || rows == 9 || rows == 11 || rows == 14 || rows == 15 ||
                     rows == 16 || rows == 17 || rows == 18 || rows == 20 || rows == 28,
                 "blocking rows must be 0 (auto), 5, 13, 16, 18, 20, 28 (2 levels), 11, 16, 17, 18 (3), "
-                "9, 15, 16 (4)");
+                "9, 14, 15, 16 (4)");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
     tuning().tb_steps = steps;
     tuning().tb_rows = rows;
@@ -707,23 +724,35 @@ int cfd_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask, int nz, in
         // ping-pong; the result's buffer and a stop inside a pair pass are
         // resolved on the device after the loop
         if ((rc = launch_fix_faces3d(phi, phi_tmp, nullptr, ny, nx, 0, nz, 0, nz - 1, s))) return rc;
-        const int pp = rbgs3d_iters_per_pass();
-        const int npairs = pp == 2 ? iterations / 2 : 0;
+        // passes of P half-sweeps (colour levels), the last one shorter
+        const int P = rbgs3d_half_per_pass(), H = 2 * iterations;
         float *a = phi, *b = phi_tmp;
-        for (int it = 0; it < iterations;) {
-            const int m = iterations - it >= pp ? pp : 1;
-            if ((rc = rbgs3d_fused_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, it, m, w, s)))
-                return rc;
-            it += m;
-            float *t = a; a = b; b = t;
+        if (iterations > 0 && tuning().tb_rows != 5 && tuning().tb_rows != 13) {
+            for (int h = 0; h < H; h += P) {
+                const int m = H - h >= P ? P : H - h;
+                if ((rc = rbgs3d_half_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, h, m, w, s, 0)))
+                    return rc;
+                float *t = a; a = b; b = t;
+            }
+        } else {
+            for (int it = 0; it < iterations; ++it) {  // the 2-level tb2 kernel (rows 5, 13)
+                if ((rc = rbgs3d_fused_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, it, 1, w, s)))
+                    return rc;
+                float *t = a; a = b; b = t;
+            }
         }
+        const int hpp = tuning().tb_rows == 5 || tuning().tb_rows == 13 ? 2 : P;
         timing_end(tk, s, iterations);
         if ((rc = launch_rbgs_count(w, iters_done, s))) return rc;
-        if (pp == 2 &&
-            (rc = rbgs3d_tbr_pass(phi, phi_tmp, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, 0, 1, w, 1,
-                                  npairs, 0, s)))
-            return rc;
-        return launch_rbgs_copy(w, phi, phi_tmp, n, pp, s);
+        // a stop inside a pass: re-run its half-sweeps up to the stop, one
+        // launch per possible count (2c - P j is even when P is); none when
+        // no stop is possible (tolerance <= 0)
+        for (int need = 1; need < hpp && k.tol > 0.f; ++need)
+            if (!(hpp % 2 == 0 && need % 2 == 1) &&
+                (rc = rbgs3d_tbr_pass(phi, phi_tmp, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, 0, need, w, hpp,
+                                      H, 0, s)))
+                return rc;
+        return launch_rbgs_copy(w, phi, phi_tmp, n, hpp, s);
     }
     for (int it = 0; it < iterations; ++it) {
         if ((rc = rbgs3d_colour_pass(0, phi, div, mask, ny, nx, 1, nz - 1, 0, k, w, it, s))) return rc;

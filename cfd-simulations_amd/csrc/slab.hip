@@ -534,7 +534,6 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     // pp iterations per pass need 2*pp-deep ghosts (the pass recomputes the
     // inner ghost planes' intermediate colours)
     const int pp = rbgs3d_iters_per_pass() == 2 && G >= 4 ? 2 : 1;
-    const int npairs = pp == 2 ? iterations / 2 : 0;
     // owned faces the passes never write, in both buffers
     const int full_lo = fixed_lo ? G : -1;
     const int full_hi = fixed_hi ? nz_local + G - 1 : -1;
@@ -602,10 +601,10 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     // pass's first iteration if the stop fell inside it, pick the buffer
     if ((rc = launch_rbgs_count(w, iters_done, s))) return rc;
     if (pp == 2 &&
-        (rc = rbgs3d_tbr_pass(phi, phi_tmp, div, nzt, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, 0, 1,
-                              w, 1, npairs, 0, s)))
+        (rc = rbgs3d_tbr_pass(phi, phi_tmp, div, nzt, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, 0, 2,
+                              w, 4, 2 * iterations, 0, s)))
         return rc;
-    return launch_rbgs_copy(w, phi, phi_tmp, plane * nzt, pp, s);
+    return launch_rbgs_copy(w, phi, phi_tmp, plane * nzt, 2 * pp, s);
 }
 
 }  // extern "C"

@@ -2,7 +2,7 @@
 """Per-kernel resource usage of one HIP source (VGPRs, spills, LDS, occupancy),
 from hipcc's -Rpass-analysis=kernel-resource-usage remarks.  Host-side tool.
 
-    python scripts/resource_usage.py cfd-simulations_amd/csrc/jacobi3d_tbr.hip [filter]
+    python scripts/resource_usage.py cfd-simulations_amd/csrc/jacobi3d_tbr.hip [filter [hipcc flags...]]
 """
 import re
 import subprocess
@@ -10,9 +10,10 @@ import sys
 
 src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
+extra = sys.argv[3:]
 out = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
                       "-ffp-contract=off", "-c", src, "-o", "/tmp/_ru.o",
-                      "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
+                      "-Rpass-analysis=kernel-resource-usage", *extra], capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
     m = re.search(r"remark: (?:\s*)(Function Name|VGPRs|VGPRs Spill|LDS Size \[bytes/block\]|Occupancy \[waves/SIMD\]|SGPRs): (\S+)", line)

@@ -321,8 +321,9 @@ def test_rbgs3d_random_bitexact(shape, masked, fused):
 
 
 # (blocking steps, rows): tuned 2-level kernel (rows 5 / 13), tall tiles with
-# one iteration per pass (steps 0 / 2 / 3), tall tiles with two (steps 4)
-GS_FUSED = [(2, 5), (2, 13), (0, 0), (3, 0), (4, 0)]
+# one iteration per pass (steps 2), one and a half (steps 0 = auto, 3: passes
+# that end inside an iteration), two (steps 4)
+GS_FUSED = [(2, 5), (2, 13), (0, 0), (2, 0), (3, 0), (4, 0)]
 
 
 @pytest.mark.parametrize("steps,rows", GS_FUSED)
@@ -349,8 +350,9 @@ def test_rbgs3d_fused_tiles_bitexact(steps, rows, zchunk, prefetch, iters):
 @pytest.mark.parametrize("steps,rows", GS_FUSED)
 @pytest.mark.parametrize("tol", [2e-5, 1.5e-5, 1e-5])  # stops after 6 / 7 / 11 iterations
 def test_rbgs3d_early_exit_fused(steps, rows, tol):
-    """The stop inside a pair pass (odd count at two iterations per pass) is
-    rolled back on the device; the count and field match the oracle."""
+    """A stop inside a pass (an odd count at two iterations per pass; any count
+    whose 2c half-sweeps end inside a pass of three) is rolled back on the
+    device; the count and field match the oracle."""
     call("cfd_set_jacobi3d_blocking", steps, rows, 0)
     rng = np.random.default_rng(13)
     div = rng.standard_normal((24, 26, 40)).astype(np.float32) * np.float32(1e-3)
@@ -371,15 +373,15 @@ def test_rbgs3d_fused_matches_colour_passes_at_512():
     g = torch.Generator(device=DEV).manual_seed(3)
     div = torch.randn((n, n, n), device=DEV, generator=g)
     outs = []
-    for steps in (1, 0, 4):
+    for steps in (1, 0, 2, 4):
         call("cfd_set_jacobi3d_blocking", steps, 0, 0)
         phi = torch.zeros_like(div)
         done = torch.zeros(1, dtype=torch.int32, device=DEV)
         h = 1.0 / (n - 1)
         K.solve_pressure_gauss_seidel3d(phi, div, h, h, h, np.float32(5e-5), None, 6, 0.0, iters_done=done)
         outs.append((phi, int(host(done)[0])))
-    assert outs[0][1] == outs[1][1] == outs[2][1] == 6
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][0], outs[2][0])
+    assert all(o[1] == 6 for o in outs)
+    assert all(torch.equal(outs[0][0], o[0]) for o in outs[1:])
 
 
 # ------------------------------------------------------------- predictor & co

@@ -90,8 +90,9 @@ def test_jacobi3d_1024_headline_kernel_bitexact(div1024):
 
 def test_rbgs3d_1024_default_tile_bitexact(div1024):
     """Config 5's kernel at full size: 2 and 3 red-black iterations (tolerance
-    1e-8, no stop) on the default 16-row GS tile, phi_tmp ping-pong with the
-    result copied back on the device for the odd count."""
+    1e-8, no stop) on the default tile -- three half-sweeps per pass on the
+    16-row 3-level tile (passes of colours 0,1,0 then 1(,0,1)), phi_tmp
+    ping-pong with the result copied back on the device."""
     n = 1024
     h, dt = 1.0 / (n - 1), np.float32(5e-5)
     ref2, n2 = oracle.rbgs3d(div1024, dx=h, dy=h, dz=h, dt=dt, iters=2, tol=1e-8, mt=True)
@@ -102,19 +103,24 @@ def test_rbgs3d_1024_default_tile_bitexact(div1024):
     tmp = torch.empty_like(d)
     done = torch.zeros(1, dtype=torch.int32, device=DEV)
     for iters, ref in ((2, ref2), (3, ref3)):
-        phi.zero_()
-        K.solve_pressure_gauss_seidel3d(phi, d, h, h, h, dt, None, iters, 1e-8, iters_done=done, phi_tmp=tmp)
-        assert last_shape()[:3] == (2, 9, 2), last_shape()
-        assert int(host(done)[0]) == iters
-        assert np.array_equal(host(phi), ref), iters
+        for tol in (1e-8, 0.0):  # tol 0: no stop possible, no rollback launch after the passes
+            phi.zero_()
+            K.solve_pressure_gauss_seidel3d(phi, d, h, h, h, dt, None, iters, tol, iters_done=done, phi_tmp=tmp)
+            if tol == 0.0 and iters == 3:
+                assert last_shape()[:3] == (3, 10, 2), last_shape()
+            assert int(host(done)[0]) == iters
+            assert np.array_equal(host(phi), ref), iters
 
 
-@pytest.mark.parametrize("rows,shape", [(16, (2, 9, 2)), (18, (2, 10, 2)), (20, (2, 11, 2)), (28, (2, 10, 3))])
-@pytest.mark.parametrize("tol,iters", [(0.0, 7), (1.5e-5, 300)])
-def test_rbgs3d_explicit_gs_tiles_ragged(rows, shape, tol, iters):
-    """Every GS tile shape on a ragged grid (y and z not multiples of the tile,
-    two x-segments), fixed count and early stop."""
-    call("cfd_set_jacobi3d_blocking", 0, rows, 0)
+@pytest.mark.parametrize("levels,rows,shape", [(2, 16, (2, 9, 2)), (2, 18, (2, 10, 2)), (2, 20, (2, 11, 2)),
+                                               (2, 28, (2, 10, 3)), (3, 16, (3, 10, 2)), (3, 18, (3, 11, 2)),
+                                               (4, 15, (4, 7, 3))])
+@pytest.mark.parametrize("tol,iters", [(0.0, 6), (1.5e-5, 300)])
+def test_rbgs3d_explicit_gs_tiles_ragged(levels, rows, shape, tol, iters):
+    """Every GS tile shape (half-sweeps per pass 2, 3, 4) on a ragged grid (y
+    and z not multiples of the tile, two x-segments), fixed count and early
+    stop."""
+    call("cfd_set_jacobi3d_blocking", levels, rows, 0)
     rng = np.random.default_rng(rows)
     div = rng.standard_normal((29, 53, 264)).astype(np.float32) * np.float32(1e-3)
     ref, n_ref = oracle.rbgs3d(div, dx=0.05, dy=0.05, dz=0.05, dt=np.float32(1e-2), iters=iters, tol=tol)
@@ -123,8 +129,9 @@ def test_rbgs3d_explicit_gs_tiles_ragged(rows, shape, tol, iters):
     phi = torch.zeros_like(dev(div))
     done = torch.zeros(1, dtype=torch.int32, device=DEV)
     K.solve_pressure_gauss_seidel3d(phi, dev(div), 0.05, 0.05, 0.05, np.float32(1e-2), None, iters, tol,
-                                    iters_done=done)
-    assert last_shape()[:3] == shape
+                                    iters_done=done, phi_tmp=torch.empty_like(phi))
+    if tol == 0.0:  # 12 half-sweeps: whole passes of 2, 3 and 4, no rollback launch
+        assert last_shape()[:3] == shape, last_shape()
     assert int(host(done)[0]) == n_ref
     assert np.array_equal(host(phi), ref)
 
@@ -316,3 +323,52 @@ def test_jacobi3d_first_pass_general_start_bitexact():
         rhs = torch.full_like(phi, float("nan"))
         K.solve_pressure_jacobi3d(phi, dev(div), 0.05, np.float32(2e-3), None, iters, rhs_ws=rhs)
         assert np.array_equal(host(phi), ref), iters
+
+
+# ------------------------------------------ GS passes of 1..4 half-sweeps
+def _rbgs3d_maxc(div, n, **kw):
+    """The oracle's per-iteration max|change|: each cell is updated once per
+    iteration, so it is max|phi_(i+1) - phi_i| in float32 (the kernel's
+    fabsf(new - old))."""
+    phi = np.zeros_like(div)
+    out = []
+    for _ in range(n):
+        nxt, _ = oracle.rbgs3d(div, phi, iters=1, tol=0.0, **kw)
+        out.append(float(np.abs(nxt - phi).max()))
+        phi = nxt
+    return np.array(out, np.float32)
+
+
+@pytest.mark.parametrize("levels", [0, 2, 3, 4])
+def test_rbgs3d_stop_at_every_iteration(levels):
+    """A stop at every iteration 1..N of solves of N = 13 and 14 iterations,
+    for passes of 2, 3 (auto) and 4 half-sweeps: with 3 per pass an iteration
+    can end in the middle of a pass, which the rollback launches (1 or 2
+    half-sweeps) undo; the count, the buffer the result lands in and every
+    value must be the oracle's."""
+    call("cfd_set_jacobi3d_blocking", levels, 0, 0)
+    rng = np.random.default_rng(40 + levels)
+    div = rng.standard_normal((19, 27, 132)).astype(np.float32) * np.float32(1e-3)
+    kw = dict(dx=0.05, dy=0.05, dz=0.05, dt=np.float32(1e-2))
+    mc = _rbgs3d_maxc(div, 14, **kw)
+    d = dev(div)
+    tmp = torch.empty_like(d)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    seen = set()
+    for c in range(1, 15):
+        lo = mc[c - 1]
+        hi = mc[:c - 1].min() if c > 1 else np.float32(np.inf)
+        if not lo < hi:
+            continue
+        tol = float(lo) * 1.0000005 if not np.isfinite(hi) else float((np.float64(lo) + np.float64(hi)) / 2)
+        if not (lo < np.float32(tol) <= hi):
+            continue
+        for N in (13, 14):
+            ref, n_ref = oracle.rbgs3d(div, iters=N, tol=tol, **kw)
+            phi = torch.zeros_like(d)
+            K.solve_pressure_gauss_seidel3d(phi, d, *(0.05,) * 3, kw["dt"], None, N, tol, iters_done=done,
+                                            phi_tmp=tmp)
+            assert int(host(done)[0]) == n_ref, (c, N, n_ref)
+            assert np.array_equal(host(phi), ref), (c, N)
+            seen.add(n_ref)
+    assert len(seen) >= 10, seen
