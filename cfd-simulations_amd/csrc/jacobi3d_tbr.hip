@@ -99,31 +99,33 @@ __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S
     if (!upd) return c;
     if (MODE == kRbgs) {
         // x % 4 == 0, so the colour updates cells k = par & 1 and k + 2 of the
-        // float4 (par is uniform over a row): those two only, as one float2
-        // pair through packed math, in the in-place kernel's operation order
+        // float4: those two only, as one float2 pair through packed math, in
+        // the in-place kernel's operation order.  The row waves pass a par that
+        // is a compile-time constant once their loops are unrolled (see
+        // `march`), so the selects below fold away there.
         typedef float v2f __attribute__((ext_vector_type(2)));
-        auto pair = [&](v2f C, v2f E, v2f Wv, v2f Nv, v2f Sv, v2f Uv, v2f Dv, v2f Rv, int x0) {
-            const v2f rhs = -Rv * a.dt_inv;
-            const v2f p = a.cx * (E + Wv);
-            const v2f q = a.cy * (Nv + Sv);
-            const v2f r = a.cz * (Uv + Dv);
-            v2f o = (((p + q) + r) - rhs) * a.cd;
-            o.x = (x0 != 0 && x0 != nx - 1) ? o.x : C.x;  // the pair's cells x0, x0 + 2 >= 2
-            o.y = (x0 + 2 != nx - 1) ? o.y : C.y;
-            if (own) {  // fmaxf ignores a NaN change like the `ch > mx` test
-                chg = fmaxf(chg, fabsf(o.x - C.x));
-                chg = fmaxf(chg, fabsf(o.y - C.y));
-            }
-            return o;
-        };
-        if (par & 1) {  // row-uniform: a scalar branch, no per-element selects
-            const v2f o = pair(v2f{c.y, c.w}, v2f{c.z, er}, v2f{c.x, c.z}, v2f{N.y, N.w}, v2f{S.y, S.w},
-                               v2f{U.y, U.w}, v2f{D.y, D.w}, v2f{d.y, d.w}, x + 1);
-            return make_float4(c.x, o.x, c.z, o.y);
+        const bool hi = (par & 1) != 0;
+        const v2f C = hi ? v2f{c.y, c.w} : v2f{c.x, c.z};
+        const v2f E = hi ? v2f{c.z, er} : v2f{c.y, c.w};
+        const v2f Wv = hi ? v2f{c.x, c.z} : v2f{wl, c.y};
+        const v2f Nv = hi ? v2f{N.y, N.w} : v2f{N.x, N.z};
+        const v2f Sv = hi ? v2f{S.y, S.w} : v2f{S.x, S.z};
+        const v2f Uv = hi ? v2f{U.y, U.w} : v2f{U.x, U.z};
+        const v2f Dv = hi ? v2f{D.y, D.w} : v2f{D.x, D.z};
+        const v2f Rv = hi ? v2f{d.y, d.w} : v2f{d.x, d.z};
+        const v2f rhs = -Rv * a.dt_inv;
+        const v2f p = a.cx * (E + Wv);
+        const v2f q = a.cy * (Nv + Sv);
+        const v2f r = a.cz * (Uv + Dv);
+        v2f o = (((p + q) + r) - rhs) * a.cd;
+        const int x0 = x + (hi ? 1 : 0);  // the pair's cells x0, x0 + 2 (x0 + 2 >= 2)
+        o.x = (x0 != 0 && x0 != nx - 1) ? o.x : C.x;
+        o.y = (x0 + 2 != nx - 1) ? o.y : C.y;
+        if (own) {  // fmaxf ignores a NaN change like the `ch > mx` test
+            chg = fmaxf(chg, fabsf(o.x - C.x));
+            chg = fmaxf(chg, fabsf(o.y - C.y));
         }
-        const v2f o = pair(v2f{c.x, c.z}, v2f{c.y, c.w}, v2f{wl, c.y}, v2f{N.x, N.z}, v2f{S.x, S.z},
-                           v2f{U.x, U.z}, v2f{D.x, D.z}, v2f{d.x, d.z}, x);
-        return make_float4(o.x, c.y, o.y, c.w);
+        return hi ? make_float4(c.x, o.x, c.z, o.y) : make_float4(o.x, c.y, o.y, c.w);
     }
     const float h2 = a.h2, dt = a.dt;
     const float cv[4] = {c.x, c.y, c.z, c.w};
@@ -415,8 +417,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 if (!ZERO) dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], st_p1 + (rr[j] - 1) * 256);
                 dma_row(plane_rsrc4(a.div, zs, nz, plane), bo[j], st_r1 + (rr[j] - 1) * 256);
             }
-            auto step = [&](int z, auto parc) {
+            auto step = [&](int z, auto parc, auto bpc) {
                 constexpr int E = decltype(parc)::value;  // (z - zs) & 1
+                // GS colour parity of row j at this step, for every level:
+                // (zoff + p + y + 1 + h0 + l - 1) with p = z - l + 1 and z = zs + E
+                // is BP ^ E ^ (j * NWR) mod 2 (BP: see march)
+                constexpr int BPv = decltype(bpc)::value;
                 float *const pw = E ? st_p1 : st_p0;
                 float *const rw = E ? st_r1 : st_r0;
                 const float *const pr = E ? st_p0 : st_p1;
@@ -483,9 +489,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
                                 const int y = y0 - K + r;
                                 float lm = 0.f;
+                                (void)y;
                                 v = level4<MODE, PREL>(c, wl, er, N, S, U, D, Rq[j][l - 1], x, nx,
-                                                      irow[j] && !fx, a,
-                                                      (a.zoff + p + y + 1 + ((a.h0 + l - 1) & 1)) & 1,
+                                                      irow[j] && !fx, a, (BPv ^ E ^ (j * NWR)) & 1,
                                                       orow[j] && p >= z0 && p < z1, lm);
                                 fold(l, lm);
                             }
@@ -516,10 +522,19 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     V[j][1] = V[j][2];
                 }
             };
-            for (int zb = zs; zb <= zl; zb += 2) {
-                step(zb, std::integral_constant<int, 0>{});
-                if (zb + 1 <= zl) step(zb + 1, std::integral_constant<int, 1>{});
-            }
+            // the z-march, instantiated per base colour parity BP (wave-uniform:
+            // zoff + zs + y0 + K + wv + h0) so that every level's colour is a
+            // compile-time constant in the GS (one copy for Jacobi)
+            auto march = [&](auto bpc) {
+                for (int zb = zs; zb <= zl; zb += 2) {
+                    step(zb, std::integral_constant<int, 0>{}, bpc);
+                    if (zb + 1 <= zl) step(zb + 1, std::integral_constant<int, 1>{}, bpc);
+                }
+            };
+            if (MODE == kRbgs && ((a.zoff + zs + y0 + K + wv + a.h0) & 1))
+                march(std::integral_constant<int, 1>{});
+            else
+                march(std::integral_constant<int, 0>{});
             wait_vmcnt<0>();  // no LDS-DMA outlives the wave
         } else {
             // ------------------------------------------------------------ row wave

@@ -22,7 +22,7 @@ step() {
 for s in "$@"; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread ;;
+    tests) step pytest_gpu 1000 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread ;;
     testsq) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
     bench) step bench 600 python bench.py ;;
     bench512) step bench512 600 python bench.py --workload jacobi3d_512 --no-cpu-baseline ;;
@@ -66,6 +66,7 @@ for s in "$@"; do
     prof_selfgs) step prof_selfgs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_selfgs -o run --output-format csv -- python3 scripts/slab_rehearsal.py --rccl-self --workload rbgs --ranks 8 --steps 1 ;;
     ab2d) step ab2d 600 bash -c 'for e in 0 1; do echo "CFD_J2_RHS_REGS=$e"; CFD_J2_RHS_REGS=$e python bench.py --workload jacobi2d_8192_f64 --no-cpu-baseline --steps 5 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
     cyl) step cyl 600 bash -c 'python scripts/cylinder_bench.py && python scripts/cylinder_bench.py --jacobi' ;;
+    sq_gs) step sq_gs 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES -d gpurun_out/sq_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 12 --no-cpu-baseline ;;
     prof_cyl) step prof_cyl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cyl -o run --output-format csv -- python3 scripts/cylinder_bench.py --steps 3 --warmup 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
