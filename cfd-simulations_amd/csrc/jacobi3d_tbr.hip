@@ -63,6 +63,9 @@ __device__ inline v4i32 plane_rsrc4(const float *base, int p, int nz, size_t pla
 // vmcnt(0)); the memory clobber keeps the compiler's LDS accesses in place
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 enum { kJacobi = 0, kRbgs = 1 };
+// register-queue slot of a plane offset v: v mod 3 / v mod k, non-negative
+constexpr int sl3(int v) { return ((v % 3) + 3) % 3; }
+constexpr int slk(int v, int k) { return ((v % k) + k) % k; }
 
 struct TbrArgs {
     const float *in;
@@ -157,7 +160,8 @@ __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S
 // rows and the 4-float x-halo chunks of every row, and computes levels
 // 1..K-1 of the chunks, in lock step (two barriers per step) with the row waves.
 template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F>
-__device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0, int z1, int y0, int xs) {
+__device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0, int z1, int y0, int xs,
+                                              int zl) {
     constexpr int NR = NWR * RPW + 2;
     constexpr int RS = 264;
     auto T = [&](int l, int r) -> float * {
@@ -172,7 +176,7 @@ __device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0,
     const int x = xs + 4 * lane;
     const bool xin = x < nx;
     const size_t plane = (size_t)ny * nx;
-    const int zs = z0 - K + 1, zl = z1 + K - 2;
+    const int zs = z0 - K + 1;  // zl: the row waves' last front plane (they may run past z1 + K - 2)
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -271,6 +275,15 @@ __device__ __noinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0,
     }
 }
 
+// The halo wave as a called function (K <= 3: measured 1.5-2.5 % faster than
+// inlined there); K = 4 inlines it (as a call it takes the TbrArgs by value in
+// VGPRs and a call frame: 168-181 VGPRs, which spill).
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F>
+__device__ __noinline__ void tbr_halo_wave_call(const TbrArgs a, float *smem, int z0, int z1, int y0,
+                                                int xs, int zl) {
+    tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
+}
+
 // (A double-buffered, one-barrier-per-step version of the (3, 11, 2) shape --
 // 139 KB of LDS -- was measured at 1007 against 1131 Gcell/s for this one.)
 // MODE kRbgs: K red-black half-sweeps per pass, level l = half-sweep h0+l-1
@@ -296,9 +309,14 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // Separate arrays per parity let the compiler see that step z's reads do
     // not alias step z's DMA (no vmcnt(0) before them).
     constexpr int SR_ = NR - 2;  // rows 1 .. NR-2 (the row waves' rows)
-    constexpr bool DMA = PD == 1 && (TOTAL + 4 * SR_ * 256) * 4 <= 160 * 1024;
+    // DMA: the phi rows by LDS-DMA; RDMA: the rhs rows too when both staging
+    // pairs fit beside the level tiles, else the rhs row of plane z + 1 is a
+    // register load issued a step ahead (4 VGPRs per row)
+    constexpr bool DMA = PD == 1 && (TOTAL + 2 * SR_ * 256) * 4 <= 160 * 1024;
+    constexpr bool RDMA = DMA && (TOTAL + 4 * SR_ * 256) * 4 <= 160 * 1024;
     constexpr int SST = DMA ? SR_ * 256 : 4;
-    __shared__ __attribute__((aligned(16))) float st_p0[SST], st_p1[SST], st_r0[SST], st_r1[SST];
+    constexpr int SSR = RDMA ? SR_ * 256 : 4;
+    __shared__ __attribute__((aligned(16))) float st_p0[SST], st_p1[SST], st_r0[SSR], st_r1[SSR];
     // level l keeps rows [l, NR - l)
     auto T = [&](int l, int r) -> float * {
         int base = 0;
@@ -366,7 +384,14 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     const bool xin = x < nx;
     const size_t plane = (size_t)ny * nx;
     const int zs = z0 - K + 1;  // first front plane
-    const int zl = z1 + K - 2;  // last front plane
+    // last front plane; the LDS-DMA march runs whole groups of 6 steps (the
+    // extra steps at the end compute planes past the chunk and store nothing)
+    const int zl0 = z1 + K - 2;
+    // register queues rotated by compile-time slots (see the DMA row wave) for
+    // the Jacobi up to 3 levels: -2.3 % per pass at K = 3; the red-black GS
+    // (two copies of the march, see march) and K = 4 spill with them
+    constexpr bool ROT = DMA && MODE == kJacobi && K <= 3;
+    const int zl = ROT ? zs + 6 * ((zl0 - zs + 6) / 6) - 1 : zl0;
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -403,22 +428,40 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             // V[j][i]: level 0 of plane z-1+i; Q[j][l][i]: level l of plane
             // (z-l)-1+i after level l is computed; Rq[j][i]: rhs of plane z-i
             float4 V[RPW][3], Q[RPW][K][3], Rq[RPW][K];
+            float4 Rn[RPW];  // !RDMA: the rhs row of the next step's plane, in flight
 #pragma unroll
             for (int j = 0; j < RPW; ++j) {
 #pragma unroll
                 for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = z4;
-                V[j][0] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]);
-                V[j][1] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs, nz, plane), bo[j]);
-                V[j][2] = z4;
-                Rq[j][0] = z4;
+                // planes zs - 1 and zs in slots 2 and 0 (slot (q - zs) mod 3), or 0
+                // and 1 (shifted queues)
+                V[j][ROT ? 2 : 0] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]);
+                V[j][ROT ? 0 : 1] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs, nz, plane), bo[j]);
+                V[j][ROT ? 1 : 2] = z4;
+                // rhs rows of planes before zs only feed levels of planes below the
+                // ones the outputs need (the pipeline fill), so they start at 0
 #pragma unroll
-                for (int i = 1; i < K; ++i) Rq[j][i] = torhs(ldb4(plane_rsrc(a.div, zs - i, nz, plane), bo[j]));
+                for (int i = 0; i < K; ++i) Rq[j][i] = z4;
                 // read at step zs (even): plane zs + 1 and rhs zs in the odd buffers
                 if (!ZERO) dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], st_p1 + (rr[j] - 1) * 256);
-                dma_row(plane_rsrc4(a.div, zs, nz, plane), bo[j], st_r1 + (rr[j] - 1) * 256);
+                if constexpr (RDMA)
+                    dma_row(plane_rsrc4(a.div, zs, nz, plane), bo[j], st_r1 + (rr[j] - 1) * 256);
+                else
+                    Rn[j] = ldb4(plane_rsrc(a.div, zs, nz, plane), bo[j]);
             }
-            auto step = [&](int z, auto parc, auto bpc) {
+            // Register queues without moves: plane q of level 0 / level l lives
+            // in slot (q - zs) mod 3 of V / Q[.][l], and (when the unroll
+            // period 6 is a multiple of K) the rhs of plane q in slot
+            // (q - zs) mod K of Rq; the march is unrolled by 6 so that every
+            // slot index is a compile-time constant.  (K = 4 shifts Rq.)
+            constexpr bool ROTR = ROT && 6 % K == 0;
+            auto step = [&](int z, auto parc, auto rotc, auto bpc) {
                 constexpr int E = decltype(parc)::value;  // (z - zs) & 1
+                constexpr int R = decltype(rotc)::value;  // (z - zs) mod 6 (ROT), else 0
+                // queue slots: level 0 / level l-1 at planes p (C), p + 1 (U), p - 1 (D)
+                // of level l's plane p = z - l + 1; the slot level l's new value takes
+                auto vs = [](int d) { return ROT ? sl3(R + d) : d + 1; };        // V: plane z + d
+                auto qs = [](int l, int d) { return ROT ? sl3(R - l - 1 + d) : d; }; // Q[l]: plane z - l - 1 + d
                 // GS colour parity of row j at this step, for every level:
                 // (zoff + p + y + 1 + h0 + l - 1) with p = z - l + 1 and z = zs + E
                 // is BP ^ E ^ (j * NWR) mod 2 (BP: see march)
@@ -433,27 +476,45 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
                         if (!ZERO) dma_row(rp, bo[j], pw + (rr[j] - 1) * 256);
-                        dma_row(rd, bo[j], rw + (rr[j] - 1) * 256);
+                        if constexpr (RDMA) dma_row(rd, bo[j], rw + (rr[j] - 1) * 256);
+                    }
+                }
+                // !RDMA: this step's rhs row (loaded last step) and the next one's load
+                float4 Rc[RPW];
+                if constexpr (!RDMA) {
+                    (void)rw;
+                    (void)rdr;
+#pragma unroll
+                    for (int j = 0; j < RPW; ++j) {
+                        Rc[j] = Rn[j];
+                        Rn[j] = ldb4(plane_rsrc(a.div, z + 1, nz, plane), bo[j]);
                     }
                 }
                 // phase W: level 0 of plane z and level l of plane z - l
 #pragma unroll
                 for (int j = 0; j < RPW; ++j) {
-                    if (xin) sts4(T(0, rr[j]) + 4 + 4 * lane, V[j][1]);
+                    if (xin) sts4(T(0, rr[j]) + 4 + 4 * lane, V[j][vs(0)]);
 #pragma unroll
                     for (int l = 1; l < K; ++l)
-                        if (xin && rr[j] >= l && rr[j] < NR - l) sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][2]);
+                        if (xin && rr[j] >= l && rr[j] < NR - l)
+                            sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][ROT ? sl3(R - l) : 2]);
                 }
                 // the previous step's DMAs have landed once at most this step's
                 // 2 * RPW remain in flight (they are issued in order)
-                wait_vmcnt<(ZERO ? 1 : 2) * RPW>();
+                wait_vmcnt<((ZERO ? 0 : 1) + 1) * RPW>();
                 lds_barrier();
 #pragma unroll
                 for (int j = 0; j < RPW; ++j) {
-                    V[j][2] = ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
+                    V[j][vs(1)] = ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
+                    constexpr int RS0 = ROTR ? slk(R, K) : 0;  // slot of this step's rhs
+                    if constexpr (!ROTR) {
 #pragma unroll
-                    for (int i = K - 1; i > 0; --i) Rq[j][i] = Rq[j][i - 1];
-                    Rq[j][0] = torhs(lds4(rdr + (rr[j] - 1) * 256 + 4 * lane));
+                        for (int i = K - 1; i > 0; --i) Rq[j][i] = Rq[j][i - 1];
+                    }
+                    if constexpr (RDMA)
+                        Rq[j][RS0] = torhs(lds4(rdr + (rr[j] - 1) * 256 + 4 * lane));
+                    else
+                        Rq[j][RS0] = torhs(Rc[j]);
                     if constexpr (RHSW) {
                         // the rhs of plane z for the later passes: owned planes and
                         // rows only (so[j] = kOob elsewhere), every x of the row
@@ -461,7 +522,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                         const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
                             a.rhs_out + (size_t)(own ? z : 0) * plane, (short)0,
                             own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
-                        const gv4f rv = {Rq[j][0].x, Rq[j][0].y, Rq[j][0].z, Rq[j][0].w};
+                        const gv4f rv = {Rq[j][RS0].x, Rq[j][RS0].y, Rq[j][RS0].z, Rq[j][RS0].w};
                         __builtin_amdgcn_raw_buffer_store_b128(rv, ro, (int)so[j], 0, 0);
                     }
                 }
@@ -474,9 +535,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     for (int j = 0; j < RPW; ++j) {
                         const int r = rr[j];
                         if (r >= l && r < NR - l) {
-                            const float4 c = l == 1 ? V[j][1] : Q[j][l - 1][1];
-                            const float4 U = l == 1 ? V[j][2] : Q[j][l - 1][2];
-                            const float4 D = l == 1 ? V[j][0] : Q[j][l - 1][0];
+                            // level l-1 at planes p (c), p + 1 (U), p - 1 (D)
+                            const float4 c = l == 1 ? V[j][vs(0)] : Q[j][l - 1][qs(l - 1, 1)];
+                            const float4 U = l == 1 ? V[j][vs(1)] : Q[j][l - 1][qs(l - 1, 2)];
+                            const float4 D = l == 1 ? V[j][vs(-1)] : Q[j][l - 1][qs(l - 1, 0)];
                             float wl = dpp_from_lower(c.w);
                             float er = dpp_from_upper(c.x);
                             const float *row = T(l - 1, r);
@@ -490,15 +552,20 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const int y = y0 - K + r;
                                 float lm = 0.f;
                                 (void)y;
-                                v = level4<MODE, PREL>(c, wl, er, N, S, U, D, Rq[j][l - 1], x, nx,
+                                v = level4<MODE, PREL>(c, wl, er, N, S, U, D,
+                                                      Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], x, nx,
                                                       irow[j] && !fx, a, (BPv ^ E ^ (j * NWR)) & 1,
                                                       orow[j] && p >= z0 && p < z1, lm);
                                 fold(l, lm);
                             }
                             if (l < K) {
-                                Q[j][l][0] = Q[j][l][1];
-                                Q[j][l][1] = Q[j][l][2];
-                                Q[j][l][2] = v;
+                                if constexpr (ROT) {
+                                    Q[j][l][sl3(R - l + 1)] = v;  // over plane p - 3, dead
+                                } else {
+                                    Q[j][l][0] = Q[j][l][1];
+                                    Q[j][l][1] = Q[j][l][2];
+                                    Q[j][l][2] = v;
+                                }
                             } else {
                                 // unconditional buffer store: rows, lanes and planes this
                                 // tile does not own fall out of range and are dropped
@@ -516,19 +583,34 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     }
                 }
                 lds_barrier();
+                if constexpr (!ROT) {
 #pragma unroll
-                for (int j = 0; j < RPW; ++j) {
-                    V[j][0] = V[j][1];
-                    V[j][1] = V[j][2];
+                    for (int j = 0; j < RPW; ++j) {
+                        V[j][0] = V[j][1];
+                        V[j][1] = V[j][2];
+                    }
                 }
             };
             // the z-march, instantiated per base colour parity BP (wave-uniform:
             // zoff + zs + y0 + K + wv + h0) so that every level's colour is a
             // compile-time constant in the GS (one copy for Jacobi)
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
             auto march = [&](auto bpc) {
-                for (int zb = zs; zb <= zl; zb += 2) {
-                    step(zb, std::integral_constant<int, 0>{}, bpc);
-                    if (zb + 1 <= zl) step(zb + 1, std::integral_constant<int, 1>{}, bpc);
+                if constexpr (!ROT) {
+                    for (int zb = zs; zb <= zl; zb += 2) {
+                        step(zb, I0{}, I0{}, bpc);
+                        if (zb + 1 <= zl) step(zb + 1, I1{}, I0{}, bpc);
+                    }
+                    return;
+                }
+                for (int zb = zs; zb <= zl; zb += 6) {  // zl - zs + 1 is a multiple of 6
+                    step(zb, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, bpc);
+                    step(zb + 1, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, bpc);
+                    step(zb + 2, std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{}, bpc);
+                    step(zb + 3, std::integral_constant<int, 1>{}, std::integral_constant<int, 3>{}, bpc);
+                    step(zb + 4, std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{}, bpc);
+                    step(zb + 5, std::integral_constant<int, 1>{}, std::integral_constant<int, 5>{}, bpc);
                 }
             };
             if (MODE == kRbgs && ((a.zoff + zs + y0 + K + wv + a.h0) & 1))
@@ -646,9 +728,11 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             }
         }
     } else {
-        // the halo wave in its own (not inlined) function, so that its
-        // registers are allocated apart from the row waves'
-        tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F>(a, smem, z0, z1, y0, xs);
+        // the halo wave (see tbr_halo_wave_call)
+        if constexpr (K == 4)
+            tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
+        else
+            tbr_halo_wave_call<K, NWR, RPW, PRE, PD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
     }
     if (MODE == kRbgs && a.maxc) {
         __shared__ float red[NIT][NWR + 1];
@@ -666,7 +750,10 @@ struct TbrShape {
     bool autopick;  // candidate for rows == 0
     int rows() const { return nwr * rpw + 2 - 2 * K; }
 };
-// (4, 11, 2) spills 9 VGPRs at 168 and runs slower than (4, 7, 3): explicit only.
+// K = 4: (4, 11, 2) -- 16 output rows, one round of 256 workgroups at 1024^2 --
+// with the phi rows by LDS-DMA and the rhs by register prefetch, 161 VGPRs:
+// 2.87 ms per pass at 1024^3 (r02), against 3.07 for (4, 10, 2) (292 tiles, a
+// partial second round) and 4.0-4.2 for (4, 7, 3) (two waves per SIMD).
 // K = 2 shapes serve the red-black GS passes (one iteration per pass); r01 at
 // 1024^3: 20 rows 2.48 ms, 18 rows 2.51 ms, 28 rows 2.60 ms per iteration.
 // (2, 9, 2): 16-row GS tiles, 256 workgroups at 1024^2 -- one full round;
@@ -674,7 +761,7 @@ struct TbrShape {
 // K = 3 shapes also serve the red-black GS (three half-sweeps, 1.5 iterations,
 // per pass: the r02 default); K = 1 only its rollback of one half-sweep.
 constexpr TbrShape kShapes[] = {{3, 11, 2, true}, {3, 10, 2, true}, {3, 7, 3, false},
-                                {4, 7, 3, true}, {4, 11, 2, false}, {4, 10, 2, false}, {2, 11, 2, true},
+                                {4, 7, 3, false}, {4, 11, 2, true}, {4, 10, 2, false}, {2, 11, 2, true},
                                 {2, 10, 2, true}, {2, 10, 3, false}, {2, 9, 2, true}, {1, 9, 2, true}};
 
 int num_cus() {
@@ -706,8 +793,8 @@ void set_cu_reserve(int n) { g_cu_reserve = n; }
 template <int MODE>
 static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStream_t s, int first = 0) {
     const int pd = jacobi3d_tb_prefetch();
-    if (first && (MODE != kJacobi || pre || pd != 1 || rows != 0 || (K != 2 && K != 3))) {
-        set_error("jacobi3d_tbr: a first pass needs Jacobi, raw div, prefetch 1, auto tiles, 2 or 3 levels");
+    if (first && (MODE != kJacobi || pre || pd != 1 || rows != 0 || K < 2)) {
+        set_error("jacobi3d_tbr: a first pass needs Jacobi, raw div, prefetch 1, auto tiles, 2..4 levels");
         return CFD_E_INVALID;
     }
     const int L = a.ze - a.zb;
@@ -782,8 +869,8 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
         case 1 * 100 + 9 * 10 + 2: if constexpr (MODE == kRbgs) CFD_TBR(1, 9, 2); break;
         case 3 * 100 + 7 * 10 + 3: if constexpr (MODE == kJacobi) CFD_TBR(3, 7, 3); break;
         case 4 * 100 + 7 * 10 + 3: CFD_TBR(4, 7, 3); break;
-        case 4 * 100 + 11 * 10 + 2: CFD_TBR(4, 11, 2); break;
-        case 4 * 100 + 10 * 10 + 2: if constexpr (MODE == kJacobi) CFD_TBR(4, 10, 2); break;
+        case 4 * 100 + 11 * 10 + 2: CFD_TBRF(4, 11, 2); break;
+        case 4 * 100 + 10 * 10 + 2: CFD_TBR(4, 10, 2); break;
         case 2 * 100 + 11 * 10 + 2: CFD_TBRF(2, 11, 2); break;
         case 2 * 100 + 10 * 10 + 2: CFD_TBRF(2, 10, 2); break;
         case 2 * 100 + 9 * 10 + 2: CFD_TBRF(2, 9, 2); break;

@@ -533,9 +533,9 @@ static bool jacobi3d_first_ok(const float *rhs_ws, bool vec_ok, int nz, int ny, 
            ny >= 3 && iters >= 2 && aligned16(rhs_ws);
 }
 
-// The blocked solve with a fused first pass of k1 = 2 or 3 sweeps (k1 =
-// iters mod K when that is 2 or 3, so the passes of K that follow need no
-// shorter remainder pass), then passes of K, any remainder last.  zero: phi
+// The blocked solve with a fused first pass of k1 = 2..4 sweeps (k1 =
+// iters mod K when that is 2 or 3, K when it is 0, so the passes of K that
+// follow need no shorter remainder pass), then passes of K, any remainder last.  zero: phi
 // starts as zeros (its boundary ring zeroed here in both arrays; nothing of
 // phi is read), and the first pass writes the array that makes the last
 // pass land in phi -- no zero fill, no RHS prologue, no final copy.  Else phi
@@ -546,7 +546,7 @@ static int jacobi3d_blocked_solve(const float *div, float *phi, float *phi_tmp, 
     int rc;
     const int K = jacobi3d_tb_levels();
     const int r = iters % K;
-    int k1 = (r == 2 || r == 3) ? r : (K < 3 ? K : 3);
+    int k1 = (r == 2 || r == 3) ? r : r == 0 ? K : (K < 3 ? K : 3);
     if (k1 > iters) k1 = iters;
     const int rest = iters - k1;
     const int npass = 1 + (rest + K - 1) / K;
