@@ -66,6 +66,8 @@ PROTOTYPES = {
     "cfd_comm_init_local": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "cfd_slab_jacobi3d_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                       c_int, c_double, c_float, c_int, c_int, P, P]),
+    "cfd_slab_jacobi3d_zero_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                           c_int, c_double, c_float, c_int, c_int, P, P]),
     "cfd_slab_cu_partition": (c_int, [c_int, c_int, P, P, c_int]),
     "cfd_jacobi3d_sweep_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_double,
                                        c_float, P, P]),

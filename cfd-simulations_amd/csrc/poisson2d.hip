@@ -15,6 +15,8 @@
 //  (f32(dx^2)*div)/dt is recomputed in-register from div every sweep: the same
 //  4 B of traffic as reading a precomputed rhs array, bit-identical to NumPy,
 //  and no prologue pass or workspace.
+#include <utility>
+
 #include "internal.hpp"
 
 namespace cfd {
@@ -226,6 +228,17 @@ __device__ inline T jac5(T E, T W, T N, T S, T d, T dx2, T dtv, bool pre) {
     return T(0.25) * (s - rhs);
 }
 
+// f(integral_constant<int, I>) for I in the sequence, in order
+template <int... I, class F>
+__device__ inline void static_for(std::integer_sequence<int, I...>, F &&f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+constexpr int gcd_c(int a, int b) { return b ? gcd_c(b, a % b) : a; }
+// steps per unrolled group of jacobi2d_tbk: lcm(3, K) (level-0 / level rows
+// rotate through 3 slots, rhs rows through K)
+template <int K>
+constexpr int kTbkUnroll = 3 * K / gcd_c(3, K);
+
 template <typename T, int VEC, int K, bool PRE, bool MASK>
 __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T *__restrict__ out,
                                                     const T *__restrict__ div,
@@ -248,8 +261,15 @@ __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T 
     const bool writer = lane >= HL && lane < 64 - HL && valid;
     auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
     auto inrow = [&](int y) { return valid && y >= 0 && y <= ny - 1; };
-    T Q[K][3][VEC];  // Q[l][i][k]: level l of row (r - l) - 1 + i
-    T R[K][VEC];     // R[j]: rhs of row r - j
+    // Register queues without moves: level l of row q lives in slot
+    // (q - rs) mod 3 of Q[l], the rhs / mask of row q in slot (q - rs) mod K
+    // of R / M, and the march is unrolled by U = lcm(3, K) steps so that every
+    // slot is a compile-time constant (the shifting queues' moves were a fifth
+    // of the VALU instructions at K = 8).  Chunks run whole groups of U steps
+    // (the launcher sizes them so; steps past a chunk store nothing).
+    constexpr int U = kTbkUnroll<K>;
+    T Q[K][3][VEC];  // Q[l][s][k]: level l of a row in slot s
+    T R[K][VEC];     // rhs of a row in slot s
     uint8_t M[K][VEC];
 #pragma unroll
     for (int l = 0; l < K; ++l)
@@ -260,21 +280,24 @@ __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T 
         }
     const int rs = y0 - K + 1;  // first front row
     const int rl = y1 + K - 2;  // last front row
+    const int nsteps = U * ((rl - rs + U) / U);
+    // level 0 of rows rs - 1, rs, rs + 1: slots 2, 0, 1 (rhs rows before rs
+    // only feed the pipeline fill, whose rows no output needs, so they stay 0)
+    if (inrow(rs - 1)) ld<T, VEC>(in + row(rs - 1), Q[0][2]);
+    if (inrow(rs)) ld<T, VEC>(in + row(rs), Q[0][0]);
+    if (inrow(rs + 1)) ld<T, VEC>(in + row(rs + 1), Q[0][1]);
+    if (inrow(rs)) {
+        ld<T, VEC>(div + row(rs), R[0]);
+        if (MASK) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-        if (inrow(rs - 1 + i)) ld<T, VEC>(in + row(rs - 1 + i), Q[0][i]);
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        if (inrow(rs - j)) {
-            ld<T, VEC>(div + row(rs - j), R[j]);
-            if (MASK) {
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) M[j][k] = mask[row(rs - j) + k];
-            }
+            for (int k = 0; k < VEC; ++k) M[0][k] = mask[row(rs) + k];
         }
     }
-    for (int r = rs; r <= rl; ++r) {
-        // prefetch: level 0 of row r+2, rhs / mask of row r+1 (next step's)
+    auto step = [&](int r, auto rotc) {
+        constexpr int RT = decltype(rotc)::value;  // (r - rs) mod U
+        constexpr int S2 = (RT + 2) % 3;  // level-0 slot of row r + 2
+        // prefetch: level 0 of row r + 2 (into the slot of row r - 1, read by
+        // level 1 below first), rhs / mask of row r + 1 (next step's)
         T nq[VEC], nd[VEC];
         uint8_t nm[VEC];
 #pragma unroll
@@ -291,58 +314,42 @@ __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T 
         for (int l = 1; l <= K; ++l) {
             const int p = r - l + 1;
             const bool fixed = p == 0 || p == ny - 1;
-            const T wl = dpp_from_lower(Q[l - 1][1][VEC - 1]);
-            const T er = dpp_from_upper(Q[l - 1][1][0]);
+            // slots: level l-1 at rows p (C), p + 1 (N), p - 1 (S); the rhs of row p
+            const int sc = ((RT - l + 1) % 3 + 3) % 3, sn = ((RT - l + 2) % 3 + 3) % 3,
+                      ss = ((RT - l) % 3 + 3) % 3, sr = ((RT - l + 1) % K + K) % K;
+            const T *C = l == 1 ? Q[0][sc] : Q[l - 1][sc];
+            const T *Nn = l == 1 ? Q[0][sn] : Q[l - 1][sn];
+            const T *Ss = l == 1 ? Q[0][ss] : Q[l - 1][ss];
+            const T wl = dpp_from_lower(C[VEC - 1]);
+            const T er = dpp_from_upper(C[0]);
             T v[VEC];
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
-                const T E = (k + 1 < VEC) ? Q[l - 1][1][k + 1] : er;
-                const T W = (k > 0) ? Q[l - 1][1][k - 1] : wl;
+                const T E = (k + 1 < VEC) ? C[k + 1] : er;
+                const T W = (k > 0) ? C[k - 1] : wl;
                 const int x = x0 + k;
-                T val = (fixed || x <= 0 || x >= nx - 1)
-                            ? Q[l - 1][1][k]
-                            : jac5<T>(E, W, Q[l - 1][2][k], Q[l - 1][0][k], R[l - 1][k], dx2, dtv, PRE);
-                if (MASK && M[l - 1][k]) val = T(0);
+                T val = (fixed || x <= 0 || x >= nx - 1) ? C[k]
+                                                         : jac5<T>(E, W, Nn[k], Ss[k], R[sr][k], dx2, dtv, PRE);
+                if (MASK && M[sr][k]) val = T(0);
                 v[k] = val;
             }
             if (l < K) {
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    Q[l][0][k] = Q[l][1][k];
-                    Q[l][1][k] = Q[l][2][k];
-                    Q[l][2][k] = v[k];
-                }
+                for (int k = 0; k < VEC; ++k) Q[l][sc][k] = v[k];  // over row p - 3 of level l, dead
             } else if (writer && p >= y0 && p < y1) {
                 st<T, VEC>(out + row(p), v);
             }
         }
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            Q[0][0][k] = Q[0][1][k];
-            Q[0][1][k] = Q[0][2][k];
-            Q[0][2][k] = nq[k];
+            Q[0][S2][k] = nq[k];  // row r + 2 over row r - 1 (dead after level 1)
+            R[(RT + 1) % K][k] = nd[k];
+            M[(RT + 1) % K][k] = nm[k];
         }
-#pragma unroll
-        for (int j = K - 1; j > 0; --j)
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                R[j][k] = R[j - 1][k];
-                M[j][k] = M[j - 1][k];
-            }
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            R[0][k] = nd[k];
-            M[0][k] = nm[k];
-        }
-    }
+    };
+    for (int rb = rs; rb < rs + nsteps; rb += U)
+        static_for(std::make_integer_sequence<int, U>{}, [&](auto i) { step(rb + decltype(i)::value, i); });
 }
-
-// Waves run in one round when the grid allows: the row chunk is sized so
-// nseg x nchunk waves fit the chip at the kernel's occupancy (a second,
-// partial round would leave most SIMDs idle while it drains), but never below
-// 2 (K-1) rows.
-// r01 8192^2 f64 K=8 (3 waves/SIMD): 41 chunks of 200 rows x 74 segments =
-// 3034 waves in one round, against 74 chunks of 112 rows (two rounds).
 template <typename T, int VEC, int K, bool PRE, bool MASK>
 static void jacobi2d_tbk_launch(const T *in, T *out, const T *div, const uint8_t *mask, int ny,
                                 int nx, T dx2, T dtv, hipStream_t s) {
@@ -372,6 +379,10 @@ static void jacobi2d_tbk_launch(const T *in, T *out, const T *div, const uint8_t
     // march (large grids get long chunks from the round sizing anyway)
     const int rmin = 2 * (K - 1);
     if (rpc < rmin) rpc = rmin;
+    // whole groups of U steps per chunk (rpc + 2K - 2 steps): no step wasted
+    // but in the last chunk
+    constexpr int U = kTbkUnroll<K>;
+    rpc = U * ceil_div(rpc + 2 * K - 2, U) - (2 * K - 2);
     nchunk = ceil_div(rows, rpc);
     const int blocks = ceil_div((long)nseg * nchunk, wpb);
     hipLaunchKernelGGL((jacobi2d_tbk<T, VEC, K, PRE, MASK>), dim3(blocks), dim3(wpb * 64), 0, s, in,

@@ -42,7 +42,7 @@ __global__ void fix_faces3d(const float *__restrict__ src, float *__restrict__ d
             size_t c;
             if (full) c = (size_t)z * plane + k;
             else c = (size_t)z * plane + (k < (size_t)nx ? k : (size_t)(ny - 1) * nx + (k - nx));
-            float v = src[c];
+            float v = src ? src[c] : 0.f;  // src NULL: zero the faces
             if (mask && mask[c]) v = 0.f;
             dst[c] = v;
         }

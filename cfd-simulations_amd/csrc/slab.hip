@@ -366,22 +366,23 @@ int cfd_comm_destroy(void *comm) {
     return CFD_OK;
 }
 
-int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
-                          float *rhs_ws, const uint8_t *mask, int nz_local, int ghost, int ny,
-                          int nx, int lo_peer, int hi_peer, int z_update_begin, int z_update_end,
-                          double h, float dt, int iters, int overlap, void *stream,
-                          void *comm_stream) {
-    SlabComm *c = reinterpret_cast<SlabComm *>(comm);
-    CFD_REQUIRE(c && div && phi && phi_tmp, "slab_jacobi3d: null pointer");
-    CFD_REQUIRE(ghost >= 1 && ghost <= 4, "slab_jacobi3d: ghost depth must be 1..4");
-    CFD_REQUIRE(nz_local >= ghost && ny >= 1 && nx >= 1 && iters >= 0, "slab_jacobi3d: bad shape");
-    const int G = ghost;
-    CFD_REQUIRE(z_update_begin >= G && z_update_end <= nz_local + G &&
-                    z_update_begin <= z_update_end,
-                "slab_jacobi3d: update range [%d,%d) outside owned planes %d..%d", z_update_begin,
-                z_update_end, G, nz_local + G - 1);
-    CFD_REQUIRE(lo_peer < c->nranks && hi_peer < c->nranks, "slab_jacobi3d: bad peer");
-    if (iters == 0) return CFD_OK;
+// The slab Jacobi solve (cfd_slab_jacobi3d_f32 / _zero_f32).  zero: phi starts
+// as zeros (every rank's, ghosts included), so nothing of phi is read before
+// the first pass writes it: no fill, no initial ghost exchange.  With a
+// workspace and the blocked kernels, the first pass of each plane range is the
+// fused one (jacobi3d_tbr_first_pass: raw div in, rhs of its planes out); the
+// planes outside the update range (ghosts, global Dirichlet planes) get theirs
+// from the RHS kernel, which the pass' halo levels read.
+static int slab_jacobi3d(SlabComm *c, const float *div, float *phi, float *phi_tmp, float *rhs_ws,
+                         const uint8_t *mask, int nz_local, int G, int ny, int nx, int lo_peer,
+                         int hi_peer, int z_update_begin, int z_update_end, double h, float dt,
+                         int iters, int overlap, void *stream, void *comm_stream, bool zero) {
+    const int ghost = G;
+    if (iters == 0) {
+        if (zero) CFD_CHECK_HIP(hipMemsetAsync(phi, 0, sizeof(float) * (size_t)(nz_local + 2 * G) * ny * nx,
+                                               as_stream(stream)));
+        return CFD_OK;
+    }
     hipStream_t s = as_stream(stream);
     hipStream_t cs = comm_stream ? as_stream(comm_stream) : s;
     PartitionScope part(c, overlap && (lo_peer >= 0 || hi_peer >= 0) &&
@@ -395,33 +396,70 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
     // Ghost planes arrive whole from the neighbours.
     const int full_lo = z_update_begin > G ? G : -1;
     const int full_hi = z_update_end < nz_local + G ? nz_local + G - 1 : -1;
-    if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
-        return rc;
-    const bool pre = rhs_ws != nullptr;
-    const float *src = div;
-    if (pre) {
-        if ((rc = launch_rhs_f32(div, rhs_ws, plane * nzt, h2, dt, s))) return rc;
-        src = rhs_ws;
-    }
-    if (c->grp && (rc = register_local(c, phi, phi_tmp, nullptr, nz_local, G, plane))) return rc;
-    // ghosts of the initial guess
-    if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
     const int zb = z_update_begin, ze = z_update_end;
-    const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(src);
+    const bool pre = rhs_ws != nullptr;
+    const bool vec_ok = nx % 4 == 0 && aligned16(phi) && aligned16(phi_tmp) && aligned16(div) &&
+                        (!pre || aligned16(rhs_ws));
     // k sweeps per pass need k-deep ghosts (and no mask): k = min(G, configured levels)
     const bool tb = G >= 2 && jacobi3d_tb_enabled() && !mask && vec_ok && ny >= 3;
     const int K = tb ? (jacobi3d_tb_levels() < G ? jacobi3d_tb_levels() : G) : 1;
+    // the fused first pass (see above); its depth k1 makes the later passes
+    // whole passes of K where it can (as in the single-GPU blocked solve)
+    const bool first = pre && K >= 2 && jacobi3d_tb_prefetch() == 1 && iters >= 2;
+    int k1 = K;
+    if (first) {
+        const int r = iters % K;
+        k1 = (r == 2 || r == 3) ? r : r == 0 ? K : (K < 3 ? K : 3);
+        if (k1 > iters) k1 = iters;
+    }
+    const int npass = first ? 1 + (iters - k1 + K - 1) / K : (iters + K - 1) / K;
+    if (zero && !first) {  // the zero fill, then the general solve
+        CFD_CHECK_HIP(hipMemsetAsync(phi, 0, sizeof(float) * plane * nzt, s));
+        zero = false;
+    }
+    if (zero) {
+        // phi = zeros: the Dirichlet faces of both buffers are zero, phi is
+        // never read, and the first pass writes the buffer that makes the
+        // last pass land in phi
+        if ((rc = launch_fix_faces3d(nullptr, phi, nullptr, ny, nx, G, nz_local + G, full_lo, full_hi, s)) ||
+            (rc = launch_fix_faces3d(nullptr, phi_tmp, nullptr, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
+            return rc;
+    } else if ((rc = launch_fix_faces3d(phi, phi_tmp, mask, ny, nx, G, nz_local + G, full_lo, full_hi, s))) {
+        return rc;
+    }
+    const float *src = div;
+    if (pre) {
+        if (first) {  // planes the first pass does not own: ghosts, global Dirichlet planes
+            if ((rc = launch_rhs_f32(div, rhs_ws, plane * zb, h2, dt, s)) ||
+                (rc = launch_rhs_f32(div + plane * ze, rhs_ws + plane * ze, plane * (nzt - ze), h2, dt, s)))
+                return rc;
+        } else if ((rc = launch_rhs_f32(div, rhs_ws, plane * nzt, h2, dt, s))) {
+            return rc;
+        }
+        src = rhs_ws;
+    }
+    if (c->grp && (rc = register_local(c, phi, phi_tmp, nullptr, nz_local, G, plane))) return rc;
+    // ghosts of the initial guess (a zero start reads none)
+    if (!zero && (rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
     const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
     // owned planes a neighbour needs after each pass: the G next to it
     const bool lo_b = lo_peer >= 0, hi_b = hi_peer >= 0;
     const bool can_overlap = overlap && (lo_peer >= 0 || hi_peer >= 0) && (ze - zb) >= 2 * G + 1;
     float *a = phi, *b = phi_tmp;
+    if (zero && npass % 2 == 1) {
+        a = phi_tmp;
+        b = phi;
+    }
     const int tk = timing_begin(s);
     int done = 0;
     while (done < iters) {
-        const int k = iters - done < K ? iters - done : K;
+        const int k = done == 0 && first ? k1 : iters - done < K ? iters - done : K;
         auto run = [&](int z0, int z1) -> int {
             if (z1 <= z0) return CFD_OK;
+            if (done == 0 && first)
+                return jacobi3d_tbr_first_pass(k, b, div, rhs_ws, a, nzt, ny, nx, z0, z1,
+                                               z0 == zb && fixed_lo, z1 == ze && fixed_hi, h2, dt,
+                                               jacobi3d_tb_zchunk(), zero, s);
             if (k == 1)
                 return jacobi3d_sweep(a, b, src, mask, nzt, ny, nx, z0, z1, h2, dt, pre, nullptr, s);
             return jacobi3d_blocked_pass(k, a, b, src, nzt, ny, nx, z0, z1, z0 == zb && fixed_lo,
@@ -453,7 +491,7 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
             CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
         }
         // after the first pass, the other buffer gets the final owned faces too
-        if (done == 0 &&
+        if (done == 0 && !zero &&
             (rc = launch_fix_faces3d(phi_tmp, phi, nullptr, ny, nx, G, nz_local + G, full_lo, full_hi, s)))
             return rc;
         done += k;
@@ -465,6 +503,43 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
     if (a != phi)
         CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(float) * plane * nzt, hipMemcpyDeviceToDevice, s));
     return CFD_OK;
+}
+
+int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
+                          float *rhs_ws, const uint8_t *mask, int nz_local, int ghost, int ny,
+                          int nx, int lo_peer, int hi_peer, int z_update_begin, int z_update_end,
+                          double h, float dt, int iters, int overlap, void *stream,
+                          void *comm_stream) {
+    SlabComm *c = reinterpret_cast<SlabComm *>(comm);
+    CFD_REQUIRE(c && div && phi && phi_tmp, "slab_jacobi3d: null pointer");
+    CFD_REQUIRE(ghost >= 1 && ghost <= 4, "slab_jacobi3d: ghost depth must be 1..4");
+    CFD_REQUIRE(nz_local >= ghost && ny >= 1 && nx >= 1 && iters >= 0, "slab_jacobi3d: bad shape");
+    const int G = ghost;
+    CFD_REQUIRE(z_update_begin >= G && z_update_end <= nz_local + G &&
+                    z_update_begin <= z_update_end,
+                "slab_jacobi3d: update range [%d,%d) outside owned planes %d..%d", z_update_begin,
+                z_update_end, G, nz_local + G - 1);
+    CFD_REQUIRE(lo_peer < c->nranks && hi_peer < c->nranks, "slab_jacobi3d: bad peer");
+    if (iters == 0) return CFD_OK;
+    return slab_jacobi3d(c, div, phi, phi_tmp, rhs_ws, mask, nz_local, G, ny, nx, lo_peer, hi_peer,
+                         z_update_begin, z_update_end, h, dt, iters, overlap, stream, comm_stream, false);
+}
+
+int cfd_slab_jacobi3d_zero_f32(void *comm, const float *div, float *phi, float *phi_tmp,
+                               float *rhs_ws, int nz_local, int ghost, int ny, int nx, int lo_peer,
+                               int hi_peer, int z_update_begin, int z_update_end, double h, float dt,
+                               int iters, int overlap, void *stream, void *comm_stream) {
+    SlabComm *c = reinterpret_cast<SlabComm *>(comm);
+    CFD_REQUIRE(c && div && phi && phi_tmp, "slab_jacobi3d_zero: null pointer");
+    CFD_REQUIRE(ghost >= 1 && ghost <= 4, "slab_jacobi3d_zero: ghost depth must be 1..4");
+    CFD_REQUIRE(nz_local >= ghost && ny >= 1 && nx >= 1 && iters >= 0, "slab_jacobi3d_zero: bad shape");
+    CFD_REQUIRE(z_update_begin >= ghost && z_update_end <= nz_local + ghost &&
+                    z_update_begin <= z_update_end,
+                "slab_jacobi3d_zero: update range [%d,%d) outside owned planes %d..%d", z_update_begin,
+                z_update_end, ghost, nz_local + ghost - 1);
+    CFD_REQUIRE(lo_peer < c->nranks && hi_peer < c->nranks, "slab_jacobi3d_zero: bad peer");
+    return slab_jacobi3d(c, div, phi, phi_tmp, rhs_ws, nullptr, nz_local, ghost, ny, nx, lo_peer, hi_peer,
+                         z_update_begin, z_update_end, h, dt, iters, overlap, stream, comm_stream, true);
 }
 
 // Distributed red-black GS (config 5).  Colours are global: local plane k is

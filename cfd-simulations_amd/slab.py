@@ -217,9 +217,17 @@ class SlabJacobi3D:
         self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1)
 
     def solve(self, iters: int, overlap: bool = True, zero_phi: bool = True):
+        p = self.plan
+        if zero_phi and self.mask is None:
+            # phi = zeros (v5.py:337) inside the solve: the first pass starts
+            # from the zeros and forms the RHS workspace (cfd_slab_jacobi3d_zero_f32)
+            call("cfd_slab_jacobi3d_zero_f32", self.comm.handle, ptr(self.div), ptr(self.phi), ptr(self.tmp),
+                 ptr(self.rhs), p.nz_local, p.ghost, self.ny, self.nx, p.lo_peer, p.hi_peer, p.z_update_begin,
+                 p.z_update_end, self.h, float(self.dt), int(iters), int(bool(overlap)), stream_handle(),
+                 self.comm_stream.cuda_stream)
+            return self.phi
         if zero_phi:
             self.phi.zero_()
-        p = self.plan
         call("cfd_slab_jacobi3d_f32", self.comm.handle, ptr(self.div), ptr(self.phi), ptr(self.tmp),
              ptr(self.rhs), ptr(self.mask), p.nz_local, p.ghost, self.ny, self.nx, p.lo_peer, p.hi_peer,
              p.z_update_begin, p.z_update_end, self.h, float(self.dt), int(iters), int(bool(overlap)),

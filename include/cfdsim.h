@@ -234,6 +234,14 @@ int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_t
                           int nx, int lo_peer, int hi_peer, int z_update_begin, int z_update_end,
                           double h, float dt, int iters, int overlap, void *stream,
                           void *comm_stream);
+/* cfd_slab_jacobi3d_f32 from phi = zeros (v5.py:337; no mask): every rank's
+ * phi (ghosts included) is taken as zeros and never read, so there is no
+ * fill and no initial ghost exchange; with rhs_ws the first pass of each plane
+ * range forms the RHS workspace itself and the last pass lands in phi. */
+int cfd_slab_jacobi3d_zero_f32(void *comm, const float *div, float *phi, float *phi_tmp,
+                               float *rhs_ws, int nz_local, int ghost, int ny, int nx, int lo_peer,
+                               int hi_peer, int z_update_begin, int z_update_end, double h, float dt,
+                               int iters, int overlap, void *stream, void *comm_stream);
 /* CU partition of an overlapped slab solve (CFD_SLAB_COMM_CUS = reserve,
  * default 16, 0 = off): the drivers run their launches on a stream masked to
  * compute_mask and the RCCL exchange on one masked to exchange_mask, so the

@@ -67,6 +67,17 @@ for s in "$@"; do
     ab2d) step ab2d 600 bash -c 'for e in 0 1; do echo "CFD_J2_RHS_REGS=$e"; CFD_J2_RHS_REGS=$e python bench.py --workload jacobi2d_8192_f64 --no-cpu-baseline --steps 5 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
     cyl) step cyl 600 bash -c 'python scripts/cylinder_bench.py && python scripts/cylinder_bench.py --jacobi' ;;
     sq_gs) step sq_gs 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES -d gpurun_out/sq_gs -o run --output-format csv -- python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 12 --no-cpu-baseline ;;
+    sq_2d) step sq_2d 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INSTS_VALU SQ_BUSY_CYCLES -d gpurun_out/sq_2d -o run --output-format csv -- python3 bench.py --workload jacobi2d_8192_f64 --steps 1 --warmup 0 --iters 80 --no-cpu-baseline ;;
+    pmc_fetch_512) step pmc_fetch_512 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_512 -o run --output-format csv -- python3 bench.py --workload jacobi3d_512 --steps 1 --warmup 0 --iters 30 --no-cpu-baseline ;;
+    pmc_write_512) step pmc_write_512 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_512 -o run --output-format csv -- python3 bench.py --workload jacobi3d_512 --steps 1 --warmup 0 --iters 30 --no-cpu-baseline ;;
+    pmc_fetch_ch) step pmc_fetch_ch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_ch -o run --output-format csv -- python3 bench.py --workload jacobi3d_channel --steps 1 --warmup 0 --iters 30 --no-cpu-baseline ;;
+    pmc_write_ch) step pmc_write_ch 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_ch -o run --output-format csv -- python3 bench.py --workload jacobi3d_channel --steps 1 --warmup 0 --iters 30 --no-cpu-baseline ;;
+    prof512) step prof512 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof512 -o run --output-format csv -- python3 bench.py --workload jacobi3d_512 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    profch) step profch 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profch -o run --output-format csv -- python3 bench.py --workload jacobi3d_channel --steps 3 --warmup 1 --no-cpu-baseline ;;
+    benchgs_n) step benchgs_n 600 python bench.py --workload rbgs3d_1024 --steps 5 ;;
+    bench512_n) step bench512_n 600 python bench.py --workload jacobi3d_512 ;;
+    benchch_n) step benchch_n 600 python bench.py --workload jacobi3d_channel ;;
+    benchcav) step benchcav 600 python bench.py --workload cavity2d_128 --steps 50 --warmup 5 ;;
     prof_cyl) step prof_cyl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cyl -o run --output-format csv -- python3 scripts/cylinder_bench.py --steps 3 --warmup 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
