@@ -131,13 +131,14 @@ def rccl_self(a):
     s = torch.cuda.current_stream().cuda_stream
 
     def solve():
-        phi.zero_()
         if gs:
+            phi.zero_()
             call("cfd_slab_rbgs3d_f32", comm.handle, ptr(div), ptr(phi), ptr(tmp), None, nzl, G, n, n, 0, 0,
                  G, nzl + G, 100, h, h, h, float(dt), a.iters, 1e-30, ptr(ws), ptr(done),
                  int(not a.no_overlap), s, cs.cuda_stream)
         else:
-            call("cfd_slab_jacobi3d_f32", comm.handle, ptr(div), ptr(phi), ptr(tmp), ptr(rhs), None, nzl, G,
+            # phi = zeros inside the solve, as SlabJacobi3D.solve does
+            call("cfd_slab_jacobi3d_zero_f32", comm.handle, ptr(div), ptr(phi), ptr(tmp), ptr(rhs), nzl, G,
                  n, n, 0, 0, G, nzl + G, h, float(dt), a.iters, int(not a.no_overlap), s, cs.cuda_stream)
 
     solve()
