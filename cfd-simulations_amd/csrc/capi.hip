@@ -40,6 +40,8 @@ static Tuning process_defaults() {
         t.gs_rw = env_int("CFD_GS_SMALL_RW", 2) == 1 ? 1 : 2;
         t.gs_vec = env_int("CFD_GS_SMALL_VEC", 1) == 4 ? 4 : 1;
         t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;
+        const int ni = env_int("CFD_GS_SMALL_NI", t.gs_ni);
+        t.gs_ni = ni >= 1 && ni <= 4 ? ni : t.gs_ni;
         return t;
     }();
     return d;
@@ -98,6 +100,13 @@ int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec
     t.gs_rw = gs_rw ? gs_rw : d.gs_rw;
     t.gs_vec = gs_vec ? gs_vec : d.gs_vec;
     t.gs_wpb = gs_wpb ? gs_wpb : d.gs_wpb;
+    return CFD_OK;
+}
+
+int cfd_set_small2d_gs_iters(int iters_per_launch) {
+    CFD_REQUIRE(iters_per_launch >= 0 && iters_per_launch <= 4,
+                "small-grid GS iterations per launch must be 0 (default) or 1..4");
+    tuning().gs_ni = iters_per_launch ? iters_per_launch : process_defaults().gs_ni;
     return CFD_OK;
 }
 

@@ -18,8 +18,11 @@ struct Tuning {
     int j2_blocking = 0;
     // small-grid 2-D Jacobi: sweeps per launch (1..8), rows per wave, cells per lane
     int j2s_k = 4, j2s_rw = 1, j2s_vec = 1;
-    // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per workgroup
-    int gs_rw = 2, gs_vec = 1, gs_wpb = 4;
+    // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per
+    // workgroup, iterations per launch (1..4; r02 at 600 x 180, us per
+    // iteration, rows per wave 2 / 1: 2 -> 2.48 / 2.54, 3 -> 2.11 / 2.33,
+    // 4 -> 2.64 / 2.24)
+    int gs_rw = 2, gs_vec = 1, gs_wpb = 4, gs_ni = 3;
 };
 Tuning &tuning();
 

@@ -888,7 +888,7 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
                                                     const uint8_t *__restrict__ mask, int ny, int nx,
                                                     int nseg, float cx, float cy, float cd,
                                                     float dt_inv, float tol, RbgsWs *ws, int it,
-                                                    int rollback, int npairs, int niters) {
+                                                    int rollback, int niters) {
     // per-iteration maxima go to kGsSlots slot rows (slot-major, after
     // maxc[niters]) instead of one word: the workgroups' device-scope atomics
     // spread over kGsSlots addresses in different lines (same-address ones
@@ -901,27 +901,35 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
     constexpr int ND = RW + 2 * (L - 1);         // div / mask rows y0-(L-1) .. y0+RW-1+L-1
     bool stopped = false;
     if (rollback) {
-        const int c = ws->flags[1];
-        if (!((c & 1) && (c - 1) / 2 < npairs)) return;  // grid-uniform
-        if (((c - 1) / 2) & 1) {                           // pair m read phi_tmp
+        // rollback = P, the iterations per launch of the solve: the stop fell
+        // inside launch g = (c - 1) / P when it ends before the launch's last
+        // iteration; re-run its first need = c - P g iterations from the
+        // launch's input buffer (no later launch overwrote it) into its
+        // output.  One rollback launch per possible need; this one does NI.
+        const int P = rollback, c = ws->flags[1], g = (c - 1) / P, need = c - P * g;
+        const int len = min(P, niters - P * g);  // iterations launch g ran
+        if (need != NI || need >= len) return;  // grid-uniform
+        it = P * g;
+        if (g & 1) {  // launch g read phi_tmp
             float *t_ = const_cast<float *>(in);
             in = out;
             out = t_;
         }
     } else {
         // the stop test's loads are issued here but acted on after the row
-        // loads, so the latencies overlap; a pair skips when either iteration
-        // of the previous pair met the tolerance
-        // lane l < kGsSlots reads slot l of iteration it-1, lane kGsSlots+l of it-2
+        // loads, so the latencies overlap; a launch skips when any of the last
+        // four iterations met the tolerance (the previous launch's: a stop
+        // earlier than those already skipped that launch)
+        // lane l reads slot l % kGsSlots of iteration it - 1 - l / kGsSlots
+        static_assert(4 * kGsSlots == 64, "one lane per (slot, iteration)");
         const int ln = threadIdx.x & 63, sl = ln % kGsSlots, back = 1 + ln / kGsSlots;
-        const bool rd = ln < 2 * kGsSlots && it - back >= 0;
+        const bool rd = it - back >= 0;
         const float pv = rd ? *reinterpret_cast<volatile float *>(&slots[(size_t)sl * niters + it - back]) : 0.f;
-        const float p1 = wave_max(ln < kGsSlots ? pv : 0.f);
-        const float p2 = wave_max(ln < kGsSlots ? 0.f : pv);
-        // (a single-iteration launch is the odd last one: it must also skip
-        // when the stop fell on the first iteration of the pair before it, or
-        // it would overwrite that pair's input, which the rollback re-reads)
-        stopped = (it > 0 && p1 < tol) || (it > 1 && p2 < tol);
+#pragma unroll
+        for (int b = 1; b <= 4; ++b) {
+            const float pb = wave_max(back == b ? pv : 0.f);
+            stopped = stopped || (it >= b && pb < tol);
+        }
         // grid-uniform (every lane read the same words): a scalar branch, so the
         // level arrays below need no exec-masked copies (584 v_mov without it)
         stopped = __builtin_amdgcn_readfirstlane((int)stopped) != 0;
@@ -1054,12 +1062,12 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
     }
 }
 
-// Small grid: launch rbgs2d_small (NI iterations from `it`; rollback mode
-// re-runs the first iteration of the pair the stop fell in).
+// Small grid: launch rbgs2d_small (NI = 1..4 iterations from `it`; rollback
+// = P != 0: re-run the iterations of the launch of P the stop fell in).
 static void rbgs2d_small_launch(int NI, const float *in, float *out, const float *div,
                                 const uint8_t *mask, int ny, int nx, float cx, float cy, float cd,
-                                float dt_inv, float tol, RbgsWs *ws, int it, int rollback, int npairs,
-                                int niters, hipStream_t s) {
+                                float dt_inv, float tol, RbgsWs *ws, int it, int rollback, int niters,
+                                hipStream_t s) {
     // shape: output rows per wave (1 or 2) and cells per lane (1 or 4); r01 at
     // 600 x 180, us per iteration: (1, 2) 2.36, (1, 1) 2.42, (4, 2) 3.38
     const int rw = tuning().gs_rw, vec = tuning().gs_vec, wpb = tuning().gs_wpb;
@@ -1069,8 +1077,7 @@ static void rbgs2d_small_launch(int NI, const float *in, float *out, const float
         const int nseg = ceil_div(nx, (64 - 2 * HL_) * V);                                           \
         const int blocks = ceil_div((long)nseg * ceil_div(ny - 2, R), W);                            \
         hipLaunchKernelGGL((rbgs2d_small<M, N, V, R, W>), dim3(blocks), dim3(64 * W), 0, s, in, out, \
-                           div, mask, ny, nx, nseg, cx, cy, cd, dt_inv, tol, ws, it, rollback, npairs, \
-                           niters);                                                          \
+                           div, mask, ny, nx, nseg, cx, cy, cd, dt_inv, tol, ws, it, rollback, niters); \
     } while (0)
 #define CFD_GSS(M, N, V, R)                              \
     do {                                                 \
@@ -1085,11 +1092,17 @@ static void rbgs2d_small_launch(int NI, const float *in, float *out, const float
             if (rw == 1) CFD_GSS(M, N, 4, 1); else CFD_GSS(M, N, 4, 2); \
         }                                                      \
     } while (0)
-    if (mask) {
-        if (NI == 2) CFD_GSS_VR(true, 2); else CFD_GSS_VR(true, 1);
-    } else {
-        if (NI == 2) CFD_GSS_VR(false, 2); else CFD_GSS_VR(false, 1);
-    }
+#define CFD_GSS_N(M)                                   \
+    do {                                               \
+        switch (NI) {                                  \
+            case 4: CFD_GSS_VR(M, 4); break;           \
+            case 3: CFD_GSS_VR(M, 3); break;           \
+            case 2: CFD_GSS_VR(M, 2); break;           \
+            default: CFD_GSS_VR(M, 1); break;          \
+        }                                              \
+    } while (0)
+    if (mask) CFD_GSS_N(true); else CFD_GSS_N(false);
+#undef CFD_GSS_N
 #undef CFD_GSS_VR
 #undef CFD_GSS
 #undef CFD_GSS_W
@@ -1246,13 +1259,13 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
         if ((rc = fix_edge_rows<float>(phi, phi_tmp, nullptr, ny, nx, s))) return rc;
         float *a = phi, *b = phi_tmp;
         if (rbgs2d_small_grid(ny, nx)) {
-            // small grid (the v5 cylinder): two iterations per launch, a single
-            // one for an odd remainder, the rollback of a stop inside a pair
-            const int npairs = iterations / 2;
+            // small grid (the v5 cylinder): P iterations per launch (the last
+            // launch shorter), then the rollback of a stop inside a launch
+            const int P = tuning().gs_ni;
             CFD_CHECK_HIP(hipMemsetAsync(w->maxc + iterations, 0, sizeof(float) * kGsSlots * (size_t)iterations, s));
             for (int it = 0; it < iterations;) {
-                const int m = iterations - it >= 2 ? 2 : 1;
-                rbgs2d_small_launch(m, a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, 0, 0, iterations, s);
+                const int m = iterations - it >= P ? P : iterations - it;
+                rbgs2d_small_launch(m, a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, 0, iterations, s);
                 CFD_LAUNCH_CHECK();
                 it += m;
                 float *t = a; a = b; b = t;
@@ -1261,12 +1274,13 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
             hipLaunchKernelGGL(rbgs_fold_slots, dim3(ceil_div(iterations, 256)), dim3(256), 0, s, w, iterations);
             CFD_LAUNCH_CHECK();
             if ((rc = launch_rbgs_count(w, iters_done, s))) return rc;
-            if (npairs > 0) {
-                rbgs2d_small_launch(1, phi, phi_tmp, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, 0, 1,
-                                    npairs, iterations, s);
+            // one launch per possible remainder (none when no stop is possible)
+            for (int need = 1; need < P && need < iterations && tol > 0.f; ++need) {
+                rbgs2d_small_launch(need, phi, phi_tmp, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, 0, P,
+                                    iterations, s);
                 CFD_LAUNCH_CHECK();
             }
-            return launch_rbgs_copy(w, phi, phi_tmp, (size_t)ny * nx, 4, s);
+            return launch_rbgs_copy(w, phi, phi_tmp, (size_t)ny * nx, 2 * P, s);
         }
         for (int it = 0; it < iterations; ++it) {
             if ((rc = rbgs2d_tb_pass(a, b, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, w, it, s)))

@@ -303,6 +303,9 @@ int cfd_reset_tuning(void);
  * (1, or 4 = 16 bytes); red-black GS rows per wave gs_rw (1, 2), cells per lane
  * gs_vec (1, 4), waves per workgroup gs_wpb (4, 16).  0 = the default. */
 int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec, int gs_wpb);
+/* Small-grid red-black GS: iterations (colour-pair levels) fused per launch,
+ * 1..4 (0 = the default); a stop inside a launch is rolled back on the device. */
+int cfd_set_small2d_gs_iters(int iters_per_launch);
 /* Select the 3-D Jacobi kernel variant (bench / tile sweep):
  * variant 0 = auto, 1 = LDS plane tile, 2 = cache (no LDS); waves = rows per
  * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */

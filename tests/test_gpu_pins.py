@@ -372,3 +372,41 @@ def test_rbgs3d_stop_at_every_iteration(levels):
             assert np.array_equal(host(phi), ref), (c, N)
             seen.add(n_ref)
     assert len(seen) >= 10, seen
+
+
+@pytest.mark.parametrize("ni", [1, 2, 3, 4])
+@pytest.mark.parametrize("shape,masked", [((1, 2, 4), True), ((4, 2, 4), False), ((1, 1, 16), True)])
+def test_rbgs2d_small_stop_at_every_iteration(ni, shape, masked):
+    """Small-grid red-black GS with 1..4 iterations per launch: a stop at
+    every iteration of solves of N = 16 and 17 iterations (a stop inside a
+    launch is re-run from the launch's input by the rollback launch of the
+    remainder), for the kernel's shapes, with and without solid cells; the
+    count, the buffer the result lands in and every value are the oracle's."""
+    vec, rw, wpb = shape
+    call("cfd_set_small2d_shape", 0, 0, 0, rw, vec, wpb)
+    call("cfd_set_small2d_gs_iters", ni)
+    rng = np.random.default_rng(7 + ni)
+    div = rng.standard_normal((22, 40)).astype(np.float32) * np.float32(1e-2)
+    mask = (rng.random(div.shape) < 0.06) if masked else None
+    kw = dict(dx=0.1, dy=0.1, dt=np.float32(1.0), mask=mask)
+    _, _, mc = oracle.rbgs2d_maxc(div, iters=17, tol=0.0, **kw)
+    d = dev(div)
+    m = None if mask is None else dev(mask)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    seen = set()
+    for c in range(1, 18):
+        lo = mc[c - 1]
+        hi = mc[:c - 1].min() if c > 1 else np.float32(np.inf)
+        if not lo < hi:
+            continue
+        tol = float(lo) * 1.0000005 if not np.isfinite(hi) else float((np.float64(lo) + np.float64(hi)) / 2)
+        if not (lo < np.float32(tol) <= hi):
+            continue
+        for N in (16, 17):
+            ref, n_ref = oracle.rbgs2d(div, iters=N, tol=tol, **kw)
+            phi = torch.zeros_like(d)
+            K.solve_pressure_gauss_seidel_fast(phi, d, 0.1, 0.1, np.float32(1.0), m, N, tol, iters_done=done)
+            assert int(host(done)[0]) == n_ref, (c, N)
+            assert np.array_equal(host(phi), ref), (c, N)
+            seen.add(n_ref)
+    assert len(seen) >= 8, seen
