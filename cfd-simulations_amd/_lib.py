@@ -78,7 +78,7 @@ PROTOTYPES = {
                                     c_double, c_double, c_double, c_float, c_double, c_int, P, P]),
     "cfd_rbgs_init": (c_int, [P, c_int, c_double, P, P]),
     "cfd_rbgs_finish": (c_int, [P, P, P, c_size_t, P, P]),
-    "cfd_set_small2d_gs_iters": (c_int, [c_int]),
+    "cfd_set_small2d_gs_iters": (c_int, [c_int, c_int]),
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_blocking": (c_int, [c_int, c_int, c_int]),
     "cfd_get_jacobi3d_levels": (c_int, []),

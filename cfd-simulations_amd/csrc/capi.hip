@@ -40,6 +40,7 @@ static Tuning process_defaults() {
         t.gs_rw = env_int("CFD_GS_SMALL_RW", 2) == 1 ? 1 : 2;
         t.gs_vec = env_int("CFD_GS_SMALL_VEC", 1) == 4 ? 4 : 1;
         t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;
+        t.gs_wg = env_int("CFD_GS_SMALL_WG", t.gs_wg) != 0;
         const int ni = env_int("CFD_GS_SMALL_NI", t.gs_ni);
         t.gs_ni = ni >= 1 && ni <= 4 ? ni : t.gs_ni;
         return t;
@@ -103,10 +104,13 @@ int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec
     return CFD_OK;
 }
 
-int cfd_set_small2d_gs_iters(int iters_per_launch) {
+int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows) {
     CFD_REQUIRE(iters_per_launch >= 0 && iters_per_launch <= 4,
                 "small-grid GS iterations per launch must be 0 (default) or 1..4");
-    tuning().gs_ni = iters_per_launch ? iters_per_launch : process_defaults().gs_ni;
+    CFD_REQUIRE(shared_rows >= 0 && shared_rows <= 2, "small-grid GS shared_rows must be 0 (default), 1 or 2");
+    const Tuning d = process_defaults();
+    tuning().gs_ni = iters_per_launch ? iters_per_launch : d.gs_ni;
+    tuning().gs_wg = shared_rows ? shared_rows == 2 : d.gs_wg;
     return CFD_OK;
 }
 

@@ -19,10 +19,13 @@ struct Tuning {
     // small-grid 2-D Jacobi: sweeps per launch (1..8), rows per wave, cells per lane
     int j2s_k = 4, j2s_rw = 1, j2s_vec = 1;
     // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per
-    // workgroup, iterations per launch (1..4; r02 at 600 x 180, us per
-    // iteration, rows per wave 2 / 1: 2 -> 2.48 / 2.54, 3 -> 2.11 / 2.33,
-    // 4 -> 2.64 / 2.24)
-    int gs_rw = 2, gs_vec = 1, gs_wpb = 4, gs_ni = 3;
+    // workgroup, iterations per launch (1..4)
+    int gs_rw = 2, gs_vec = 1, gs_wpb = 4, gs_ni = 4;
+    // small-grid GS: rows shared in a 16-wave workgroup (rbgs2d_wg) instead of
+    // per-wave halo rows (rbgs2d_small).  r02 at 600 x 180, us per iteration
+    // by iterations per launch 2 / 3 / 4: shared 3.04 / 2.33 / 1.97; per-wave
+    // (2 rows per wave) 2.46 / 2.10 / 2.63, (1 row) 2.54 / 2.33 / 2.24
+    int gs_wg = 1;
 };
 Tuning &tuning();
 
@@ -62,6 +65,11 @@ int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float 
 int jacobi3d_tbr_first_pass(int K, float *out, const float *div, float *rhs_out, const float *in,
                             int nz, int ny, int nx, int zb, int ze, int fixed_lo, int fixed_hi,
                             float h2, float dt, int zchunk, bool zero, hipStream_t s);
+// jacobi2d_tbk.hip: one temporally blocked 2-D pass of K sweeps (T, VEC =
+// float, 4 / double, 2)
+template <typename T, int VEC>
+int jacobi2d_tbk_pass(int K, const T *in, T *out, const T *div, const uint8_t *mask, int ny, int nx,
+                      T dx2, T dtv, bool pre, hipStream_t s);
 // red-black GS workspace (declared below) passes on tall tiles
 struct RbgsWs;
 struct RbgsConsts;

@@ -15,42 +15,9 @@
 //  (f32(dx^2)*div)/dt is recomputed in-register from div every sweep: the same
 //  4 B of traffic as reading a precomputed rhs array, bit-identical to NumPy,
 //  and no prologue pass or workspace.
-#include <utility>
-
-#include "internal.hpp"
+#include "stencil2d.hpp"
 
 namespace cfd {
-
-template <typename T, int VEC>
-struct VecOf {
-    typedef T type __attribute__((ext_vector_type(VEC)));
-};
-template <typename T>
-struct VecOf<T, 1> {
-    using type = T;
-};
-
-template <typename T, int VEC>
-__device__ inline void ld(const T *p, T (&r)[VEC]) {
-    if constexpr (VEC == 1) {
-        r[0] = p[0];
-    } else {
-        typename VecOf<T, VEC>::type v = *reinterpret_cast<const typename VecOf<T, VEC>::type *>(p);
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) r[k] = v[k];
-    }
-}
-template <typename T, int VEC>
-__device__ inline void st(T *p, const T (&r)[VEC]) {
-    if constexpr (VEC == 1) {
-        p[0] = r[0];
-    } else {
-        typename VecOf<T, VEC>::type v;
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) v[k] = r[k];
-        *reinterpret_cast<typename VecOf<T, VEC>::type *>(p) = v;
-    }
-}
 
 // One Jacobi sweep over rows [1, ny-1).  Grid: waves = nseg * nchunk.
 // PRE: `div` holds the precomputed rhs = (dx2*div)/dt (same bits as in-register)
@@ -205,218 +172,7 @@ static int jacobi2d_sweep(const T *in, T *out, const T *div, const uint8_t *mask
     return CFD_OK;
 }
 
-// ---------------------------------------------------------------------------
-// Temporally blocked 2-D Jacobi: K sweeps per pass (K = 2..6, 8, 10, 12): one pass reads
-// phi^k and the rhs once and writes phi^(k+K), 12 B (f32) / 24 B (f64) per
-// cell for K cell-updates.  A wave owns 64 lanes x VEC cells, but its
-// x-segments OVERLAP by HL = ceil(K / VEC) lanes on each side: it writes only
-// the inner (64 - 2 HL) * VEC cells, so every lane runs the same code, and the
-// intermediate levels it needs near the segment edge are computed in-wave
-// (erosion: level l is exact HL*VEC - l cells deep into the halo lanes), never
-// exchanged.  Rows march with register queues, the 2-D analogue of
-// jacobi3d_tbk: at front row r, level l is computed for row r - l + 1 from
-// the level-(l-1) queue (rows p-1, p, p+1) and lane shuffles.  Every level
-// uses the single sweep's operation order and mask rule (masked cells -> 0,
-// edges included; Dirichlet rows/columns copied), so the result is
-// bit-identical to K single sweeps.
-template <typename T>
-__device__ inline T jac5(T E, T W, T N, T S, T d, T dx2, T dtv, bool pre) {
-    T s = E + W;
-    s = s + N;
-    s = s + S;
-    const T rhs = pre ? d : (dx2 * d) / dtv;
-    return T(0.25) * (s - rhs);
-}
 
-// f(integral_constant<int, I>) for I in the sequence, in order
-template <int... I, class F>
-__device__ inline void static_for(std::integer_sequence<int, I...>, F &&f) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-constexpr int gcd_c(int a, int b) { return b ? gcd_c(b, a % b) : a; }
-// steps per unrolled group of jacobi2d_tbk: lcm(3, K) (level-0 / level rows
-// rotate through 3 slots, rhs rows through K)
-template <int K>
-constexpr int kTbkUnroll = 3 * K / gcd_c(3, K);
-
-template <typename T, int VEC, int K, bool PRE, bool MASK>
-__global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T *__restrict__ out,
-                                                    const T *__restrict__ div,
-                                                    const uint8_t *__restrict__ mask, int ny,
-                                                    int nx, int nseg, int rows_per_chunk, T dx2,
-                                                    T dtv) {
-    constexpr int HL = (K + VEC - 1) / VEC;    // halo lanes per side
-    constexpr int SOUT = (64 - 2 * HL) * VEC;  // cells written per wave
-    const int lane = threadIdx.x & 63;
-    const int wpb = blockDim.x / 64;
-    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
-    const long wave = (long)bid * wpb + threadIdx.x / 64;
-    const int seg = (int)(wave % nseg);
-    const int chunk = (int)(wave / nseg);
-    const int y0 = 1 + chunk * rows_per_chunk;
-    if (y0 >= ny - 1) return;  // wave-uniform
-    const int y1 = min(y0 + rows_per_chunk, ny - 1);
-    const int x0 = seg * SOUT - HL * VEC + lane * VEC;  // this lane's first cell
-    const bool valid = x0 >= 0 && x0 < nx;
-    const bool writer = lane >= HL && lane < 64 - HL && valid;
-    auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
-    auto inrow = [&](int y) { return valid && y >= 0 && y <= ny - 1; };
-    // Register queues without moves: level l of row q lives in slot
-    // (q - rs) mod 3 of Q[l], the rhs / mask of row q in slot (q - rs) mod K
-    // of R / M, and the march is unrolled by U = lcm(3, K) steps so that every
-    // slot is a compile-time constant (the shifting queues' moves were a fifth
-    // of the VALU instructions at K = 8).  Chunks run whole groups of U steps
-    // (the launcher sizes them so; steps past a chunk store nothing).
-    constexpr int U = kTbkUnroll<K>;
-    T Q[K][3][VEC];  // Q[l][s][k]: level l of a row in slot s
-    T R[K][VEC];     // rhs of a row in slot s
-    uint8_t M[K][VEC];
-#pragma unroll
-    for (int l = 0; l < K; ++l)
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            Q[l][0][k] = Q[l][1][k] = Q[l][2][k] = R[l][k] = T(0);
-            M[l][k] = 0;
-        }
-    const int rs = y0 - K + 1;  // first front row
-    const int rl = y1 + K - 2;  // last front row
-    const int nsteps = U * ((rl - rs + U) / U);
-    // level 0 of rows rs - 1, rs, rs + 1: slots 2, 0, 1 (rhs rows before rs
-    // only feed the pipeline fill, whose rows no output needs, so they stay 0)
-    if (inrow(rs - 1)) ld<T, VEC>(in + row(rs - 1), Q[0][2]);
-    if (inrow(rs)) ld<T, VEC>(in + row(rs), Q[0][0]);
-    if (inrow(rs + 1)) ld<T, VEC>(in + row(rs + 1), Q[0][1]);
-    if (inrow(rs)) {
-        ld<T, VEC>(div + row(rs), R[0]);
-        if (MASK) {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) M[0][k] = mask[row(rs) + k];
-        }
-    }
-    auto step = [&](int r, auto rotc) {
-        constexpr int RT = decltype(rotc)::value;  // (r - rs) mod U
-        constexpr int S2 = (RT + 2) % 3;  // level-0 slot of row r + 2
-        // prefetch: level 0 of row r + 2 (into the slot of row r - 1, read by
-        // level 1 below first), rhs / mask of row r + 1 (next step's)
-        T nq[VEC], nd[VEC];
-        uint8_t nm[VEC];
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) { nq[k] = nd[k] = T(0); nm[k] = 0; }
-        if (inrow(r + 2)) ld<T, VEC>(in + row(r + 2), nq);
-        if (inrow(r + 1)) {
-            ld<T, VEC>(div + row(r + 1), nd);
-            if (MASK) {
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) nm[k] = mask[row(r + 1) + k];
-            }
-        }
-#pragma unroll
-        for (int l = 1; l <= K; ++l) {
-            const int p = r - l + 1;
-            const bool fixed = p == 0 || p == ny - 1;
-            // slots: level l-1 at rows p (C), p + 1 (N), p - 1 (S); the rhs of row p
-            const int sc = ((RT - l + 1) % 3 + 3) % 3, sn = ((RT - l + 2) % 3 + 3) % 3,
-                      ss = ((RT - l) % 3 + 3) % 3, sr = ((RT - l + 1) % K + K) % K;
-            const T *C = l == 1 ? Q[0][sc] : Q[l - 1][sc];
-            const T *Nn = l == 1 ? Q[0][sn] : Q[l - 1][sn];
-            const T *Ss = l == 1 ? Q[0][ss] : Q[l - 1][ss];
-            const T wl = dpp_from_lower(C[VEC - 1]);
-            const T er = dpp_from_upper(C[0]);
-            T v[VEC];
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const T E = (k + 1 < VEC) ? C[k + 1] : er;
-                const T W = (k > 0) ? C[k - 1] : wl;
-                const int x = x0 + k;
-                T val = (fixed || x <= 0 || x >= nx - 1) ? C[k]
-                                                         : jac5<T>(E, W, Nn[k], Ss[k], R[sr][k], dx2, dtv, PRE);
-                if (MASK && M[sr][k]) val = T(0);
-                v[k] = val;
-            }
-            if (l < K) {
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) Q[l][sc][k] = v[k];  // over row p - 3 of level l, dead
-            } else if (writer && p >= y0 && p < y1) {
-                st<T, VEC>(out + row(p), v);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            Q[0][S2][k] = nq[k];  // row r + 2 over row r - 1 (dead after level 1)
-            R[(RT + 1) % K][k] = nd[k];
-            M[(RT + 1) % K][k] = nm[k];
-        }
-    };
-    for (int rb = rs; rb < rs + nsteps; rb += U)
-        static_for(std::make_integer_sequence<int, U>{}, [&](auto i) { step(rb + decltype(i)::value, i); });
-}
-template <typename T, int VEC, int K, bool PRE, bool MASK>
-static void jacobi2d_tbk_launch(const T *in, T *out, const T *div, const uint8_t *mask, int ny,
-                                int nx, T dx2, T dtv, hipStream_t s) {
-    constexpr int HL = (K + VEC - 1) / VEC;
-    constexpr int SOUT = (64 - 2 * HL) * VEC;
-    constexpr int wpb = 4;
-    const int nseg = ceil_div(nx, SOUT);
-    const int rows = ny - 2;
-    static int slots = 0;  // resident waves per chip
-    if (slots <= 0) {
-        int nb = 0, dev = 0, ncu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jacobi2d_tbk<T, VEC, K, PRE, MASK>,
-                                                         wpb * 64, 0) != hipSuccess ||
-            hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            nb <= 0 || ncu <= 0) {
-            (void)hipGetLastError();
-            nb = 2;
-            ncu = 256;
-        }
-        slots = nb * wpb * ncu;
-    }
-    int nchunk = slots / nseg;
-    if (nchunk < 1) nchunk = 1;
-    int rpc = ceil_div(rows, nchunk);
-    // at least 2 (K-1) rows: the 2K-2 re-marched rows are at most half the
-    // march (large grids get long chunks from the round sizing anyway)
-    const int rmin = 2 * (K - 1);
-    if (rpc < rmin) rpc = rmin;
-    // whole groups of U steps per chunk (rpc + 2K - 2 steps): no step wasted
-    // but in the last chunk
-    constexpr int U = kTbkUnroll<K>;
-    rpc = U * ceil_div(rpc + 2 * K - 2, U) - (2 * K - 2);
-    nchunk = ceil_div(rows, rpc);
-    const int blocks = ceil_div((long)nseg * nchunk, wpb);
-    hipLaunchKernelGGL((jacobi2d_tbk<T, VEC, K, PRE, MASK>), dim3(blocks), dim3(wpb * 64), 0, s, in,
-                       out, div, mask, ny, nx, nseg, rpc, dx2, dtv);
-}
-
-template <typename T, int VEC>
-static int jacobi2d_tbk_pass(int K, const T *in, T *out, const T *div, const uint8_t *mask, int ny,
-                             int nx, T dx2, T dtv, bool pre, hipStream_t s) {
-    if (ny - 2 <= 0) return CFD_OK;
-#define CFD_J2K(KV, PR, M) jacobi2d_tbk_launch<T, VEC, KV, PR, M>(in, out, div, mask, ny, nx, dx2, dtv, s)
-#define CFD_J2KK(KV)                                                              \
-    do {                                                                          \
-        if (mask) {                                                               \
-            if (pre) CFD_J2K(KV, true, true); else CFD_J2K(KV, false, true);      \
-        } else {                                                                  \
-            if (pre) CFD_J2K(KV, true, false); else CFD_J2K(KV, false, false);    \
-        }                                                                         \
-    } while (0)
-    switch (K) {
-        case 2: CFD_J2KK(2); break;
-        case 3: CFD_J2KK(3); break;
-        case 4: CFD_J2KK(4); break;
-        case 5: CFD_J2KK(5); break;
-        case 6: CFD_J2KK(6); break;
-        case 10: CFD_J2KK(10); break;
-        case 12: CFD_J2KK(12); break;
-        default: CFD_J2KK(8); break;
-    }
-#undef CFD_J2KK
-#undef CFD_J2K
-    CFD_LAUNCH_CHECK();
-    return CFD_OK;
-}
 
 // K-level Jacobi for small grids (the v5 cylinder, config 1): each wave owns
 // two output rows and loads every row it needs up front (level 0 rows
@@ -1062,6 +818,172 @@ __global__ __launch_bounds__(64 * WPB) void rbgs2d_small(const float *__restrict
     }
 }
 
+// rbgs2d_small with the rows shared inside a workgroup: 16 waves stack in y,
+// each holding two rows of a 32-row tile (level 0 rows y0 - L .. y0 + 31 - L,
+// L = 2 NI colour levels), so a level is one LDS exchange of the waves' edge
+// rows and one barrier instead of every wave recomputing 2L halo rows of its
+// own (rbgs2d_small: sum over levels of 2 + 2(L - l) rows per wave).  A tile
+// writes its 32 - 2L inner rows.  x as in rbgs2d_small (one cell per lane by
+// default, HL = ceil(L / VEC) halo lanes per side).  Stop test, max|change|
+// slots, rollback: as rbgs2d_small, so the two kernels are interchangeable
+// launch for launch (same cells, operation order, counts).
+template <bool MASK, int NI, int VEC>
+__global__ __launch_bounds__(1024) void rbgs2d_wg(const float *__restrict__ in, float *__restrict__ out,
+                                                  const float *__restrict__ div,
+                                                  const uint8_t *__restrict__ mask, int ny, int nx,
+                                                  int nseg, float cx, float cy, float cd, float dt_inv,
+                                                  float tol, RbgsWs *ws, int it, int rollback,
+                                                  int niters) {
+    constexpr int WPB = 16, RW = 2, T0 = WPB * RW;
+    constexpr int L = 2 * NI;                // colour levels
+    constexpr int OUT = T0 - 2 * L;          // output rows per tile
+    constexpr int HL = (L + VEC - 1) / VEC;  // halo lanes per side
+    constexpr int SOUT = (64 - 2 * HL) * VEC;
+    constexpr int RS = 64 * VEC;  // LDS row
+    static_assert(OUT >= 2, "too many levels for the tile");
+    __shared__ float S[2][T0][RS];  // level parity, tile row
+    __shared__ float red[NI][WPB];
+    float *slots = ws->maxc + niters;
+    bool stopped = false;
+    if (rollback) {
+        const int P = rollback, c = ws->flags[1], g = (c - 1) / P, need = c - P * g;
+        const int len = min(P, niters - P * g);
+        if (need != NI || need >= len) return;  // grid-uniform
+        it = P * g;
+        if (g & 1) {
+            float *t_ = const_cast<float *>(in);
+            in = out;
+            out = t_;
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int seg = bid % nseg, tile = bid / nseg;
+    const int ytop = 1 + tile * OUT - L;  // global row of tile row 0
+    const int x0 = seg * SOUT - HL * VEC + lane * VEC;
+    const bool valid = x0 >= 0 && x0 < nx;
+    const bool writer = lane >= HL && lane < 64 - HL && valid;
+    auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
+    float A[RW][VEC], RH[RW][VEC];
+    bool U0[RW][VEC], U1[RW][VEC];
+    float mx[NI];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) mx[q] = 0.f;
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+        const int y = ytop + RW * w + j;
+        const bool in_ = valid && y >= 0 && y <= ny - 1;
+        const size_t rc = row(min(max(y, 0), ny - 1));
+        float D[VEC];
+        ld<float, VEC>(in + rc, A[j]);
+        ld<float, VEC>(div + rc, D);
+        uint32_t m4 = 0;
+        if (MASK && VEC == 4) {
+            m4 = *reinterpret_cast<const uint32_t *>(mask + rc);
+        } else if (MASK) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) m4 |= (uint32_t)mask[rc + k] << (8 * k);
+        }
+        const bool edge = y <= 0 || y >= ny - 1;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            A[j][k] = in_ ? A[j][k] : 0.f;
+            RH[j][k] = -(in_ ? D[k] : 0.f) * dt_inv;
+            const int x = x0 + k;
+            const bool ok = in_ && !edge && x >= 1 && x < nx - 1 && !(MASK && ((m4 >> (8 * k)) & 0xff));
+            const bool even = ((y + x + 1) & 1) == 0;
+            U0[j][k] = ok && even;
+            U1[j][k] = ok && !even;
+        }
+    }
+    if (!rollback) {
+        // the stop test, issued behind the row loads so that the two latencies
+        // overlap; a launch skips when any of the last four iterations met the
+        // tolerance (grid-uniform: every wave leaves before the first barrier)
+        const int ln = threadIdx.x & 63, sl = ln % kGsSlots, back = 1 + ln / kGsSlots;
+        const bool rd = it - back >= 0;
+        const float pv = rd ? *reinterpret_cast<volatile float *>(&slots[(size_t)sl * niters + it - back]) : 0.f;
+        bool stopped = false;
+#pragma unroll
+        for (int b = 1; b <= 4; ++b) {
+            const float pb = wave_max(back == b ? pv : 0.f);
+            stopped = stopped || (it >= b && pb < tol);
+        }
+        if (__builtin_amdgcn_readfirstlane((int)stopped) != 0) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&ws->flags[1], it);
+            return;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) S[0][RW * w + j][lane * VEC + k] = A[j][k];
+    __syncthreads();
+#pragma unroll
+    for (int l = 1; l <= L; ++l) {
+        const int par = (l - 1) & 1;  // colour of this level
+        const int rb = (l - 1) & 1, wb = l & 1;
+        float B[RW][VEC];
+#pragma unroll
+        for (int j = 0; j < RW; ++j) {
+            const int i = RW * w + j;  // tile row
+            // rows i - 1 / i + 1 of level l - 1: this wave's own in registers,
+            // the neighbour waves' from LDS (tile rows outside are never read:
+            // rows 0 and T0 - 1 are not updated at any level >= 1)
+            float Nn[VEC], Sv[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                Nn[k] = j + 1 < RW ? A[j + 1][k] : (i + 1 < T0 ? S[rb][i + 1][lane * VEC + k] : 0.f);
+                Sv[k] = j > 0 ? A[j - 1][k] : (i > 0 ? S[rb][i - 1][lane * VEC + k] : 0.f);
+            }
+            const float wl = dpp_from_lower(A[j][VEC - 1]);
+            const float er = dpp_from_upper(A[j][0]);
+            const bool live = i >= l && i < T0 - l;  // rows level l is defined on
+            const bool own = i >= L && i < T0 - L && ytop + i <= ny - 2;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const bool upd = live && (par ? U1[j][k] : U0[j][k]);
+                const float E = (k + 1 < VEC) ? A[j][k + 1] : er;
+                const float W = (k > 0) ? A[j][k - 1] : wl;
+                const float nv = ((cx * (E + W) + cy * (Nn[k] + Sv[k])) - RH[j][k]) * cd;
+                B[j][k] = upd ? nv : A[j][k];
+                const float ch = upd ? fabsf(nv - A[j][k]) : 0.f;
+                if (writer && own) mx[(l - 1) / 2] = fmaxf(mx[(l - 1) / 2], ch);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                A[j][k] = B[j][k];
+                S[wb][RW * w + j][lane * VEC + k] = B[j][k];
+            }
+        __syncthreads();
+    }
+    if (!stopped && writer) {
+#pragma unroll
+        for (int j = 0; j < RW; ++j) {
+            const int i = RW * w + j, y = ytop + i;
+            if (i >= L && i < T0 - L && y <= ny - 2) st<float, VEC>(out + row(y), A[j]);
+        }
+    }
+    if (rollback) return;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+        const float m = wave_max(mx[q]);
+        if (lane == 0) red[q][w] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x < NI && !stopped) {
+        const int q = threadIdx.x;
+        float b = red[q][0];
+#pragma unroll
+        for (int v = 1; v < WPB; ++v) b = fmaxf(b, red[q][v]);
+        if (b > 0.0f) atomic_max_nonneg(&slots[(size_t)(blockIdx.x % kGsSlots) * niters + it + q], b);
+    }
+}
+
 // Small grid: launch rbgs2d_small (NI = 1..4 iterations from `it`; rollback
 // = P != 0: re-run the iterations of the launch of P the stop fell in).
 static void rbgs2d_small_launch(int NI, const float *in, float *out, const float *div,
@@ -1071,6 +993,29 @@ static void rbgs2d_small_launch(int NI, const float *in, float *out, const float
     // shape: output rows per wave (1 or 2) and cells per lane (1 or 4); r01 at
     // 600 x 180, us per iteration: (1, 2) 2.36, (1, 1) 2.42, (4, 2) 3.38
     const int rw = tuning().gs_rw, vec = tuning().gs_vec, wpb = tuning().gs_wpb;
+    if (tuning().gs_wg) {  // rows shared in the workgroup (rbgs2d_wg), one cell per lane
+#define CFD_GSW(M, N)                                                                              \
+    do {                                                                                           \
+        constexpr int HL_ = 2 * N, OUT_ = 32 - 4 * N;                                              \
+        const int nseg = ceil_div(nx, 64 - 2 * HL_);                                               \
+        const int blocks = nseg * ceil_div(ny - 2, OUT_);                                          \
+        hipLaunchKernelGGL((rbgs2d_wg<M, N, 1>), dim3(blocks), dim3(1024), 0, s, in, out, div, mask, \
+                           ny, nx, nseg, cx, cy, cd, dt_inv, tol, ws, it, rollback, niters);       \
+    } while (0)
+#define CFD_GSW_N(M)                                  \
+    do {                                              \
+        switch (NI) {                                 \
+            case 4: CFD_GSW(M, 4); break;             \
+            case 3: CFD_GSW(M, 3); break;             \
+            case 2: CFD_GSW(M, 2); break;             \
+            default: CFD_GSW(M, 1); break;            \
+        }                                             \
+    } while (0)
+        if (mask) CFD_GSW_N(true); else CFD_GSW_N(false);
+#undef CFD_GSW_N
+#undef CFD_GSW
+        return;
+    }
 #define CFD_GSS_W(M, N, V, R, W)                                                                     \
     do {                                                                                             \
         constexpr int HL_ = (2 * N + V - 1) / V;                                                     \

@@ -304,8 +304,10 @@ int cfd_reset_tuning(void);
  * gs_vec (1, 4), waves per workgroup gs_wpb (4, 16).  0 = the default. */
 int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec, int gs_wpb);
 /* Small-grid red-black GS: iterations (colour-pair levels) fused per launch,
- * 1..4 (0 = the default); a stop inside a launch is rolled back on the device. */
-int cfd_set_small2d_gs_iters(int iters_per_launch);
+ * 1..4 (0 = the default); a stop inside a launch is rolled back on the device.
+ * shared_rows: 1 = each wave recomputes its halo rows (rbgs2d_small), 2 = the
+ * rows of a 16-wave workgroup are shared through LDS (rbgs2d_wg), 0 = default. */
+int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows);
 /* Select the 3-D Jacobi kernel variant (bench / tile sweep):
  * variant 0 = auto, 1 = LDS plane tile, 2 = cache (no LDS); waves = rows per
  * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */

@@ -212,6 +212,7 @@ def test_rbgs2d_small_odd_tail_stop_in_last_pair(shape):
     small-kernel shape: (cells per lane, rows per wave, waves per workgroup)."""
     vec, rw, wpb = shape
     call("cfd_set_small2d_shape", 0, 0, 0, rw, vec, wpb)
+    call("cfd_set_small2d_gs_iters", 2, 1)  # the per-wave kernel, iteration pairs
     div, tol, s = _stop_at_first_of_last_pair()
     N = s + 3
     ref, n_ref = oracle.rbgs2d(div, dx=0.1, dy=0.1, dt=np.float32(1.0), iters=N, tol=tol)
@@ -231,6 +232,7 @@ def test_rbgs2d_small_shapes_bitexact(shape, iters, tol):
     parities, odd counts."""
     vec, rw, wpb = shape
     call("cfd_set_small2d_shape", 0, 0, 0, rw, vec, wpb)
+    call("cfd_set_small2d_gs_iters", 2, 1)  # the per-wave kernel (the default shares rows)
     rng = np.random.default_rng(12)
     div = rng.standard_normal((66, 132)).astype(np.float32) * np.float32(1e-3)
     mask = rng.random(div.shape) < 0.05
@@ -375,8 +377,9 @@ def test_rbgs3d_stop_at_every_iteration(levels):
 
 
 @pytest.mark.parametrize("ni", [1, 2, 3, 4])
-@pytest.mark.parametrize("shape,masked", [((1, 2, 4), True), ((4, 2, 4), False), ((1, 1, 16), True)])
-def test_rbgs2d_small_stop_at_every_iteration(ni, shape, masked):
+@pytest.mark.parametrize("shape,masked,shared", [((1, 2, 4), True, 1), ((4, 2, 4), False, 1), ((1, 1, 16), True, 1),
+                                                 ((1, 2, 4), True, 2), ((1, 2, 4), False, 2)])
+def test_rbgs2d_small_stop_at_every_iteration(ni, shape, masked, shared):
     """Small-grid red-black GS with 1..4 iterations per launch: a stop at
     every iteration of solves of N = 16 and 17 iterations (a stop inside a
     launch is re-run from the launch's input by the rollback launch of the
@@ -384,7 +387,7 @@ def test_rbgs2d_small_stop_at_every_iteration(ni, shape, masked):
     count, the buffer the result lands in and every value are the oracle's."""
     vec, rw, wpb = shape
     call("cfd_set_small2d_shape", 0, 0, 0, rw, vec, wpb)
-    call("cfd_set_small2d_gs_iters", ni)
+    call("cfd_set_small2d_gs_iters", ni, shared)
     rng = np.random.default_rng(7 + ni)
     div = rng.standard_normal((22, 40)).astype(np.float32) * np.float32(1e-2)
     mask = (rng.random(div.shape) < 0.06) if masked else None
