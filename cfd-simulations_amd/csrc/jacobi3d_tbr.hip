@@ -728,11 +728,16 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             }
         }
     } else {
-        // the halo wave (see tbr_halo_wave_call)
+        // the halo wave (see tbr_halo_wave_call).  Its global loads are plain
+        // register loads; at K = 4 they run HPD = 2 planes ahead (the halo wave
+        // is on that step's critical path: 2.976 -> 2.891 ms per pass); at
+        // K <= 3 one plane (two: neutral for the Jacobi, -2 % for the GS,
+        // which then spills a VGPR)
+        constexpr int HPD = DMA && K == 4 ? 2 : PD;
         if constexpr (K == 4)
-            tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
+            tbr_halo_wave<K, NWR, RPW, PRE, HPD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
         else
-            tbr_halo_wave_call<K, NWR, RPW, PRE, PD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
+            tbr_halo_wave_call<K, NWR, RPW, PRE, HPD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
     }
     if (MODE == kRbgs && a.maxc) {
         __shared__ float red[NIT][NWR + 1];
