@@ -150,6 +150,31 @@ def cpu_baseline(shape, iters_total_hint, gs=False):
             "sample": desc + f"; {t:.2f} s; host has {os.cpu_count()} logical CPUs, NumPy uses 1"}
 
 
+def cpu_baseline_all_cores(shape, gs=False):
+    """The oracle's OpenMP C restatement (bit-identical to the serial one) on
+    every thread OpenMP is given here (OMP_NUM_THREADS; 16 on the GPU box's CPU
+    share): the all-core CPU comparison point for the 3-D workloads."""
+    import oracle
+    nz = min(shape[0], 256)
+    sample = (nz, shape[1], shape[2])
+    rng = np.random.default_rng(1234)
+    div = rng.standard_normal(sample, dtype=np.float32)
+    h = 1.0 / (shape[2] - 1)
+    it = 4
+    t0 = time.perf_counter()
+    if gs:
+        oracle.rbgs3d(div, dx=h, dy=h, dz=h, dt=np.float32(5e-5), iters=it, tol=GS_TOL, mt=True)
+        what = "oracle_rbgs3d_f32_mt"
+    else:
+        oracle.jacobi3d(div, h=h, dt=np.float32(5e-5), iters=it, mt=True)
+        what = "oracle_jacobi3d_f32_mt"
+    t = time.perf_counter() - t0
+    cells = (sample[0] - 2) * (sample[1] - 2) * (sample[2] - 2) * it
+    return {"value": cells / t / 1e9, "unit": "Gcell-updates/s", "cores": oracle.threads(), "kind": "port",
+            "sample": f"{sample[0]}x{sample[1]}x{sample[2]} slab of the grid, {it} iterations, {what} (C, "
+                      f"OpenMP over planes); {t:.2f} s"}
+
+
 def cavity_bench():
     """Config 1 (single GPU): LidDrivenCavitySolver.time_step() repeated; the
     pressure solve is the small-grid 2-D Jacobi kernel (4 sweeps per launch),
@@ -435,6 +460,8 @@ def main():
                                              if verified else "MISMATCH")
     if rank == 0 and world == 1 and not ARGS.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(shape, iters, gs)
+        if len(shape) == 3:
+            out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(shape, gs)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if use_slab and len(shape) == 3:
