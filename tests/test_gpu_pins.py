@@ -245,6 +245,26 @@ def test_rbgs2d_small_shapes_bitexact(shape, iters, tol):
     assert np.array_equal(host(phi), ref)
 
 
+@pytest.mark.parametrize("ni", [2, 3, 4])
+@pytest.mark.parametrize("iters,tol", [(37, 0.0), (400, 3e-5), (401, 1.5e-5)])
+def test_rbgs2d_shared_rows_cylinder_grid(ni, iters, tol):
+    """The shared-row small-grid GS (rbgs2d_wg, the default) with 2..4
+    iterations per launch on the v5 cylinder's grid shape: several tiles in
+    x and y, solid cells, counts not a multiple of the launch depth, early
+    stops of both parities."""
+    call("cfd_set_small2d_gs_iters", ni, 2)
+    rng = np.random.default_rng(31 + ni)
+    div = rng.standard_normal((180, 600)).astype(np.float32) * np.float32(1e-3)
+    mask = rng.random(div.shape) < 0.03
+    ref, n_ref = oracle.rbgs2d(div, dx=0.05, dy=0.05, dt=np.float32(1e-2), iters=iters, tol=tol, mask=mask)
+    phi = torch.zeros_like(dev(div))
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.solve_pressure_gauss_seidel_fast(phi, dev(div), 0.05, 0.05, np.float32(1e-2), dev(mask), iters, tol,
+                                       iters_done=done)
+    assert int(host(done)[0]) == n_ref
+    assert np.array_equal(host(phi), ref)
+
+
 @pytest.mark.parametrize("k,rw,vec", [(1, 1, 1), (3, 2, 1), (5, 1, 4), (8, 2, 4), (4, 2, 1)])
 def test_jacobi2d_small_shapes_bitexact(k, rw, vec):
     """The small-grid Jacobi kernel's non-default shapes (sweeps per launch
