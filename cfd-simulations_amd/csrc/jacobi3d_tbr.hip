@@ -154,6 +154,40 @@ __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S
     return make_float4(o[0], o[1], o[2], o[3]);
 }
 
+// Red-black GS pairs: in a float4 at x % 4 == 0 a colour owns the cells
+// h, h + 2 (h = 0 or 1, the same for every level of a row in a z-step, see
+// the DMA row wave); pick / other take the pair at h / 1 - h, join puts `a`
+// at h and `b` at 1 - h.
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+__device__ inline v2f_t pick2(float4 f, int h) { return h ? v2f_t{f.y, f.w} : v2f_t{f.x, f.z}; }
+__device__ inline float4 join2(v2f_t a, v2f_t b, int h) {
+    return h ? make_float4(b.x, a.x, b.y, a.y) : make_float4(a.x, b.x, a.y, b.y);
+}
+// One red-black level on a pair: C its cells' old values, O the other
+// colour's pair of the same row (E / W, with the lanes' DPP neighbours), N,
+// S, U, D the neighbour rows' / planes' pairs at the same positions, R the
+// raw div pair; level4's operation order and edge rule, so the same bits.
+__device__ inline v2f_t level2(v2f_t C, v2f_t O, float wl, float er, v2f_t N, v2f_t S, v2f_t U, v2f_t D,
+                               v2f_t R, int h, int x, int nx, bool upd, const TbrArgs &a, bool own,
+                               float &chg) {
+    if (!upd) return C;
+    const v2f_t E = h ? v2f_t{O.y, er} : v2f_t{O.x, O.y};
+    const v2f_t W = h ? v2f_t{O.x, O.y} : v2f_t{wl, O.x};
+    const v2f_t rhs = -R * a.dt_inv;
+    const v2f_t p = a.cx * (E + W);
+    const v2f_t q = a.cy * (N + S);
+    const v2f_t r = a.cz * (U + D);
+    v2f_t o = (((p + q) + r) - rhs) * a.cd;
+    const int x0 = x + h;  // the pair's cells x0, x0 + 2
+    o.x = (x0 != 0 && x0 != nx - 1) ? o.x : C.x;
+    o.y = (x0 + 2 != nx - 1) ? o.y : C.y;
+    if (own) {
+        chg = fmaxf(chg, fabsf(o.x - C.x));
+        chg = fmaxf(chg, fabsf(o.y - C.y));
+    }
+    return o;
+}
+
 }  // namespace
 
 // The halo wave of jacobi3d_tbr (see there): loads the two outermost level-0
@@ -387,10 +421,11 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // last front plane; the LDS-DMA march runs whole groups of 6 steps (the
     // extra steps at the end compute planes past the chunk and store nothing)
     const int zl0 = z1 + K - 2;
-    // register queues rotated by compile-time slots (see the DMA row wave) for
-    // the Jacobi up to 3 levels: -2.3 % per pass at K = 3; the red-black GS
-    // (two copies of the march, see march) and K = 4 spill with them
-    constexpr bool ROT = DMA && MODE == kJacobi && K <= 3;
+    // register queues rotated by compile-time slots (see the DMA row wave) up
+    // to 3 levels: -2.3 % per pass for the Jacobi at K = 3, -2.9 % for the
+    // red-black GS (whose level queues hold pairs, so its two march copies fit
+    // with them at 2 rows per wave); K = 4 spills with them
+    constexpr bool ROT = DMA && K <= 3 && (MODE == kJacobi || RPW <= 2);
     const int zl = ROT ? zs + 6 * ((zl0 - zs + 6) / 6) - 1 : zl0;
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
@@ -427,12 +462,17 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             }
             // V[j][i]: level 0 of plane z-1+i; Q[j][l][i]: level l of plane
             // (z-l)-1+i after level l is computed; Rq[j][i]: rhs of plane z-i
-            float4 V[RPW][3], Q[RPW][K][3], Rq[RPW][K];
+            // GS: Q holds only the pair a level updated (the other colour's
+            // cells keep the previous level's values, which the level below
+            // holds): half the registers of the level queues
+            using QT = std::conditional_t<MODE == kRbgs, v2f_t, float4>;
+            float4 V[RPW][3], Rq[RPW][K];
+            QT Q[RPW][K][3];
             float4 Rn[RPW];  // !RDMA: the rhs row of the next step's plane, in flight
 #pragma unroll
             for (int j = 0; j < RPW; ++j) {
 #pragma unroll
-                for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = z4;
+                for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = QT{};
                 // planes zs - 1 and zs in slots 2 and 0 (slot (q - zs) mod 3), or 0
                 // and 1 (shifted queues)
                 V[j][ROT ? 2 : 0] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]);
@@ -496,8 +536,19 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     if (xin) sts4(T(0, rr[j]) + 4 + 4 * lane, V[j][vs(0)]);
 #pragma unroll
                     for (int l = 1; l < K; ++l)
-                        if (xin && rr[j] >= l && rr[j] < NR - l)
-                            sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][ROT ? sl3(R - l) : 2]);
+                        if (xin && rr[j] >= l && rr[j] < NR - l) {
+                            if constexpr (MODE == kRbgs) {
+                                // level l of plane z - l: its own pair (computed last
+                                // step, at 1 - h) joined with level l - 1's (two steps
+                                // ago, at h) -- or level 0's
+                                const int h = (BPv ^ E ^ (j * NWR)) & 1;
+                                const v2f_t lo = l == 1 ? pick2(V[j][vs(-1)], h)
+                                                        : Q[j][l - 1][ROT ? sl3(R - l) : 1];
+                                sts4(T(l, rr[j]) + 4 + 4 * lane, join2(lo, Q[j][l][ROT ? sl3(R - l) : 2], h));
+                            } else {
+                                sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][ROT ? sl3(R - l) : 2]);
+                            }
+                        }
                 }
                 // the previous step's DMAs have landed once at most this step's
                 // 2 * RPW remain in flight (they are issued in order)
@@ -534,7 +585,54 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
                         const int r = rr[j];
-                        if (r >= l && r < NR - l) {
+                        if constexpr (MODE == kRbgs) {
+                          if (r >= l && r < NR - l) {
+                            // the colour's cells h, h + 2 of plane p: their old values
+                            // (level l - 2's pair, or level 0), the other colour's pair
+                            // of the same row (level l - 1) for E / W, level l - 1's
+                            // pairs of planes p +- 1 and rows r +- 1 (same positions)
+                            const int h = (BPv ^ E ^ (j * NWR)) & 1;
+                            const v2f_t Cp = l == 1   ? pick2(V[j][vs(0)], h)
+                                             : l == 2 ? pick2(V[j][vs(-1)], h)
+                                                      : Q[j][l - 2][qs(l - 2, 0)];
+                            const v2f_t Op = l == 1 ? pick2(V[j][vs(0)], 1 - h) : Q[j][l - 1][qs(l - 1, 1)];
+                            const v2f_t Up = l == 1 ? pick2(V[j][vs(1)], h) : Q[j][l - 1][qs(l - 1, 2)];
+                            const v2f_t Dp = l == 1 ? pick2(V[j][vs(-1)], h) : Q[j][l - 1][qs(l - 1, 0)];
+                            const float *row = T(l - 1, r);
+                            float wl = dpp_from_lower(Op.y), er = dpp_from_upper(Op.x);
+                            const float wl_l = row[3], er_l = row[260];
+                            if (lane == 0) wl = wl_l;
+                            if (lane == 63) er = er_l;
+                            v2f_t v = Cp;
+                            if (xin) {
+                                const v2f_t N = pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
+                                const v2f_t Sv = pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
+                                float lm = 0.f;
+                                v = level2(Cp, Op, wl, er, N, Sv, Up, Dp, pick2(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], h), h, x, nx,
+                                           irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, lm);
+                                fold(l, lm);
+                            }
+                            if (l < K) {
+                                if constexpr (ROT) {
+                                    Q[j][l][sl3(R - l + 1)] = v;
+                                } else {
+                                    Q[j][l][0] = Q[j][l][1];
+                                    Q[j][l][1] = Q[j][l][2];
+                                    Q[j][l][2] = v;
+                                }
+                            } else {
+                                // level K of plane p: this pair at h, level K - 1's at 1 - h
+                                const float4 f = join2(v, Op, h);
+                                const bool own = p >= z0 && p < z1;
+                                const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+                                    a.out + (size_t)(own ? p : 0) * plane, (short)0,
+                                    own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
+                                const gv4f vv = {f.x, f.y, f.z, f.w};
+                                __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, 0);
+                            }
+                            __builtin_amdgcn_sched_barrier(0);
+                          }
+                        } else if (r >= l && r < NR - l) {
                             // level l-1 at planes p (c), p + 1 (U), p - 1 (D)
                             const float4 c = l == 1 ? V[j][vs(0)] : Q[j][l - 1][qs(l - 1, 1)];
                             const float4 U = l == 1 ? V[j][vs(1)] : Q[j][l - 1][qs(l - 1, 2)];
