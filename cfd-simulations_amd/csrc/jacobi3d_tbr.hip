@@ -163,6 +163,19 @@ __device__ inline v2f_t pick2(float4 f, int h) { return h ? v2f_t{f.y, f.w} : v2
 __device__ inline float4 join2(v2f_t a, v2f_t b, int h) {
     return h ? make_float4(b.x, a.x, b.y, a.y) : make_float4(a.x, b.x, a.y, b.y);
 }
+// GS tiles (SPLIT): the 256 cells of a tile row are stored by colour pair,
+// cells 4 i + {0, 2} at 4 + 2 i and cells 4 i + {1, 3} at 132 + 2 i, so a
+// lane reads its pair as one conflict-free ds_read_b64 (the float4 layout
+// makes it a ds_read2_b32 of words 8 B apart at a 16-B lane stride: bank
+// conflicts); the x-halo columns 0..3 / 260..263 keep the plain layout, and
+// the cells next to them (xs at 4, xs + 255 at 259) land where they were.
+__device__ inline void sts4s(float *row, int lane, float4 v) {
+    *reinterpret_cast<v2f_t *>(row + 4 + 2 * lane) = v2f_t{v.x, v.z};
+    *reinterpret_cast<v2f_t *>(row + 132 + 2 * lane) = v2f_t{v.y, v.w};
+}
+__device__ inline v2f_t lds2s(const float *row, int lane, int h) {
+    return *reinterpret_cast<const v2f_t *>(row + 4 + 128 * h + 2 * lane);
+}
 // One red-black level on a pair: C its cells' old values, O the other
 // colour's pair of the same row (E / W, with the lanes' DPP neighbours), N,
 // S, U, D the neighbour rows' / planes' pairs at the same positions, R the
@@ -193,7 +206,7 @@ __device__ inline v2f_t level2(v2f_t C, v2f_t O, float wl, float er, v2f_t N, v2
 // The halo wave of jacobi3d_tbr (see there): loads the two outermost level-0
 // rows and the 4-float x-halo chunks of every row, and computes levels
 // 1..K-1 of the chunks, in lock step (two barriers per step) with the row waves.
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F>
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT>
 __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0, int z1, int y0, int xs,
                                               int zl) {
     constexpr int NR = NWR * RPW + 2;
@@ -259,8 +272,13 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
         Hq[PD - 1] = ldhp(z + 1 + PD);
         Rn[PD - 1] = ldh(a.div, z + PD);
         // phase W
-        if (elo) sts4(T(0, 0) + 4 + 4 * lane, lo);
-        if (ehi) sts4(T(0, NR - 1) + 4 + 4 * lane, hi);
+        if constexpr (SPLIT) {
+            if (elo) sts4s(T(0, 0), lane, lo);
+            if (ehi) sts4s(T(0, NR - 1), lane, hi);
+        } else {
+            if (elo) sts4(T(0, 0) + 4 + 4 * lane, lo);
+            if (ehi) sts4(T(0, NR - 1) + 4 + 4 * lane, hi);
+        }
         if (hon) {
             sts4(T(0, hr) + col, H[0][1]);
 #pragma unroll
@@ -312,10 +330,10 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
 // The halo wave as a called function (K <= 3: measured 1.5-2.5 % faster than
 // inlined there); K = 4 inlines it (as a call it takes the TbrArgs by value in
 // VGPRs and a call frame: 168-181 VGPRs, which spill).
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F>
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT>
 __device__ __noinline__ void tbr_halo_wave_call(const TbrArgs a, float *smem, int z0, int z1, int y0,
                                                 int xs, int zl) {
-    tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
+    tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F, SPLIT>(a, smem, z0, z1, y0, xs, zl);
 }
 
 // (A double-buffered, one-barrier-per-step version of the (3, 11, 2) shape --
@@ -348,6 +366,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // register load issued a step ahead (4 VGPRs per row)
     constexpr bool DMA = PD == 1 && (TOTAL + 2 * SR_ * 256) * 4 <= 160 * 1024;
     constexpr bool RDMA = DMA && (TOTAL + 4 * SR_ * 256) * 4 <= 160 * 1024;
+    // GS tiles by colour pair (sts4s): +1.2 % at K = 3; at K = 4 it spills
+    constexpr bool SPLIT = MODE == kRbgs && DMA && K <= 3;
     constexpr int SST = DMA ? SR_ * 256 : 4;
     constexpr int SSR = RDMA ? SR_ * 256 : 4;
     __shared__ __attribute__((aligned(16))) float st_p0[SST], st_p1[SST], st_r0[SSR], st_r1[SSR];
@@ -533,7 +553,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 // phase W: level 0 of plane z and level l of plane z - l
 #pragma unroll
                 for (int j = 0; j < RPW; ++j) {
-                    if (xin) sts4(T(0, rr[j]) + 4 + 4 * lane, V[j][vs(0)]);
+                    if (xin) {
+                        if constexpr (SPLIT)
+                            sts4s(T(0, rr[j]), lane, V[j][vs(0)]);
+                        else
+                            sts4(T(0, rr[j]) + 4 + 4 * lane, V[j][vs(0)]);
+                    }
 #pragma unroll
                     for (int l = 1; l < K; ++l)
                         if (xin && rr[j] >= l && rr[j] < NR - l) {
@@ -544,7 +569,11 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const int h = (BPv ^ E ^ (j * NWR)) & 1;
                                 const v2f_t lo = l == 1 ? pick2(V[j][vs(-1)], h)
                                                         : Q[j][l - 1][ROT ? sl3(R - l) : 1];
-                                sts4(T(l, rr[j]) + 4 + 4 * lane, join2(lo, Q[j][l][ROT ? sl3(R - l) : 2], h));
+                                const float4 f = join2(lo, Q[j][l][ROT ? sl3(R - l) : 2], h);
+                                if constexpr (SPLIT)
+                                    sts4s(T(l, rr[j]), lane, f);
+                                else
+                                    sts4(T(l, rr[j]) + 4 + 4 * lane, f);
                             } else {
                                 sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][ROT ? sl3(R - l) : 2]);
                             }
@@ -605,8 +634,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             if (lane == 63) er = er_l;
                             v2f_t v = Cp;
                             if (xin) {
-                                const v2f_t N = pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
-                                const v2f_t Sv = pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
+                                const v2f_t N = SPLIT ? lds2s(T(l - 1, r + 1), lane, h)
+                                                      : pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
+                                const v2f_t Sv = SPLIT ? lds2s(T(l - 1, r - 1), lane, h)
+                                                       : pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
                                 float lm = 0.f;
                                 v = level2(Cp, Op, wl, er, N, Sv, Up, Dp, pick2(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], h), h, x, nx,
                                            irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, lm);
@@ -833,9 +864,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         // which then spills a VGPR)
         constexpr int HPD = DMA && K == 4 ? 2 : PD;
         if constexpr (K == 4)
-            tbr_halo_wave<K, NWR, RPW, PRE, HPD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
+            tbr_halo_wave<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT>(a, smem, z0, z1, y0, xs, zl);
         else
-            tbr_halo_wave_call<K, NWR, RPW, PRE, HPD, MODE, F>(a, smem, z0, z1, y0, xs, zl);
+            tbr_halo_wave_call<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT>(a, smem, z0, z1, y0, xs, zl);
     }
     if (MODE == kRbgs && a.maxc) {
         __shared__ float red[NIT][NWR + 1];
