@@ -556,7 +556,9 @@ def _gather_uneven(dist, parts, mine, rank):
 
 
 def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):
-    """Config 3: time every (variant, waves, zchunk) tile on this grid."""
+    """Config 3: time every tile on this grid: the single-sweep kernel's
+    (variant, waves, zchunk), the 2-level kernel's rows, and the tall-tile
+    kernels' (levels, output rows, zchunk)."""
     import torch
     res = []
     call("cfd_set_jacobi3d_blocking", 1, 0, 0)
@@ -593,6 +595,32 @@ def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):
             per = ms.value / n.value
             res.append({"tb_rows": rows, "zchunk": zchunk, "prefetch": pf, "ms_per_sweep": round(per, 4),
                         "GBps_pass": round(cells * 12 / (2 * per) / 1e6, 1),
+                        "Gcell_per_s": round(cells / per / 1e6, 1)})
+            print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
+    # the tall-tile kernels (the default family): levels per pass x output rows
+    # per tile (the shape) x z-chunk (0: the launcher's cost model)
+    call("cfd_set_jacobi3d_prefetch", 0)
+    for lv, rows in [(3, 16), (3, 18), (3, 17), (4, 16), (4, 14), (4, 15)]:
+        for zchunk in (0, 64, 128, 256, 512):
+            call("cfd_set_jacobi3d_blocking", lv, rows, zchunk)
+            phi.zero_()
+            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 12, phi_tmp=tmp, rhs_ws=rhs)
+            torch.cuda.synchronize()
+            call("cfd_timing_enable", 1)
+            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 24, phi_tmp=tmp, rhs_ws=rhs)
+            ms = ctypes.c_double()
+            n = ctypes.c_longlong()
+            call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(n), 1)
+            call("cfd_timing_enable", 0)
+            per = ms.value / n.value
+            shape = [ctypes.c_int() for _ in range(4)]
+            call("cfd_get_last_tbr_shape", *[ctypes.byref(v) for v in shape])
+            shape = [v.value for v in shape]
+            res.append({"tbr_levels": lv, "tb_rows": rows, "zchunk": zchunk,
+                        "shape": {"levels": shape[0], "row_waves": shape[1], "rows_per_wave": shape[2],
+                                  "zchunk": shape[3]},
+                        "ms_per_sweep": round(per, 4), "ms_per_pass": round(per * lv, 4),
+                        "GBps_pass": round(cells * 12 / (lv * per) / 1e6, 1),
                         "Gcell_per_s": round(cells / per / 1e6, 1)})
             print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
     call("cfd_set_jacobi3d_blocking", ARGS.tb, ARGS.tb_rows, ARGS.tb_zchunk)
