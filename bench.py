@@ -408,8 +408,8 @@ def main():
         spl = levels if blocked else 1
     elif use_slab:  # slab passes: one iteration, two with --tb 4
         spl = 2 if blocked and ARGS.tb == 4 else 1
-    else:  # single GPU: --tb half-sweeps per pass (auto 3: one and a half iterations)
-        spl = (ARGS.tb if ARGS.tb >= 2 else 3) / 2 if blocked else 1
+    else:  # single GPU: half-sweeps per pass (--tb, or the library's auto: 4 = two iterations)
+        spl = int(lib().cfd_get_rbgs3d_levels()) / 2 if blocked else 1
     launch_ms = sweep_ms * spl
     alg_bytes = cells_rank * bpc  # one pass moves bpc bytes per cell whatever it fuses
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9

@@ -82,6 +82,7 @@ PROTOTYPES = {
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_blocking": (c_int, [c_int, c_int, c_int]),
     "cfd_get_jacobi3d_levels": (c_int, []),
+    "cfd_get_rbgs3d_levels": (c_int, []),
     "cfd_get_jacobi2d_levels": (c_int, []),
     "cfd_set_jacobi3d_prefetch": (c_int, [c_int]),
     "cfd_set_jacobi2d_blocking": (c_int, [c_int]),

@@ -113,7 +113,7 @@ int rbgs3d_colour_pass(int colour, float *phi, const float *div, const uint8_t *
                        int nx, int z0, int z1, int zoff, const RbgsConsts &k, RbgsWs *ws, int it,
                        hipStream_t s);
 int rbgs3d_iters_per_pass();  // slab solves: 1, or 2 (blocking depth 4)
-int rbgs3d_half_per_pass();   // single-GPU solves: half-sweeps per pass, 2..4 (auto 3)
+int rbgs3d_half_per_pass();   // single-GPU solves: half-sweeps per pass, 2..4 (auto 4)
 int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
                       int iters, RbgsWs *ws, hipStream_t s, int lag = 0);

@@ -450,17 +450,13 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float chg[NIT];  // GS: max|change| of own cells per iteration (h0 >> 1) + q
+    // GS: max|change| of own cells per level (a compile-time slot, one v_max
+    // per update), folded into the pass's iterations after the march
+    float chgl[MODE == kRbgs ? K : 1];
 #pragma unroll
-    for (int i = 0; i < NIT; ++i) chg[i] = 0.f;
-    // fold a level's max|change| into its iteration's slot: level l is
-    // iteration (h0 >> 1) + q(l), q(l) = ((h0 & 1) + l - 1) >> 1
+    for (int i = 0; i < (MODE == kRbgs ? K : 1); ++i) chgl[i] = 0.f;
     auto fold = [&](int l, float lm) {
-        if constexpr (MODE == kRbgs) {
-            const int q = ((a.h0 & 1) + l - 1) >> 1;
-#pragma unroll
-            for (int i = 0; i < NIT; ++i) chg[i] = q == i ? fmaxf(chg[i], lm) : chg[i];
-        }
+        if constexpr (MODE == kRbgs) chgl[l - 1] = fmaxf(chgl[l - 1], lm);
     };
 
     if (wv < NWR) {
@@ -638,10 +634,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                                       : pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
                                 const v2f_t Sv = SPLIT ? lds2s(T(l - 1, r - 1), lane, h)
                                                        : pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
-                                float lm = 0.f;
                                 v = level2(Cp, Op, wl, er, N, Sv, Up, Dp, pick2(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], h), h, x, nx,
-                                           irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, lm);
-                                fold(l, lm);
+                                           irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, chgl[l - 1]);
                             }
                             if (l < K) {
                                 if constexpr (ROT) {
@@ -869,6 +863,16 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             tbr_halo_wave_call<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT>(a, smem, z0, z1, y0, xs, zl);
     }
     if (MODE == kRbgs && a.maxc) {
+        // level l is iteration (h0 >> 1) + q(l), q(l) = ((h0 & 1) + l - 1) >> 1
+        float chg[NIT];
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) chg[i] = 0.f;
+#pragma unroll
+        for (int l = 1; l <= (MODE == kRbgs ? K : 1); ++l) {
+            const int q = ((a.h0 & 1) + l - 1) >> 1;
+#pragma unroll
+            for (int i = 0; i < NIT; ++i) chg[i] = q == i ? fmaxf(chg[i], chgl[l - 1]) : chg[i];
+        }
         __shared__ float red[NIT][NWR + 1];
 #pragma unroll
         for (int i = 0; i < NIT; ++i)  // the iterations this pass touched (workgroup-uniform)

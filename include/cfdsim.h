@@ -321,6 +321,9 @@ int cfd_set_jacobi3d_config(int variant, int waves, int zchunk);
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk);
 /* Jacobi sweeps per blocked pass currently in effect (2..4). */
 int cfd_get_jacobi3d_levels(void);
+/* Red-black GS half-sweeps (colour levels) per fused pass of a single-GPU
+ * cfd_rbgs3d_f32 solve currently in effect (2..4; auto 4 = two iterations). */
+int cfd_get_rbgs3d_levels(void);
 /* Prefetch distance of the blocked kernel in planes (0 = auto = 1, 1, 2). */
 int cfd_set_jacobi3d_prefetch(int planes);
 

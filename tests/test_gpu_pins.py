@@ -7,8 +7,8 @@ red-black GS paths reassociate nothing).
   rows> the bench runs), with and without the RHS workspace; the test asserts
   that this shape ran.
 * Config 5's kernel: 1024^3 red-black GS, 2 and 3 iterations on the default
-  16-row tile (2 levels, 9 x 2), and the explicit 16 / 18 / 20 / 28-row GS
-  tiles on a ragged grid, with an early stop.
+  16-row tile (4 levels, 11 x 2) and on the 3-level one (10 x 2), and every
+  explicit GS tile (2, 3, 4 levels) on a ragged grid, with an early stop.
 * Config 4's grid: 1024 x 1024 x 512 through SlabJacobi3D with a one-rank RCCL
   communicator (3-deep ghosts, overlap on).
 * The device powf behind the SUPG tau vs libm.
@@ -90,9 +90,11 @@ def test_jacobi3d_1024_headline_kernel_bitexact(div1024):
 
 def test_rbgs3d_1024_default_tile_bitexact(div1024):
     """Config 5's kernel at full size: 2 and 3 red-black iterations (tolerance
-    1e-8, no stop) on the default tile -- three half-sweeps per pass on the
-    16-row 3-level tile (passes of colours 0,1,0 then 1(,0,1)), phi_tmp
-    ping-pong with the result copied back on the device."""
+    1e-8, no stop) on the default tile -- four half-sweeps per pass on the
+    16-row 4-level tile (11 row waves x 2 rows; 3 iterations = a 4-level pass
+    and a 2-level one) -- and on the 3-level tile (passes of colours 0,1,0
+    then 1(,0,1)), phi_tmp ping-pong with the result copied back on the
+    device."""
     n = 1024
     h, dt = 1.0 / (n - 1), np.float32(5e-5)
     ref2, n2 = oracle.rbgs3d(div1024, dx=h, dy=h, dz=h, dt=dt, iters=2, tol=1e-8, mt=True)
@@ -102,19 +104,23 @@ def test_rbgs3d_1024_default_tile_bitexact(div1024):
     phi = torch.zeros_like(d)
     tmp = torch.empty_like(d)
     done = torch.zeros(1, dtype=torch.int32, device=DEV)
-    for iters, ref in ((2, ref2), (3, ref3)):
-        for tol in (1e-8, 0.0):  # tol 0: no stop possible, no rollback launch after the passes
-            phi.zero_()
-            K.solve_pressure_gauss_seidel3d(phi, d, h, h, h, dt, None, iters, tol, iters_done=done, phi_tmp=tmp)
-            if tol == 0.0 and iters == 3:
-                assert last_shape()[:3] == (3, 10, 2), last_shape()
-            assert int(host(done)[0]) == iters
-            assert np.array_equal(host(phi), ref), iters
+    assert int(lib().cfd_get_rbgs3d_levels()) == 4
+    for levels in (0, 3):
+        call("cfd_set_jacobi3d_blocking", levels, 0, 0)
+        for iters, ref in ((2, ref2), (3, ref3)):
+            for tol in (1e-8, 0.0):  # tol 0: no stop possible, no rollback launch after the passes
+                phi.zero_()
+                K.solve_pressure_gauss_seidel3d(phi, d, h, h, h, dt, None, iters, tol, iters_done=done,
+                                                phi_tmp=tmp)
+                if tol == 0.0 and iters == (2 if levels == 0 else 3):
+                    assert last_shape()[:3] == ((4, 11, 2) if levels == 0 else (3, 10, 2)), last_shape()
+                assert int(host(done)[0]) == iters
+                assert np.array_equal(host(phi), ref), (levels, iters)
 
 
 @pytest.mark.parametrize("levels,rows,shape", [(2, 16, (2, 9, 2)), (2, 18, (2, 10, 2)), (2, 20, (2, 11, 2)),
                                                (2, 28, (2, 10, 3)), (3, 16, (3, 10, 2)), (3, 18, (3, 11, 2)),
-                                               (4, 15, (4, 7, 3))])
+                                               (4, 15, (4, 7, 3)), (4, 16, (4, 11, 2))])
 @pytest.mark.parametrize("tol,iters", [(0.0, 6), (1.5e-5, 300)])
 def test_rbgs3d_explicit_gs_tiles_ragged(levels, rows, shape, tol, iters):
     """Every GS tile shape (half-sweeps per pass 2, 3, 4) on a ragged grid (y
