@@ -451,12 +451,18 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     // GS: max|change| of own cells per level (a compile-time slot, one v_max
-    // per update), folded into the pass's iterations after the march
-    float chgl[MODE == kRbgs ? K : 1];
+    // per update), folded into the pass's iterations after the march.  A
+    // 4-level pass always starts at an even half-sweep (the solve's passes of
+    // 4 from h0 = 0, slab passes from h0 = 2 it; rollbacks run 1 or 2
+    // levels), so there levels 1, 2 and 3, 4 are one iteration each and share
+    // a slot (2 VGPRs: no spill at 4 levels)
+    constexpr int KS = MODE == kRbgs ? (K == 4 ? 2 : K) : 1;
+    auto slot = [](int l) { return K == 4 ? (l - 1) >> 1 : l - 1; };
+    float chgl[KS];
 #pragma unroll
-    for (int i = 0; i < (MODE == kRbgs ? K : 1); ++i) chgl[i] = 0.f;
+    for (int i = 0; i < KS; ++i) chgl[i] = 0.f;
     auto fold = [&](int l, float lm) {
-        if constexpr (MODE == kRbgs) chgl[l - 1] = fmaxf(chgl[l - 1], lm);
+        if constexpr (MODE == kRbgs) chgl[slot(l)] = fmaxf(chgl[slot(l)], lm);
     };
 
     if (wv < NWR) {
@@ -635,7 +641,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const v2f_t Sv = SPLIT ? lds2s(T(l - 1, r - 1), lane, h)
                                                        : pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
                                 v = level2(Cp, Op, wl, er, N, Sv, Up, Dp, pick2(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], h), h, x, nx,
-                                           irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, chgl[l - 1]);
+                                           irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, chgl[slot(l)]);
                             }
                             if (l < K) {
                                 if constexpr (ROT) {
@@ -871,7 +877,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         for (int l = 1; l <= (MODE == kRbgs ? K : 1); ++l) {
             const int q = ((a.h0 & 1) + l - 1) >> 1;
 #pragma unroll
-            for (int i = 0; i < NIT; ++i) chg[i] = q == i ? fmaxf(chg[i], chgl[l - 1]) : chg[i];
+            for (int i = 0; i < NIT; ++i) chg[i] = q == i ? fmaxf(chg[i], chgl[slot(l)]) : chg[i];
         }
         __shared__ float red[NIT][NWR + 1];
 #pragma unroll
