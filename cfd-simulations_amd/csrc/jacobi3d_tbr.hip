@@ -173,6 +173,8 @@ __device__ inline void sts4s(float *row, int lane, float4 v) {
     *reinterpret_cast<v2f_t *>(row + 4 + 2 * lane) = v2f_t{v.x, v.z};
     *reinterpret_cast<v2f_t *>(row + 132 + 2 * lane) = v2f_t{v.y, v.w};
 }
+// pair-tile row (PT): left chunk pair | 64 lanes x pair | right chunk pair
+constexpr int kPairRow = 132;
 __device__ inline v2f_t lds2s(const float *row, int lane, int h) {
     return *reinterpret_cast<const v2f_t *>(row + 4 + 128 * h + 2 * lane);
 }
@@ -206,17 +208,17 @@ __device__ inline v2f_t level2(v2f_t C, v2f_t O, float wl, float er, v2f_t N, v2
 // The halo wave of jacobi3d_tbr (see there): loads the two outermost level-0
 // rows and the 4-float x-halo chunks of every row, and computes levels
 // 1..K-1 of the chunks, in lock step (two barriers per step) with the row waves.
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT>
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT, bool PT>
 __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0, int z1, int y0, int xs,
                                               int zl) {
     constexpr int NR = NWR * RPW + 2;
-    constexpr int RS = 264;
+    constexpr int RS = 264, RS2 = kPairRow;
     auto T = [&](int l, int r) -> float * {
         int base = 0;
 #pragma unroll
         for (int m = 0; m < K; ++m)
-            if (m < l) base += (NR - 2 * m) * RS;
-        return smem + base + (r - l) * RS;
+            if (m < l) base += (NR - 2 * m) * (PT && m ? RS2 : RS);
+        return smem + base + (r - l) * (PT && l ? RS2 : RS);
     };
     const int nz = a.nz, ny = a.ny, nx = a.nx;
     const int lane = threadIdx.x & 63;
@@ -283,7 +285,14 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
             sts4(T(0, hr) + col, H[0][1]);
 #pragma unroll
             for (int l = 1; l < K; ++l)
-                if (hr >= l && hr < NR - l) sts4(T(l, hr) + col, H[l][2]);
+                if (hr >= l && hr < NR - l) {
+                    if constexpr (PT) {  // the pair level l updated in plane z - l
+                        const int hl = (a.zoff + (z - l) + yr + 1 + ((a.h0 + l - 1) & 1)) & 1;
+                        *reinterpret_cast<v2f_t *>(T(l, hr) + (side ? 130 : 0)) = pick2(H[l][2], hl);
+                    } else {
+                        sts4(T(l, hr) + col, H[l][2]);
+                    }
+                }
         }
         __syncthreads();
         // phase R: levels 1..K-1 of the halo chunks
@@ -292,16 +301,27 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
             const int p = z - l + 1;
             if (hact && hr >= l && hr < NR - l) {
                 const float4 c = H[l - 1][1];
-                const float inner = T(l - 1, hr)[side ? 259 : 4];
+                const int par = (a.zoff + p + yr + 1 + ((a.h0 + l - 1) & 1)) & 1;
+                // the row wave's cell next to the chunk (xs, or xs + 255), level
+                // l - 1; in a pair tile it is there when this level uses it (the
+                // chunk updates its cell 3 / cell 0 next to it)
+                const float inner = PT && l > 1 ? T(l - 1, hr)[side ? 129 : 2] : T(l - 1, hr)[side ? 259 : 4];
                 float4 v = c;
                 if (hon) {
-                    const float4 N = lds4(T(l - 1, hr + 1) + col);
-                    const float4 S = lds4(T(l - 1, hr - 1) + col);
+                    float4 N, S;
+                    if (PT && l > 1) {  // pairs at this level's positions
+                        const v2f_t n2 = *reinterpret_cast<const v2f_t *>(T(l - 1, hr + 1) + (side ? 130 : 0));
+                        const v2f_t s2 = *reinterpret_cast<const v2f_t *>(T(l - 1, hr - 1) + (side ? 130 : 0));
+                        N = join2(n2, n2, par);
+                        S = join2(s2, s2, par);
+                    } else {
+                        N = lds4(T(l - 1, hr + 1) + col);
+                        S = lds4(T(l - 1, hr - 1) + col);
+                    }
                     float dummy = 0.f;
                     v = level4<MODE, PRE>(c, side ? inner : 0.f, side ? 0.f : inner, N, S,
                                           H[l - 1][2], H[l - 1][0], Hr[l - 1], hx, nx,
-                                          hint && !fixedp(p), a,
-                                          (a.zoff + p + yr + 1 + ((a.h0 + l - 1) & 1)) & 1, false, dummy);
+                                          hint && !fixedp(p), a, par, false, dummy);
                 }
                 H[l][0] = H[l][1];
                 H[l][1] = H[l][2];
@@ -330,10 +350,10 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
 // The halo wave as a called function (K <= 3: measured 1.5-2.5 % faster than
 // inlined there); K = 4 inlines it (as a call it takes the TbrArgs by value in
 // VGPRs and a call frame: 168-181 VGPRs, which spill).
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT>
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT, bool PT>
 __device__ __noinline__ void tbr_halo_wave_call(const TbrArgs a, float *smem, int z0, int z1, int y0,
                                                 int xs, int zl) {
-    tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F, SPLIT>(a, smem, z0, z1, y0, xs, zl);
+    tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F, SPLIT, PT>(a, smem, z0, z1, y0, xs, zl);
 }
 
 // (A double-buffered, one-barrier-per-step version of the (3, 11, 2) shape --
@@ -348,9 +368,17 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     constexpr int RS = 264;            // LDS row: 4 halo | 256 | 4 halo floats
     static_assert(K >= 1 && K <= 4 && W >= 1, "bad shape");
     static_assert(2 * NR <= 64, "halo wave: one lane per (row, side)");
+    // PT (red-black GS on the LDS-DMA path): the tiles of levels 1..K-1 hold
+    // only the pair a level updated (kPairRow floats a row: the left chunk's
+    // pair, 64 lanes' pairs, the right chunk's): a level's neighbours read
+    // the pair at their own positions, which is the one the level below
+    // updated (see the row wave); half the LDS of those tiles, so the rhs rows
+    // come by LDS-DMA too at 4 levels
+    constexpr bool PT = MODE == kRbgs && PD == 1 && K == 4;  // (at 3 levels: 16 VGPRs spill)
+    constexpr int RS2 = kPairRow;
     constexpr int TOTAL = [] {
         int t = 0;
-        for (int l = 0; l < K; ++l) t += (NR - 2 * l) * RS;
+        for (int l = 0; l < K; ++l) t += (NR - 2 * l) * (PT && l ? RS2 : RS);
         return t;
     }();
     __shared__ __attribute__((aligned(16))) float smem[TOTAL];
@@ -376,10 +404,11 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         int base = 0;
 #pragma unroll
         for (int m = 0; m < K; ++m)
-            if (m < l) base += (NR - 2 * m) * RS;
-        return smem + base + (r - l) * RS;
+            if (m < l) base += (NR - 2 * m) * (PT && m ? RS2 : RS);
+        return smem + base + (r - l) * (PT && l ? RS2 : RS);
     };
 
+    static_assert(!PT || DMA, "pair tiles: LDS-DMA path");
     static_assert(MODE == kJacobi || !PRE, "GS: raw div");
     static_assert(F == 0 || (MODE == kJacobi && !PRE && DMA), "first pass: Jacobi, raw div, DMA path");
     constexpr bool ZERO = (F & kFirstZero) != 0, RHSW = (F & kFirstRhs) != 0;
@@ -571,11 +600,17 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const int h = (BPv ^ E ^ (j * NWR)) & 1;
                                 const v2f_t lo = l == 1 ? pick2(V[j][vs(-1)], h)
                                                         : Q[j][l - 1][ROT ? sl3(R - l) : 1];
-                                const float4 f = join2(lo, Q[j][l][ROT ? sl3(R - l) : 2], h);
-                                if constexpr (SPLIT)
-                                    sts4s(T(l, rr[j]), lane, f);
-                                else
-                                    sts4(T(l, rr[j]) + 4 + 4 * lane, f);
+                                if constexpr (PT) {  // its own pair only
+                                    (void)lo;
+                                    *reinterpret_cast<v2f_t *>(T(l, rr[j]) + 2 + 2 * lane) =
+                                        Q[j][l][ROT ? sl3(R - l) : 2];
+                                } else {
+                                    const float4 f = join2(lo, Q[j][l][ROT ? sl3(R - l) : 2], h);
+                                    if constexpr (SPLIT)
+                                        sts4s(T(l, rr[j]), lane, f);
+                                    else
+                                        sts4(T(l, rr[j]) + 4 + 4 * lane, f);
+                                }
                             } else {
                                 sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][ROT ? sl3(R - l) : 2]);
                             }
@@ -631,15 +666,27 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             const v2f_t Dp = l == 1 ? pick2(V[j][vs(-1)], h) : Q[j][l - 1][qs(l - 1, 0)];
                             const float *row = T(l - 1, r);
                             float wl = dpp_from_lower(Op.y), er = dpp_from_upper(Op.x);
-                            const float wl_l = row[3], er_l = row[260];
+                            // cell xs - 1 (the left chunk's cell 3) and xs + 256 (the
+                            // right chunk's cell 0), level l - 1; in a pair tile the
+                            // left pair holds cells 1, 3 when h = 0 and the right one
+                            // cells 0, 2 when h = 1, the cases that read them
+                            const bool pt = PT && l > 1;
+                            const float wl_l = pt ? row[1] : row[3], er_l = pt ? row[130] : row[260];
                             if (lane == 0) wl = wl_l;
                             if (lane == 63) er = er_l;
                             v2f_t v = Cp;
                             if (xin) {
-                                const v2f_t N = SPLIT ? lds2s(T(l - 1, r + 1), lane, h)
-                                                      : pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
-                                const v2f_t Sv = SPLIT ? lds2s(T(l - 1, r - 1), lane, h)
-                                                       : pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
+                                v2f_t N, Sv;
+                                if (pt) {
+                                    N = *reinterpret_cast<const v2f_t *>(T(l - 1, r + 1) + 2 + 2 * lane);
+                                    Sv = *reinterpret_cast<const v2f_t *>(T(l - 1, r - 1) + 2 + 2 * lane);
+                                } else if (SPLIT) {
+                                    N = lds2s(T(l - 1, r + 1), lane, h);
+                                    Sv = lds2s(T(l - 1, r - 1), lane, h);
+                                } else {
+                                    N = pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
+                                    Sv = pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
+                                }
                                 v = level2(Cp, Op, wl, er, N, Sv, Up, Dp, pick2(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], h), h, x, nx,
                                            irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, chgl[slot(l)]);
                             }
@@ -864,9 +911,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         // which then spills a VGPR)
         constexpr int HPD = DMA && K == 4 ? 2 : PD;
         if constexpr (K == 4)
-            tbr_halo_wave<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT>(a, smem, z0, z1, y0, xs, zl);
+            tbr_halo_wave<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT, PT>(a, smem, z0, z1, y0, xs, zl);
         else
-            tbr_halo_wave_call<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT>(a, smem, z0, z1, y0, xs, zl);
+            tbr_halo_wave_call<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT, PT>(a, smem, z0, z1, y0, xs, zl);
     }
     if (MODE == kRbgs && a.maxc) {
         // level l is iteration (h0 >> 1) + q(l), q(l) = ((h0 & 1) + l - 1) >> 1
