@@ -394,8 +394,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // register load issued a step ahead (4 VGPRs per row)
     constexpr bool DMA = PD == 1 && (TOTAL + 2 * SR_ * 256) * 4 <= 160 * 1024;
     constexpr bool RDMA = DMA && (TOTAL + 4 * SR_ * 256) * 4 <= 160 * 1024;
-    // GS tiles by colour pair (sts4s): +1.2 % at K = 3; at K = 4 it spills
-    constexpr bool SPLIT = MODE == kRbgs && DMA && K <= 3;
+    // GS level-0 tile by colour pair (sts4s; at 3 levels every tile): +1.2 %
+    // at K = 3
+    constexpr bool SPLIT = MODE == kRbgs && DMA;
     constexpr int SST = DMA ? SR_ * 256 : 4;
     constexpr int SSR = RDMA ? SR_ * 256 : 4;
     __shared__ __attribute__((aligned(16))) float st_p0[SST], st_p1[SST], st_r0[SSR], st_r1[SSR];
