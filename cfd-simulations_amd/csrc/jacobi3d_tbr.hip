@@ -180,15 +180,16 @@ __device__ inline v2f_t lds2s(const float *row, int lane, int h) {
 }
 // One red-black level on a pair: C its cells' old values, O the other
 // colour's pair of the same row (E / W, with the lanes' DPP neighbours), N,
-// S, U, D the neighbour rows' / planes' pairs at the same positions, R the
-// raw div pair; level4's operation order and edge rule, so the same bits.
+// S, U, D the neighbour rows' / planes' pairs at the same positions, rhs the
+// pair of -div * dt_inv (formed once per row as it enters the queue, the
+// product level4 forms per update); level4's operation order and edge rule,
+// so the same bits.
 __device__ inline v2f_t level2(v2f_t C, v2f_t O, float wl, float er, v2f_t N, v2f_t S, v2f_t U, v2f_t D,
-                               v2f_t R, int h, int x, int nx, bool upd, const TbrArgs &a, bool own,
+                               v2f_t rhs, int h, int x, int nx, bool upd, const TbrArgs &a, bool own,
                                float &chg) {
     if (!upd) return C;
     const v2f_t E = h ? v2f_t{O.y, er} : v2f_t{O.x, O.y};
     const v2f_t W = h ? v2f_t{O.x, O.y} : v2f_t{wl, O.x};
-    const v2f_t rhs = -R * a.dt_inv;
     const v2f_t p = a.cx * (E + W);
     const v2f_t q = a.cy * (N + S);
     const v2f_t r = a.cz * (U + D);
@@ -416,6 +417,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     constexpr bool PREL = PRE || RHSW;  // the row waves' queues hold the rhs
     // the rhs from raw div (RHSW), the same bits as k_rhs_f32
     auto torhs = [&](float4 d) {
+        if constexpr (MODE == kRbgs) {  // -div * dt_inv (v5.py:209, rhs = -div / dt as * (1/dt))
+            d.x = -d.x * a.dt_inv;
+            d.y = -d.y * a.dt_inv;
+            d.z = -d.z * a.dt_inv;
+            d.w = -d.w * a.dt_inv;
+        }
         if constexpr (RHSW) {
             d.x = (a.h2 * d.x) / a.dt;
             d.y = (a.h2 * d.y) / a.dt;
