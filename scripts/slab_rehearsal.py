@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--rccl-self", action="store_true")
     ap.add_argument("--comm-priority", type=int, default=1, help="1: high-priority comm stream")
     ap.add_argument("--prefetch", type=int, default=0, help="cfd_set_jacobi3d_prefetch (0 auto, 1 DMA, 2 regs)")
+    ap.add_argument("--tb", type=int, default=0,
+                    help="--rccl-self red-black GS: 4 = two iterations per pass (4-deep ghosts), else one")
     a = ap.parse_args()
     if a.rccl_self:
         return rccl_self(a)
@@ -114,7 +116,9 @@ def rccl_self(a):
     n, R = a.n, a.ranks
     nz = a.nz or n
     gs = a.workload == "rbgs"
-    G = 2 if gs else 3
+    G = (4 if a.tb == 4 else 2) if gs else 3
+    if gs and a.tb == 4:
+        call("cfd_set_jacobi3d_blocking", 4, 0, 0)  # rbgs3d_iters_per_pass() = 2
     nzl = nz // R
     shape = (nzl + 2 * G, n, n)
     h = 1.0 / (n - 1)
