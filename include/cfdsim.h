@@ -117,7 +117,10 @@ size_t cfd_rbgs_workspace_bytes(int iterations);
 int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, int nx,
                    double dx, double dy, float dt, int iterations, double tolerance,
                    float *phi_tmp, void *ws, int *iters_done, void *stream);
-/* 3-D red-black generalisation: colour c updates (z+i+j) parity == (1+c)%2. */
+/* 3-D red-black generalisation: colour c updates (z+i+j) parity == (1+c)%2.
+ * The fused 3-D path runs cfd_get_rbgs3d_levels() half-sweeps per HBM pass
+ * (default 4: two iterations; cfd_set_jacobi3d_blocking(2..4, ...) sets it),
+ * a stop inside a pass rolled back on the device. */
 int cfd_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask, int nz, int ny, int nx,
                    double dx, double dy, double dz, float dt, int iterations, double tolerance,
                    float *phi_tmp, void *ws, int *iters_done, void *stream);
