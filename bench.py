@@ -3,9 +3,10 @@
 
 Default workload (north_star, BASELINE.json): 7-point Jacobi on a 1024^3 fp32
 grid, one "step" = one pressure solve = zero-fill phi + ITERS (200) Jacobi
-sweeps, inputs resident in HBM.  N GPUs: z-slab decomposition with RCCL halo
-exchange overlapped with the interior sweep; strong scaling (the grid is
-fixed, each rank owns 1024/N planes).
+sweeps, inputs resident in HBM.  N GPUs: z-slab decomposition with the halo
+exchange overlapped with the interior pass -- copy engines writing into the
+neighbours' IPC-mapped ghost planes (default; --transport rccl: RCCL
+send/recv); strong scaling (the grid is fixed, each rank owns 1024/N planes).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -78,6 +79,8 @@ def parse():
     ap.add_argument("--tb-zchunk", type=int, default=0)
     ap.add_argument("--tb-prefetch", type=int, default=0, help="planes of prefetch in the blocked kernel")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--transport", default="ce", choices=["ce", "rccl"],
+                    help="slab halo transport: copy engines over IPC (default) or RCCL send/recv")
     ap.add_argument("--no-rhs-ws", action="store_true", help="form the RHS in-register every sweep")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="skip the N>1 parity check")
@@ -287,8 +290,8 @@ def main():
     if gs:
         nz, ny, nx = shape
         h = 1.0 / (nx - 1)
-        # two GS iterations per pass (--tb 4) need 4-deep ghosts
-        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else (4 if ARGS.tb == 4 else 2))
+        # two GS iterations per slab pass (the default; --tb 2/3: one) need 4-deep ghosts
+        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else (2 if ARGS.tb in (2, 3) else 4))
         if not use_slab:
             div = torch.randn(shape, generator=g, device=dev, dtype=torch.float32)
             phi = torch.zeros_like(div)
@@ -301,7 +304,7 @@ def main():
                 K.solve_pressure_gauss_seidel3d(phi, div, h, h, h, dt, None, iters, GS_TOL, workspace=gs_ws,
                                                 iters_done=gs_done, phi_tmp=tmp)
         else:
-            comm = S.RcclComm(rank, world)
+            comm = make_comm(S, rank, world)
             sj = S.SlabRBGS3D(plan, ny, nx, h, h, h, dt, comm, device=dev)
             sj.div.copy_(torch.randn(sj.div.shape, generator=g, device=dev, dtype=torch.float32))
             gs_done = sj.iters_done
@@ -331,7 +334,7 @@ def main():
                     # pass starts from the zeros and forms the RHS workspace
                     K.solve_pressure_jacobi3d_zero(phi, div, h, dt, iters, phi_tmp=tmp, rhs_ws=rhs)
         else:
-            comm = S.RcclComm(rank, world)
+            comm = make_comm(S, rank, world)
             sj = S.SlabJacobi3D(plan, ny, nx, h, dt, comm, device=dev, rhs_workspace=not ARGS.no_rhs_ws)
             sj.div.copy_(torch.randn(sj.div.shape, generator=g, device=dev, dtype=torch.float32))
 
@@ -398,16 +401,18 @@ def main():
 
     value = cells_all * ARGS.steps / elapsed / 1e9
     # roofline of the dominant kernel, per launch.  A temporally blocked launch
-    # (jacobi3d_tb2) performs 2 sweeps in one HBM pass: 12 B of algorithmic
-    # traffic per cell per launch = 6 B per cell-update.
+    # (jacobi3d_tbr<K>) performs K sweeps in one HBM pass: 12 B of algorithmic
+    # traffic per cell per launch = 12/K B per cell-update.
     blocked = ARGS.tb != 1 and (iters >= 2 or gs)
     levels = int(lib().cfd_get_jacobi3d_levels() if len(shape) == 3 else lib().cfd_get_jacobi2d_levels())
     # sweeps per launch: K Jacobi sweeps per blocked pass; the GS timing
     # counts iterations, and a fused GS pass is one (two with --tb 4)
     if not gs:
         spl = levels if blocked else 1
-    elif use_slab:  # slab passes: one iteration, two with --tb 4
-        spl = 2 if blocked and ARGS.tb == 4 else 1
+    elif use_slab:  # slab passes: two iterations with 4-deep ghosts, else one
+        spl = 2 if blocked and plan.ghost == 4 else 1
+    elif ARGS.tb_rows in (5, 13):  # the tb2 kernel: one iteration per pass
+        spl = 1
     else:  # single GPU: half-sweeps per pass (--tb, or the library's auto: 4 = two iterations)
         spl = int(lib().cfd_get_rbgs3d_levels()) / 2 if blocked else 1
     launch_ms = sweep_ms * spl
@@ -429,8 +434,8 @@ def main():
         "data": "synthetic (div ~ N(0,1), seeded; phi zero-filled each step like v5.py:337)",
         "config": {"workload": workload, "grid": list(shape), "iters_per_step": iters,
                    "decomposition": "z-slab" if len(shape) == 3 else "none",
-                   "halo": ("rccl send/recv, overlapped" if not ARGS.no_overlap else "rccl send/recv")
-                   if use_slab else "none",
+                   "halo": ((TRANSPORT_NAMES[TRANSPORT] + (", overlapped" if not ARGS.no_overlap else ""))
+                            if use_slab else "none"),
                    "kernel_variant": ARGS.variant, "waves": ARGS.waves, "zchunk": ARGS.zchunk,
                    "temporal_blocking": ARGS.tb, "tb_rows": ARGS.tb_rows,
                    "rhs_workspace": not ARGS.no_rhs_ws},
@@ -468,6 +473,32 @@ def main():
         comm.close()
     if use_slab:
         dist.destroy_process_group()
+
+
+TRANSPORT = None
+TRANSPORT_NAMES = {"ce": "copy engines (SDMA into IPC-mapped neighbour ghosts)", "rccl": "rccl send/recv"}
+
+
+def make_comm(S, rank, world):
+    """The slab comm of --transport; a copy-engine comm that cannot map its
+    peers' buffers (no IPC between these GPUs) falls back to RCCL, and the
+    JSON line's config.halo says which one ran."""
+    global TRANSPORT
+    if ARGS.transport == "ce":
+        import torch
+        comm = None
+        try:  # collective: every rank raises if any rank fails to map its peers
+            comm = S.CopyEngineComm(rank, world)
+            probe = torch.zeros((2, 4096), dtype=torch.float32, device="cuda")
+            comm.attach(probe[0], probe[1])
+            TRANSPORT = "ce"
+            return comm
+        except Exception as e:  # noqa: BLE001 -- reported, then RCCL
+            if comm is not None:
+                comm.close()
+            print(f"WARNING: copy-engine transport unavailable ({e}); using RCCL", file=sys.stderr)
+    TRANSPORT = "rccl"
+    return S.RcclComm(rank, world)
 
 
 def blocked_kernel_name(levels, rows):

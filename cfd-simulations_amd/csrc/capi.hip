@@ -16,11 +16,20 @@ void set_error(const char *fmt, ...) {
 
 // Sweep timing for the bench harness: each solve brackets its sweep launches
 // with a HIP event pair recorded on the stream it launches on.
+// The event pool is reused after each cfd_timing_read(reset) / enable and
+// capped: past kMaxPairs unread solves, further solves are not timed and the
+// next read reports the overflow.  A thread's events are released when it exits.
 struct Timing {
-    bool on = false;
+    static constexpr size_t kMaxPairs = 1 << 14;
+    bool on = false, overflow = false;
     std::vector<hipEvent_t> start, stop;
     std::vector<long long> sweeps;
     size_t used = 0;
+    ~Timing() {
+        // return codes ignored: at process exit the runtime may already be gone
+        for (hipEvent_t e : start) (void)hipEventDestroy(e);
+        for (hipEvent_t e : stop) (void)hipEventDestroy(e);
+    }
 };
 static thread_local Timing g_timing;  // per host thread, like the tuning knobs
 
@@ -54,6 +63,10 @@ Tuning &tuning() {
 
 int timing_begin(hipStream_t s) {
     if (!g_timing.on) return -1;
+    if (g_timing.used >= Timing::kMaxPairs) {
+        g_timing.overflow = true;
+        return -1;
+    }
     if (g_timing.used == g_timing.start.size()) {
         hipEvent_t a, b;
         if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
@@ -117,11 +130,14 @@ int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows) {
 int cfd_timing_enable(int enable) {
     g_timing.on = enable != 0;
     g_timing.used = 0;
+    g_timing.overflow = false;
     return CFD_OK;
 }
 
 int cfd_timing_read(double *ms, long long *sweeps, int reset) {
     CFD_REQUIRE(ms && sweeps, "timing_read: null pointer");
+    CFD_REQUIRE(!g_timing.overflow, "timing_read: more than %zu solves were timed without a read",
+                Timing::kMaxPairs);
     double total = 0.0;
     long long n = 0;
     for (size_t k = 0; k < g_timing.used; ++k) {
@@ -133,7 +149,10 @@ int cfd_timing_read(double *ms, long long *sweeps, int reset) {
     }
     *ms = total;
     *sweeps = n;
-    if (reset) g_timing.used = 0;
+    if (reset) {
+        g_timing.used = 0;
+        g_timing.overflow = false;
+    }
     return CFD_OK;
 }
 }

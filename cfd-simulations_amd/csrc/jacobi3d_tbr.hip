@@ -988,7 +988,7 @@ void set_cu_reserve(int n) { g_cu_reserve = n; }
 // (2.48 ms per pass) beat 18-row tiles in 9 rounds of 103 planes (2.62 ms)
 // and in 5 rounds of 205 planes (2.79 ms); the model orders them the same.
 // Pick the shape and z-chunk (see above) and launch.
-// first: 0, or the kFirst* flags of a Jacobi first pass (K = 2, 3 auto shapes).
+// first: 0, or the kFirst* flags of a Jacobi first pass (K = 2..4 auto shapes).
 template <int MODE>
 static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStream_t s, int first = 0) {
     const int pd = jacobi3d_tb_prefetch();
@@ -1062,6 +1062,16 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
         CFD_TBR(KV, NW, RP);                                                                 \
     } while (0)
     const int code = best->K * 100 + best->nwr * 10 + best->rpw;
+    // only the CFD_TBRF shapes below have first-pass instantiations; a first
+    // pass on any other shape would silently run as a plain pass (rhs_out
+    // never written, phi read from `out`)
+    if (first && code != 3 * 100 + 11 * 10 + 2 && code != 3 * 100 + 10 * 10 + 2 &&
+        code != 4 * 100 + 11 * 10 + 2 && code != 2 * 100 + 11 * 10 + 2 && code != 2 * 100 + 10 * 10 + 2 &&
+        code != 2 * 100 + 9 * 10 + 2) {
+        set_error("jacobi3d_tbr: tile shape (%d levels, %d x %d rows) has no first-pass variant", best->K,
+                  best->nwr, best->rpw);
+        return CFD_E_INVALID;
+    }
     switch (code) {
         case 3 * 100 + 11 * 10 + 2: CFD_TBRF(3, 11, 2); break;
         case 3 * 100 + 10 * 10 + 2: CFD_TBRF(3, 10, 2); break;
@@ -1093,7 +1103,7 @@ int jacobi3d_tbr_pass(int K, int rows, const float *in, float *out, const float 
     return tbr_launch<kJacobi>(a, K, rows, zchunk, pre, s);
 }
 
-// The first pass of a solve (K = 2, 3): raw div in, f32(h*h)*div/dt of the
+// The first pass of a solve (K = 2..4): raw div in, f32(h*h)*div/dt of the
 // owned cells out to rhs_out for the later passes; zero != 0: level 0 is
 // phi = 0 and `out` is the only array of phi touched (any of the pair).
 int jacobi3d_tbr_first_pass(int K, float *out, const float *div, float *rhs_out, const float *in,

@@ -467,7 +467,9 @@ RbgsConsts rbgs3d_consts(double dx, double dy, double dz, float dt, double toler
 // Red-black GS iterations per fused pass of a slab solve: 2 when the blocking
 // depth is set to 4 levels (then a stop inside a pair is rolled back after the
 // loop), else 1.
-int rbgs3d_iters_per_pass() { return tuning().tb_steps == 4 ? 2 : 1; }
+// Slab GS iterations per fused pass where the ghosts allow two (ghost 4):
+// 2 unless the blocking depth is set to 2 or 3 (or off).
+int rbgs3d_iters_per_pass() { return tuning().tb_steps == 4 || tuning().tb_steps == 0 ? 2 : 1; }
 // Half-sweeps (colour levels) per fused pass of a single-GPU solve: the
 // blocking depth, 2..4; auto = 4 (two iterations per HBM pass on the K = 4
 // tall tiles: 2.86 ms per pass at 1024^3 = 745 Gcell/s, against 2.19 ms per

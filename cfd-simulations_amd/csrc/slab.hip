@@ -70,8 +70,77 @@ struct LocalGroup {
     bool broken = false;
 };
 
+// ---------------------------------------------------------------------------
+// Copy-engine transport (cfd_comm_init_ipc): the halo exchange without CUs.
+// Each rank maps its z-neighbours' field buffers (IPC handles of their
+// allocations, exchanged once by the caller: cfd_comm_ipc_export / _import)
+// and writes its boundary planes straight into their ghost planes with the
+// copy engines (hipMemcpyDeviceToDeviceNoCU: SDMA, ~58 GB/s per stream on
+// MI355X, measured by scripts/sdma_probe.hip), one stream per direction so the
+// two directions run on two engines.  Behind each copy, on the same stream, a
+// hipStreamWriteValue32 bumps a sequence word in the receiver's flag block
+// (uncached device memory).  The receiver's compute stream runs a one-wave
+// sync kernel (k_ce_sync) after each pass: it waits, with a bounded spin,
+// until both neighbours' words reach the expected count, so the next pass's
+// boundary launches, dispatched after it, read complete ghosts.  Why this
+// replaces RCCL here: RCCL's send/recv kernel needs 132 VGPRs and 20 KB of
+// LDS per block, which no CU has free beside the one-workgroup-per-CU tall-tile
+// interior, so it needed a CU partition (16 CUs reserved, 240-CU tile plans:
+// 13 % slower interiors, and the 256-workgroup 4-level GS tile in two rounds).
+// The copy engines take no CU at all, so the interior keeps the single-GPU
+// plan.  Ordering: counts are monotonic per direction and every rank runs the
+// same exchanges, so no host handshake is needed; a copy into a neighbour's
+// buffer can only start after that neighbour's previous sync (its boundary
+// launches, the only readers of ghost planes, precede the planes it sends,
+// which our next pass waits for), so no ghost plane is overwritten while read.
+// The red-black GS stop rule needs the global max|change| of each iteration:
+// the same sync kernel stores this rank's maxima into every rank's gather ring
+// (8-byte {tag, value} granules, system-scope stores into the uncached flag
+// blocks) and waits for every rank's granule of the pass, max-reduces them and
+// writes the global value back to the workspace before the next pass's stop
+// test reads it.
+constexpr int kCeMaxRanks = 16;
+constexpr int kCeRing = 256;             // gather slots, iterations in flight
+constexpr int kCeFromLo = 0;             // u32 word: exchanges received from the lo neighbour
+constexpr int kCeFromHi = 32;            // ... from the hi neighbour (own 128-B line)
+constexpr int kCeGatherWord = 256;       // gather ring (u64 granules) at byte 1024
+constexpr size_t kCeFlagBytes = 4 * (size_t)kCeGatherWord + 8 * (size_t)kCeRing * kCeMaxRanks;
+constexpr uint32_t kCeMagic = 0x43464445u;  // "CFDE"
+
+// What a rank exports for its peers (host bytes, cfd_comm_ipc_blob_bytes)
+struct CeBlob {
+    uint32_t magic, version;
+    int32_t rank, nranks;
+    hipIpcMemHandle_t buf_h[2];  // allocations holding phi and phi_tmp
+    uint64_t buf_off[2];         // byte offset of the array in its allocation
+    uint64_t buf_n[2];           // elements of each array
+    hipIpcMemHandle_t flags_h;   // the flag block
+};
+
+struct CeState {
+    unsigned *flags = nullptr;      // this rank's flag block (uncached)
+    unsigned **peers_dev = nullptr; // every rank's flag block, as mapped here (device array)
+    int *status = nullptr;          // bit 0: a sync kernel timed out
+    hipStream_t xs[2] = {nullptr, nullptr};  // copy streams: to lo, to hi
+    hipEvent_t xev[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    std::vector<CeBlob> blobs;      // every rank's, after import
+    struct Map {
+        int rank;
+        hipIpcMemHandle_t h;
+        char *base;
+    };
+    std::vector<Map> maps;          // IPC mappings opened by this process
+    std::vector<unsigned *> peer_flags;
+    float *mine[2] = {nullptr, nullptr};
+    size_t mine_n = 0;
+    unsigned sent[2] = {0, 0}, recvd[2] = {0, 0}, gathered = 0;
+    bool attached = false;
+};
+
 struct SlabComm {
     ncclComm_t comm = nullptr;
+    std::unique_ptr<CeState> ce;      // copy-engine transport instead of RCCL
     std::shared_ptr<LocalGroup> grp;  // in-process transport instead of RCCL
     int rank = 0, nranks = 1;
     hipEvent_t ev_boundary = nullptr, ev_comm = nullptr;
@@ -152,8 +221,9 @@ struct PartitionScope {
     bool on = false;
     PartitionScope(SlabComm *c_, bool want, hipStream_t &s, hipStream_t &cs) : c(c_), caller(s) {
         // not for an in-process group: its ranks share one GPU's CUs anyway,
-        // and 2 masked queues per rank oversubscribe the hardware queues
-        if (!want || c->grp || partition_streams(c) != 1) return;
+        // and 2 masked queues per rank oversubscribe the hardware queues; not
+        // for the copy-engine transport, whose exchange takes no CUs
+        if (!want || c->grp || c->ce || partition_streams(c) != 1) return;
         if (hipEventRecord(c->ev_fork, s) != hipSuccess ||
             hipStreamWaitEvent(c->cstream, c->ev_fork, 0) != hipSuccess)
             return;
@@ -282,6 +352,184 @@ static int exchange(SlabComm *c, float *a, int nzl, int G, size_t plane, int lo,
     return CFD_OK;
 }
 
+// ------------------------------------------------- copy-engine transport
+static const hipMemcpyKind kCopyEngine = (hipMemcpyKind)1024;  // hipMemcpyDeviceToDeviceNoCU
+// bounded spins: a peer that never signals ends the wait (status bit 0, the
+// solve's result is then garbage and cfd_comm_status reports it) instead of
+// hanging the GPU.  s_memrealtime ticks at 100 MHz: 20 s.
+constexpr unsigned long long kCeSpinLimit = 2000000000ull;
+
+struct CeSyncArgs {
+    const unsigned *flags;           // this rank's flag block
+    unsigned want_lo, want_hi;       // counts to wait for (0: no such neighbour)
+    float *maxc;                     // GS maxima: publish, gather, write back
+    int it0, cnt;                    // iterations it0 .. it0 + cnt - 1 (cnt 0: none)
+    unsigned tag0;                   // gather tag of iteration it0
+    int nranks, rank;
+    unsigned *const *peers;          // every rank's flag block
+    int *status;
+};
+
+__global__ __launch_bounds__(64) void k_ce_sync(CeSyncArgs a) {
+    const int lane = threadIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    bool ok = true;
+    // once one wait has expired the comm is broken: later syncs return at
+    // once (the solve's result is garbage either way), so a stopped peer costs
+    // one timeout, not one per pass
+    const bool broken = __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    auto expired = [&]() { return broken || wall_clock64() - t0 > kCeSpinLimit; };
+    // publish first, so that no peer waits on this rank's own waits
+    for (int q = 0; q < a.cnt; ++q) {
+        const unsigned tag = a.tag0 + (unsigned)q;
+        const unsigned long long g =
+            ((unsigned long long)__float_as_uint(a.maxc[a.it0 + q]) << 32) | (unsigned long long)tag;
+        if (lane < a.nranks) {
+            unsigned long long *ring = reinterpret_cast<unsigned long long *>(a.peers[lane] + kCeGatherWord);
+            __hip_atomic_store(ring + (size_t)(tag % kCeRing) * kCeMaxRanks + a.rank, g, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    // the neighbours' ghost planes of the pass
+    if ((lane == 0 && a.want_lo) || (lane == 1 && a.want_hi)) {
+        const unsigned *w = a.flags + (lane == 0 ? kCeFromLo : kCeFromHi);
+        const unsigned want = lane == 0 ? a.want_lo : a.want_hi;
+        while ((int)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - want) < 0) {
+            if (expired()) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    // every rank's maxima of the pass -> the global max
+    for (int q = 0; q < a.cnt; ++q) {
+        const unsigned tag = a.tag0 + (unsigned)q;
+        float m = 0.f;
+        if (lane < a.nranks) {
+            const unsigned long long *g = reinterpret_cast<const unsigned long long *>(a.flags + kCeGatherWord) +
+                                          (size_t)(tag % kCeRing) * kCeMaxRanks + lane;
+            unsigned long long v;
+            while ((unsigned)(v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != tag) {
+                if (expired()) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            m = __uint_as_float((unsigned)(v >> 32));
+        }
+        for (int off = 32; off; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        if (lane == 0) a.maxc[a.it0 + q] = m;
+    }
+    if (!ok) atomicOr(a.status, 1);
+}
+
+static int ce_map(CeState &ce, int rank, const hipIpcMemHandle_t &h, char **base) {
+    for (const CeState::Map &m : ce.maps)
+        if (m.rank == rank && !memcmp(&m.h, &h, sizeof h)) {
+            *base = m.base;
+            return CFD_OK;
+        }
+    void *p = nullptr;
+    CFD_CHECK_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    ce.maps.push_back({rank, h, static_cast<char *>(p)});
+    *base = static_cast<char *>(p);
+    return CFD_OK;
+}
+
+// buffer bi (0 = phi, 1 = phi_tmp as attached) of rank `peer`, as mapped here
+static int ce_peer_buf(SlabComm *c, int peer, int bi, float **buf, size_t *n) {
+    CeState &ce = *c->ce;
+    if (peer == c->rank) {
+        *buf = ce.mine[bi];
+        *n = ce.mine_n;
+        return CFD_OK;
+    }
+    const CeBlob &b = ce.blobs[peer];
+    char *base = nullptr;
+    int rc = ce_map(ce, peer, b.buf_h[bi], &base);
+    if (rc) return rc;
+    *buf = reinterpret_cast<float *>(base + b.buf_off[bi]);
+    *n = b.buf_n[bi];
+    return CFD_OK;
+}
+
+// the copy-engine exchange of array `a` (phi or phi_tmp as attached): the G
+// owned planes next to each neighbour go into its ghost planes once `ready`
+// (recorded on the compute stream after the boundary planes) has fired, then
+// the neighbour's sequence word is bumped
+static int exchange_ce(SlabComm *c, const float *a, int nzl, int G, size_t plane, int lo, int hi,
+                       hipEvent_t ready) {
+    CeState &ce = *c->ce;
+    const int bi = a == ce.mine[0] ? 0 : a == ce.mine[1] ? 1 : -1;
+    CFD_REQUIRE(bi >= 0, "slab (copy engines): exchange of a buffer that was not attached");
+    const size_t n = (size_t)G * plane;
+    for (int d = 0; d < 2; ++d) {
+        const int peer = d == 0 ? lo : hi;
+        if (peer < 0) continue;
+        float *dst = nullptr;
+        size_t pn = 0;
+        int rc = ce_peer_buf(c, peer, bi, &dst, &pn);
+        if (rc) return rc;
+        CFD_REQUIRE(pn >= 2 * n, "slab (copy engines): rank %d's buffer is smaller than its ghosts", peer);
+        // to lo: our first owned planes -> its last (hi) ghost planes, its
+        // from-hi word; to hi: our last owned planes -> its first ghost planes
+        const float *src = d == 0 ? a + n : a + (size_t)nzl * plane;
+        if (d == 0) dst += pn - n;
+        unsigned *word = ce.peer_flags[peer] + (d == 0 ? kCeFromHi : kCeFromLo);
+        CFD_CHECK_HIP(hipStreamWaitEvent(ce.xs[d], ready, 0));
+        CFD_CHECK_HIP(hipMemcpyAsync(dst, src, n * sizeof(float), kCopyEngine, ce.xs[d]));
+        CFD_CHECK_HIP(hipStreamWriteValue32(ce.xs[d], word, ++ce.sent[d], 0));
+        ce.used[d] = true;
+    }
+    return CFD_OK;
+}
+
+// on stream s: wait for the ghosts of the last exchange (and, cnt > 0, make
+// maxc[it0 .. it0+cnt) the global maxima)
+static int ce_sync(SlabComm *c, hipStream_t s, int lo, int hi, float *maxc, int it0, int cnt) {
+    CeState &ce = *c->ce;
+    CeSyncArgs a{};
+    a.flags = ce.flags;
+    a.want_lo = lo >= 0 ? ++ce.recvd[0] : 0u;
+    a.want_hi = hi >= 0 ? ++ce.recvd[1] : 0u;
+    a.maxc = maxc;
+    a.it0 = it0;
+    a.cnt = maxc ? cnt : 0;
+    a.tag0 = ce.gathered + 1;
+    ce.gathered += (unsigned)a.cnt;
+    a.nranks = c->nranks;
+    a.rank = c->rank;
+    a.peers = ce.peers_dev;
+    a.status = ce.status;
+    if (!a.want_lo && !a.want_hi && !a.cnt) return CFD_OK;
+    hipLaunchKernelGGL(k_ce_sync, dim3(1), dim3(64), 0, s, a);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// end of a solve: the caller's stream covers this rank's outgoing copies
+static int ce_join(SlabComm *c, hipStream_t s) {
+    CeState &ce = *c->ce;
+    for (int d = 0; d < 2; ++d) {
+        if (!ce.used[d]) continue;
+        CFD_CHECK_HIP(hipEventRecord(ce.xev[d], ce.xs[d]));
+        CFD_CHECK_HIP(hipStreamWaitEvent(s, ce.xev[d], 0));
+        ce.used[d] = false;
+    }
+    return CFD_OK;
+}
+
+static int ce_check_attached(SlabComm *c, const float *phi, const float *phi_tmp) {
+    CeState &ce = *c->ce;
+    CFD_REQUIRE(ce.attached && (phi == ce.mine[0] || phi == ce.mine[1]) &&
+                    (!phi_tmp || phi_tmp == (phi == ce.mine[0] ? ce.mine[1] : ce.mine[0])),
+                "slab (copy engines): phi / phi_tmp are not the buffers attached with "
+                "cfd_comm_ipc_import");
+    return CFD_OK;
+}
+
 }  // namespace cfd
 
 using namespace cfd;
@@ -342,9 +590,146 @@ int cfd_comm_init_local(int nranks, void **comms) {
     return CFD_OK;
 }
 
+int cfd_comm_init_ipc(int nranks, int rank, void **comm) {
+    CFD_REQUIRE(comm && nranks >= 1 && nranks <= kCeMaxRanks && rank >= 0 && rank < nranks,
+                "comm_init_ipc: 1..%d ranks, 0 <= rank < nranks", kCeMaxRanks);
+    std::unique_ptr<SlabComm> c(new SlabComm());
+    c->rank = rank;
+    c->nranks = nranks;
+    c->ce.reset(new CeState());
+    CeState &ce = *c->ce;
+    CFD_CHECK_HIP(hipExtMallocWithFlags((void **)&ce.flags, kCeFlagBytes, hipDeviceMallocUncached));
+    CFD_CHECK_HIP(hipMemset(ce.flags, 0, kCeFlagBytes));
+    CFD_CHECK_HIP(hipMalloc((void **)&ce.peers_dev, sizeof(unsigned *) * kCeMaxRanks));
+    CFD_CHECK_HIP(hipMalloc((void **)&ce.status, sizeof(int)));
+    CFD_CHECK_HIP(hipMemset(ce.status, 0, sizeof(int)));
+    for (int d = 0; d < 2; ++d) {
+        CFD_CHECK_HIP(hipStreamCreateWithFlags(&ce.xs[d], hipStreamNonBlocking));
+        CFD_CHECK_HIP(hipEventCreateWithFlags(&ce.xev[d], hipEventDisableTiming));
+    }
+    CFD_CHECK_HIP(hipEventCreateWithFlags(&c->ev_boundary, hipEventDisableTiming));
+    CFD_CHECK_HIP(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
+    CFD_CHECK_HIP(hipDeviceSynchronize());
+    *comm = c.release();
+    return CFD_OK;
+}
+
+size_t cfd_comm_ipc_blob_bytes(void) { return sizeof(CeBlob); }
+
+int cfd_comm_ipc_export(void *comm, const float *phi, const float *phi_tmp, size_t n, void *blob) {
+    SlabComm *c = reinterpret_cast<SlabComm *>(comm);
+    CFD_REQUIRE(c && c->ce && phi && phi_tmp && phi != phi_tmp && n > 0 && blob,
+                "comm_ipc_export: needs a copy-engine comm, two distinct buffers and a blob");
+    CeState &ce = *c->ce;
+    CeBlob b;
+    memset(&b, 0, sizeof b);
+    b.magic = kCeMagic;
+    b.version = 1;
+    b.rank = c->rank;
+    b.nranks = c->nranks;
+    const float *bufs[2] = {phi, phi_tmp};
+    for (int i = 0; i < 2; ++i) {
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        CFD_CHECK_HIP(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)bufs[i]));
+        const size_t off = (size_t)((const char *)bufs[i] - (const char *)base);
+        CFD_REQUIRE(off + n * sizeof(float) <= size, "comm_ipc_export: buffer %d overruns its allocation", i);
+        CFD_CHECK_HIP(hipIpcGetMemHandle(&b.buf_h[i], (void *)base));
+        b.buf_off[i] = off;
+        b.buf_n[i] = n;
+    }
+    CFD_CHECK_HIP(hipIpcGetMemHandle(&b.flags_h, ce.flags));
+    ce.mine[0] = const_cast<float *>(phi);
+    ce.mine[1] = const_cast<float *>(phi_tmp);
+    ce.mine_n = n;
+    ce.attached = false;  // until the import
+    memcpy(blob, &b, sizeof b);
+    return CFD_OK;
+}
+
+int cfd_comm_ipc_import(void *comm, const void *blobs, int nblobs) {
+    SlabComm *c = reinterpret_cast<SlabComm *>(comm);
+    CFD_REQUIRE(c && c->ce && blobs && nblobs == c->nranks,
+                "comm_ipc_import: needs a copy-engine comm and one blob per rank (%d)", c ? c->nranks : 0);
+    CeState &ce = *c->ce;
+    CFD_REQUIRE(ce.mine[0], "comm_ipc_import: export this rank's buffers first");
+    // every solve of the previous attachment is complete before its mappings go
+    CFD_CHECK_HIP(hipDeviceSynchronize());
+    std::vector<CeBlob> in((size_t)nblobs);
+    memcpy(in.data(), blobs, sizeof(CeBlob) * (size_t)nblobs);
+    for (int r = 0; r < nblobs; ++r)
+        CFD_REQUIRE(in[r].magic == kCeMagic && in[r].version == 1 && in[r].rank == r &&
+                        in[r].nranks == c->nranks,
+                    "comm_ipc_import: blob %d is not rank %d's export of a %d-rank comm", r, r, c->nranks);
+    // buffer mappings of an earlier attachment are dropped (flag blocks stay)
+    std::vector<CeState::Map> keep;
+    for (const CeState::Map &m : ce.maps) {
+        bool flags = false;
+        for (const CeBlob &b : ce.blobs)
+            if (b.rank == m.rank && !memcmp(&b.flags_h, &m.h, sizeof m.h)) flags = true;
+        if (flags)
+            keep.push_back(m);
+        else
+            CFD_CHECK_HIP(hipIpcCloseMemHandle(m.base));
+    }
+    ce.maps.swap(keep);
+    ce.blobs.swap(in);
+    ce.peer_flags.assign((size_t)c->nranks, nullptr);
+    for (int r = 0; r < c->nranks; ++r) {
+        if (r == c->rank) {
+            ce.peer_flags[r] = ce.flags;
+            continue;
+        }
+        char *base = nullptr;
+        int rc = ce_map(ce, r, ce.blobs[r].flags_h, &base);
+        if (rc) return rc;
+        ce.peer_flags[r] = reinterpret_cast<unsigned *>(base);
+    }
+    CFD_CHECK_HIP(hipMemcpy(ce.peers_dev, ce.peer_flags.data(), sizeof(unsigned *) * c->nranks,
+                            hipMemcpyHostToDevice));
+    // the z-neighbours' buffers are mapped now (others on first use)
+    for (int r : {c->rank - 1, c->rank + 1}) {
+        if (r < 0 || r >= c->nranks) continue;
+        for (int bi = 0; bi < 2; ++bi) {
+            float *p = nullptr;
+            size_t n = 0;
+            int rc = ce_peer_buf(c, r, bi, &p, &n);
+            if (rc) return rc;
+        }
+    }
+    ce.attached = true;
+    return CFD_OK;
+}
+
+int cfd_comm_status(void *comm, int *timeouts) {
+    SlabComm *c = reinterpret_cast<SlabComm *>(comm);
+    CFD_REQUIRE(c && timeouts, "comm_status: null argument");
+    *timeouts = 0;
+    if (!c->ce) return CFD_OK;
+    CFD_CHECK_HIP(hipDeviceSynchronize());
+    CFD_CHECK_HIP(hipMemcpy(timeouts, c->ce->status, sizeof(int), hipMemcpyDeviceToHost));
+    if (*timeouts) {
+        set_error("slab (copy engines): a wait for a neighbour timed out");
+        return CFD_E_COMM;
+    }
+    return CFD_OK;
+}
+
 int cfd_comm_destroy(void *comm) {
     if (!comm) return CFD_OK;
     SlabComm *c = reinterpret_cast<SlabComm *>(comm);
+    if (c->ce) {
+        CeState &ce = *c->ce;
+        (void)hipDeviceSynchronize();
+        for (const CeState::Map &m : ce.maps) (void)hipIpcCloseMemHandle(m.base);
+        for (int d = 0; d < 2; ++d) {
+            if (ce.xs[d]) (void)hipStreamDestroy(ce.xs[d]);
+            if (ce.xev[d]) (void)hipEventDestroy(ce.xev[d]);
+        }
+        if (ce.flags) (void)hipFree(ce.flags);
+        if (ce.peers_dev) (void)hipFree(ce.peers_dev);
+        if (ce.status) (void)hipFree(ce.status);
+    }
     if (c->ev_boundary) (void)hipEventDestroy(c->ev_boundary);
     if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
@@ -439,8 +824,18 @@ static int slab_jacobi3d(SlabComm *c, const float *div, float *phi, float *phi_t
         src = rhs_ws;
     }
     if (c->grp && (rc = register_local(c, phi, phi_tmp, nullptr, nz_local, G, plane))) return rc;
+    if (c->ce && (rc = ce_check_attached(c, phi, phi_tmp))) return rc;
     // ghosts of the initial guess (a zero start reads none)
-    if (!zero && (rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
+    if (!zero) {
+        if (c->ce) {
+            CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
+            if ((rc = exchange_ce(c, phi, nz_local, G, plane, lo_peer, hi_peer, c->ev_boundary)) ||
+                (rc = ce_sync(c, s, lo_peer, hi_peer, nullptr, 0, 0)))
+                return rc;
+        } else if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) {
+            return rc;
+        }
+    }
     const int fixed_lo = zb > G, fixed_hi = ze < nz_local + G;
     // owned planes a neighbour needs after each pass: the G next to it
     const bool lo_b = lo_peer >= 0, hi_b = hi_peer >= 0;
@@ -467,7 +862,14 @@ static int slab_jacobi3d(SlabComm *c, const float *div, float *phi, float *phi_t
         };
         if (!can_overlap) {
             if ((rc = run(zb, ze))) return rc;
-            if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
+            if (c->ce) {
+                CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
+                if ((rc = exchange_ce(c, b, nz_local, G, plane, lo_peer, hi_peer, c->ev_boundary)) ||
+                    (rc = ce_sync(c, s, lo_peer, hi_peer, nullptr, 0, 0)))
+                    return rc;
+            } else if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, s))) {
+                return rc;
+            }
         } else {
             // boundary planes first, their exchange on the comm stream, the
             // interior meanwhile on the main stream
@@ -485,10 +887,18 @@ static int slab_jacobi3d(SlabComm *c, const float *div, float *phi, float *phi_t
             // depend on them (a wait captures the event as recorded so far)
             CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
             if ((rc = run(ib, ie))) return rc;
-            CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
-            if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, cs))) return rc;
-            CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
-            CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
+            if (c->ce) {
+                // copy engines: no CUs, so nothing to reserve; the next pass
+                // waits for the neighbours' planes behind the interior
+                if ((rc = exchange_ce(c, b, nz_local, G, plane, lo_peer, hi_peer, c->ev_boundary)) ||
+                    (rc = ce_sync(c, s, lo_peer, hi_peer, nullptr, 0, 0)))
+                    return rc;
+            } else {
+                CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
+                if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, cs))) return rc;
+                CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
+                CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
+            }
         }
         // after the first pass, the other buffer gets the final owned faces too
         if (done == 0 && !zero &&
@@ -499,6 +909,7 @@ static int slab_jacobi3d(SlabComm *c, const float *div, float *phi, float *phi_t
         a = b;
         b = t;
     }
+    if (c->ce && (rc = ce_join(c, s))) return rc;
     timing_end(tk, s, iters);
     if (a != phi)
         CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(float) * plane * nzt, hipMemcpyDeviceToDevice, s));
@@ -590,8 +1001,21 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
         return CFD_OK;
     };
     if (c->grp && (rc = register_local(c, phi, phi_tmp, w, nz_local, G, plane))) return rc;
+    // copy engines: the exchange of `a` and the next pass's wait for it (with
+    // the global maxima of iterations it .. it+cnt-1 when cnt > 0)
+    auto ce_step = [&](float *a, int it, int cnt) -> int {
+        int r;
+        CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
+        if ((r = exchange_ce(c, a, nz_local, G, plane, lo_peer, hi_peer, c->ev_boundary))) return r;
+        return ce_sync(c, s, lo_peer, hi_peer, reduce ? w->maxc : nullptr, it, cnt);
+    };
+    if (c->ce && (rc = ce_check_attached(c, phi, phi_tmp))) return rc;
     // ghosts of the initial guess
-    if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
+    if (c->ce) {
+        if ((rc = ce_step(phi, 0, 0))) return rc;
+    } else if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) {
+        return rc;
+    }
     const int tk = timing_begin(s);
     const bool fused = G >= 2 && rbgs3d_fused_ok(phi, phi_tmp, div, mask, nx);
     if (!fused) {
@@ -599,10 +1023,15 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
             for (int colour = 0; colour < 2; ++colour) {
                 if ((rc = rbgs3d_colour_pass(colour, phi, div, mask, ny, nx, zb, ze, zoff, k, w, it, s)))
                     return rc;
-                if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
+                if (c->ce) {
+                    if ((rc = ce_step(phi, it, colour))) return rc;  // maxima after colour 1
+                } else if ((rc = exchange(c, phi, nz_local, G, plane, lo_peer, hi_peer, s))) {
+                    return rc;
+                }
             }
-            if ((rc = allreduce(it, 1, s))) return rc;
+            if (!c->ce && (rc = allreduce(it, 1, s))) return rc;
         }
+        if (c->ce && (rc = ce_join(c, s))) return rc;
         timing_end(tk, s, iterations);
         return launch_rbgs_finish(w, phi, nullptr, plane * nzt, iters_done, s);
     }
@@ -622,7 +1051,7 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
     // wasted pass n+1; it writes the buffer of iteration n-1, so iteration n's
     // result is intact, and maxc of a skipped pass stays 0 (< tol), which keeps
     // every later pass skipped.  rbgs_count / rbgs_copy are unchanged.
-    const int lag = can_overlap && reduce && pp == 1 ? 1 : 0;
+    const int lag = can_overlap && reduce && pp == 1 && !c->ce ? 1 : 0;
     float *a = phi, *b = phi_tmp;
     for (int it = 0; it < iterations;) {
         const int m = iterations - it >= pp ? pp : 1;
@@ -633,8 +1062,12 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
         };
         if (!can_overlap) {
             if ((rc = run(zb, ze))) return rc;
-            if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, s))) return rc;
-            if ((rc = allreduce(it, m, s))) return rc;
+            if (c->ce) {
+                if ((rc = ce_step(b, it, m))) return rc;
+            } else if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, s)) ||
+                       (rc = allreduce(it, m, s))) {
+                return rc;
+            }
         } else {
             int ib = zb, ie = ze;
             if (lo_peer >= 0) {
@@ -648,6 +1081,18 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
             // interior enqueued before the exchange (see the Jacobi driver)
             CFD_CHECK_HIP(hipEventRecord(c->ev_boundary, s));
             if ((rc = run(ib, ie))) return rc;
+            if (c->ce) {
+                // copies started after the boundary planes; the sync behind
+                // the interior waits for the ghosts and combines the maxima
+                if ((rc = exchange_ce(c, b, nz_local, G, plane, lo_peer, hi_peer, c->ev_boundary)) ||
+                    (rc = ce_sync(c, s, lo_peer, hi_peer, reduce ? w->maxc : nullptr, it, m)))
+                    return rc;
+                it += m;
+                float *t = a;
+                a = b;
+                b = t;
+                continue;
+            }
             CFD_CHECK_HIP(hipStreamWaitEvent(cs, c->ev_boundary, 0));
             if ((rc = exchange(c, b, nz_local, G, plane, lo_peer, hi_peer, cs))) return rc;
             // lagged: the next pass waits for the exchange only (and, through
@@ -671,6 +1116,7 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
         CFD_CHECK_HIP(hipEventRecord(c->ev_comm, cs));
         CFD_CHECK_HIP(hipStreamWaitEvent(s, c->ev_comm, 0));
     }
+    if (c->ce && (rc = ce_join(c, s))) return rc;
     timing_end(tk, s, iterations);
     // count (same on every rank: the maxima are global), re-run a pair
     // pass's first iteration if the stop fell inside it, pick the buffer

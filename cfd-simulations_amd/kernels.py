@@ -32,6 +32,20 @@ def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
     return t
 
 
+def _like(phi: torch.Tensor, t, name: str):
+    """A companion array of phi (div, scratch, workspace): same shape, dtype,
+    device, C-contiguous -- the kernels index it with phi's strides, so a
+    mismatch would read or write out of bounds.  None passes through."""
+    if t is None:
+        return None
+    if tuple(t.shape) != tuple(phi.shape) or t.dtype != phi.dtype or t.device != phi.device:
+        raise ValueError(f"{name} must match phi: got {tuple(t.shape)} {t.dtype} on {t.device}, "
+                         f"phi is {tuple(phi.shape)} {phi.dtype} on {phi.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be C-contiguous")
+    return t
+
+
 def _shape2d(t: torch.Tensor):
     if t.dim() != 2:
         raise ValueError(f"expected a 2-D (ny, nx) array, got shape {tuple(t.shape)}")
@@ -125,7 +139,8 @@ def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iteratio
     need = int(lib().cfd_rbgs_workspace_bytes(int(iterations)))
     if ws is None or ws.numel() * ws.element_size() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
-    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
+    tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
+    _like(phi, div_u_star, "div_u_star")
     call("cfd_rbgs2d_f32", ptr(_f32(phi, "phi")), ptr(_f32(div_u_star, "div_u_star")), ptr(m), ny, nx,
          float(dx), float(dy), float(np.float32(dt)), int(iterations), float(tolerance), ptr(_f32(tmp, "phi_tmp")),
          ptr(ws), ptr(iters_done), stream_handle())
@@ -140,7 +155,9 @@ def solve_pressure_jacobi(phi, div_u_star, dx, dt, mask, iterations, phi_tmp=Non
     ny, nx = _shape2d(phi)
     if div_u_star.dtype != phi.dtype:
         raise TypeError("phi and div_u_star must share a dtype")
-    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
+    _like(phi, div_u_star, "div_u_star")
+    _like(phi, rhs_ws, "rhs_ws")
+    tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
     m = _mask_u8(mask, phi.shape)
     fn = {torch.float32: "cfd_jacobi2d_f32", torch.float64: "cfd_jacobi2d_f64"}.get(phi.dtype)
     if fn is None:
@@ -156,7 +173,9 @@ def solve_pressure_jacobi3d(phi, div, h, dt, mask, iterations, phi_tmp=None, res
     if phi.dim() != 3:
         raise ValueError("expected (nz, ny, nx)")
     nz, ny, nx = (int(s) for s in phi.shape)
-    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
+    _like(phi, _f32(div, "div"), "div")
+    _like(phi, rhs_ws, "rhs_ws")
+    tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
     m = _mask_u8(mask, phi.shape)
     call("cfd_jacobi3d_f32", ptr(_f32(div, "div")), ptr(_f32(phi, "phi")), ptr(tmp), ptr(rhs_ws), ptr(m),
          nz, ny, nx, float(h), float(np.float32(dt)), int(iterations), int(resid_every), ptr(resid_out),
@@ -173,9 +192,9 @@ def solve_pressure_jacobi3d_zero(phi, div, h, dt, iterations, phi_tmp=None, rhs_
         raise ValueError("expected (nz, ny, nx)")
     nz, ny, nx = (int(s) for s in phi.shape)
     tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
-    for t, name in ((tmp, "phi_tmp"), (rhs_ws, "rhs_ws")):
-        if t is not None and (t.shape != phi.shape or t.dtype != torch.float32 or not t.is_contiguous()):
-            raise ValueError(f"{name} must be a contiguous float32 array of phi's shape")
+    _f32(phi, "phi")
+    for t, name in ((tmp, "phi_tmp"), (rhs_ws, "rhs_ws"), (div, "div")):
+        _like(phi, t, name)
     call("cfd_jacobi3d_zero_f32", ptr(_f32(div, "div")), ptr(_f32(phi, "phi")), ptr(tmp), ptr(rhs_ws),
          nz, ny, nx, float(h), float(np.float32(dt)), int(iterations), stream_handle())
     return phi
@@ -191,7 +210,8 @@ def solve_pressure_gauss_seidel3d(phi, div, dx, dy, dz, dt, mask, iterations, to
     ws = workspace
     if ws is None or ws.numel() * ws.element_size() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
-    tmp = torch.empty_like(phi) if phi_tmp is None else phi_tmp
+    tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
+    _like(phi, div, "div")
     call("cfd_rbgs3d_f32", ptr(_f32(phi, "phi")), ptr(_f32(div, "div")), ptr(m), nz, ny, nx, float(dx),
          float(dy), float(dz), float(np.float32(dt)), int(iterations), float(tolerance), ptr(_f32(tmp, "phi_tmp")),
          ptr(ws), ptr(iters_done), stream_handle())

@@ -2,9 +2,11 @@
 
 The reference runs on one node's CPU threads (SURVEY.md section 2,
 "Parallelism").  Here the (nz, ny, nx) grid is cut on the slowest axis.  Each
-rank holds its owned planes plus one ghost plane per side.  After every sweep
-the ranks swap boundary planes with their z-neighbours over RCCL send/recv
-(xGMI), and that swap overlaps the interior sweep on a second HIP stream.
+rank holds its owned planes plus G ghost planes per side.  After every pass
+the ranks swap boundary planes with their z-neighbours over xGMI -- by default
+with the copy engines (SDMA writes into the neighbours' IPC-mapped ghost
+planes, no CU taken from the interior), or with RCCL send/recv -- and that swap
+overlaps the interior pass.
 With G-deep ghosts (G = 2..4) the sweeps run temporally blocked: G sweeps per
 pass and one G-plane exchange per pass, 1/G as many messages at the same bytes
 per sweep.  Jacobi updates reassociate nothing across planes, so the decomposed
@@ -168,6 +170,99 @@ class RcclComm:
             pass
 
 
+class CopyEngineComm:
+    """Copy-engine slab transport (cfd_comm_init_ipc): no RCCL.  Each rank maps
+    its z-neighbours' field buffers through IPC handles and the SDMA engines
+    write its boundary planes straight into their ghost planes, so the halo
+    exchange takes no CU from the interior launch (see slab.hip).  The handle
+    blobs travel over the torch.distributed process group once per pair of
+    buffers (``attach``, called by SlabJacobi3D / SlabRBGS3D)."""
+
+    def __init__(self, rank: int, nranks: int, group=None):
+        import ctypes
+        handle = ctypes.c_void_p()
+        call("cfd_comm_init_ipc", int(nranks), int(rank), ctypes.byref(handle))
+        self.handle = handle
+        self.rank, self.nranks, self.group = rank, nranks, group
+        self._attached = None
+
+    def attach(self, phi: torch.Tensor, phi_tmp: torch.Tensor):
+        """Export this rank's two field buffers, gather every rank's blob (a
+        collective over the process group), map the neighbours' buffers."""
+        import ctypes
+        key = (phi.data_ptr(), phi_tmp.data_ptr(), phi.numel())
+        if self._attached == key:
+            return
+        if phi.shape != phi_tmp.shape or phi.dtype != torch.float32 or not phi.is_cuda:
+            raise ValueError("attach: two float32 device arrays of one shape")
+        nb = int(lib().cfd_comm_ipc_blob_bytes())
+        blob = (ctypes.c_char * nb)()
+        err = None
+        try:
+            call("cfd_comm_ipc_export", self.handle, ptr(phi), ptr(phi_tmp), phi.numel(),
+                 ctypes.addressof(blob))
+        except Exception as e:  # noqa: BLE001 -- every rank learns of it below
+            err = e
+        self._agree(err, "export")
+        mine = bytes(blob.raw)
+        if self.nranks > 1:
+            import torch.distributed as dist
+            blobs = [None] * self.nranks
+            dist.all_gather_object(blobs, mine, group=self.group)
+        else:
+            blobs = [mine]
+        allb = (ctypes.c_char * (nb * self.nranks)).from_buffer_copy(b"".join(blobs))
+        try:
+            call("cfd_comm_ipc_import", self.handle, ctypes.addressof(allb), self.nranks)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        self._agree(err, "import")
+        self._attached = key
+
+    def _agree(self, err, what):
+        """Collective: raise on every rank if `what` failed on any (so that no
+        rank is left waiting in the next collective)."""
+        ok = err is None
+        if self.nranks > 1:
+            import torch.distributed as dist
+            dev = torch.device("cuda", torch.cuda.current_device()) \
+                if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+            ok = bool(t.item())
+        if not ok:
+            raise RuntimeError(f"copy-engine comm: {what} failed on "
+                               f"{'this rank: ' + str(err) if err else 'another rank'}")
+
+    def status(self) -> int:
+        """Synchronises the device; raises CfdError if a wait for a neighbour
+        timed out (cfd_comm_status)."""
+        import ctypes
+        t = ctypes.c_int(0)
+        call("cfd_comm_status", self.handle, ctypes.byref(t))
+        return t.value
+
+    def close(self):
+        if self.handle:
+            call("cfd_comm_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_comm(rank: int, nranks: int, transport: str = "ce", group=None):
+    """The slab transport: "ce" (copy engines over IPC, the default) or "rccl"."""
+    if transport == "ce":
+        return CopyEngineComm(rank, nranks, group)
+    if transport == "rccl":
+        return RcclComm(rank, nranks, group)
+    raise ValueError(f"unknown slab transport {transport!r}")
+
+
 class LocalComm:
     """One rank of an in-process slab group (cfd_comm_init_local): N ranks
     driven by N host threads on one GPU, for tests and rehearsals where RCCL
@@ -212,6 +307,8 @@ class SlabJacobi3D:
         self.rhs = torch.empty(shape, dtype=torch.float32, device=self.device) if rhs_workspace else None
         self.mask = None if mask is None else mask.to(torch.uint8).contiguous()
         self.comm = comm
+        if hasattr(comm, "attach"):
+            comm.attach(self.phi, self.tmp)
         # high priority: its own HW queue (ROCclr pools queues per priority), so
         # the exchange is dispatched beside the interior launch, not behind it
         self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1)
@@ -257,6 +354,8 @@ class SlabRBGS3D:
         self.iters_done = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.ws = None
         self.comm = comm
+        if hasattr(comm, "attach"):
+            comm.attach(self.phi, self.tmp)
         # high priority: its own HW queue (ROCclr pools queues per priority), so
         # the exchange is dispatched beside the interior launch, not behind it
         self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1)
@@ -293,4 +392,4 @@ def sweep_range(phi_in, phi_out, div, mask, z_begin, z_end, h, dt, resid=None):
          float(np.float32(dt)), ptr(resid), stream_handle())
 
 
-__all__ = ["SlabPlan", "RcclComm", "LocalComm", "SlabJacobi3D", "SlabRBGS3D", "sweep_range", "comm_unique_id", "lib"]
+__all__ = ["SlabPlan", "RcclComm", "CopyEngineComm", "make_comm", "LocalComm", "SlabJacobi3D", "SlabRBGS3D", "sweep_range", "comm_unique_id", "lib"]

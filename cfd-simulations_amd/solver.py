@@ -306,22 +306,27 @@ class OptimizedTurbulentSolver:
         """save_data_to_hdf5 layout (v5.py:454-470) as .npz (h5py is absent):
         group step_%06d with u, v, vorticity, X, Y and the time attribute.
         Like the reference's file (opened in append mode, a group written
-        once), an existing snapshot file keeps its groups and gains this one.
-        phi and the step counter are added (the reference stores neither) so
-        that load_snapshot restarts the run exactly."""
+        once, v5.py:457-458), an existing snapshot file keeps its groups and
+        gains this one: the new group's arrays are appended as members of the
+        .npz zip archive, so a save costs O(one group) however many the file
+        holds, and a group already present is left alone without reading the
+        device.  phi and the step counter are added (the reference stores
+        neither) so that load_snapshot restarts the run exactly."""
+        import zipfile
         g = f"step_{step:06d}"
-        groups = {}
-        if os.path.exists(path):
-            with np.load(path, allow_pickle=False) as old:
-                groups = {k: old[k] for k in old.files}
-        if f"{g}/u" not in groups:  # `if group_name not in f` (v5.py:458)
-            groups.update({f"{g}/u": self.u.cpu().numpy(), f"{g}/v": self.v.cpu().numpy(),
-                           f"{g}/vorticity": self.compute_vorticity().cpu().numpy(),
-                           f"{g}/X": self.X, f"{g}/Y": self.Y, f"{g}/phi": self.phi.cpu().numpy(),
-                           f"{g}/time": np.float64(current_time), f"{g}/solver_step": np.int64(self.step)})
-        tmp = str(path) + ".tmp.npz"
-        np.savez_compressed(tmp, **groups)
-        os.replace(tmp, path)
+        exists = os.path.exists(path)
+        if exists:
+            with zipfile.ZipFile(path, "r") as z:
+                if f"{g}/u.npy" in z.namelist():  # `if group_name not in f` (v5.py:458)
+                    return
+        groups = {f"{g}/u": self.u.cpu().numpy(), f"{g}/v": self.v.cpu().numpy(),
+                  f"{g}/vorticity": self.compute_vorticity().cpu().numpy(),
+                  f"{g}/X": self.X, f"{g}/Y": self.Y, f"{g}/phi": self.phi.cpu().numpy(),
+                  f"{g}/time": np.float64(current_time), f"{g}/solver_step": np.int64(self.step)}
+        with zipfile.ZipFile(path, "a" if exists else "w", compression=zipfile.ZIP_DEFLATED) as z:
+            for k, arr in groups.items():
+                with z.open(f"{k}.npy", "w", force_zip64=True) as f:
+                    np.lib.format.write_array(f, np.asanyarray(arr), allow_pickle=False)
 
     def load_snapshot(self, path, step=None):
         """Restart from a save_snapshot file: group step_%06d (the latest

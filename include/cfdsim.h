@@ -205,11 +205,36 @@ int cfd_nonfinite_count_f32(const float *a, const float *b, size_t n, int *out, 
 
 /* ------------------------------------------------- multi-GPU slab Jacobi */
 /* One process per GPU.  The global (nz, ny, nx) grid is split on z; rank r
- * holds nz_local owned planes plus one ghost plane on each side: local array
- * (nz_local + 2, ny, nx), owned planes 1..nz_local.  Ghost planes are filled
- * by RCCL send/recv over xGMI after each sweep. */
+ * holds nz_local owned planes plus `ghost` (1..4) ghost planes on each side:
+ * local array (nz_local + 2*ghost, ny, nx), owned planes ghost ..
+ * ghost+nz_local-1.  After each pass the ghost planes are refilled from the
+ * z-neighbours over xGMI by one of two transports (a `comm` is either):
+ *  - copy engines (cfd_comm_init_ipc, the default of the Python side): each
+ *    rank maps its neighbours' field buffers through IPC handles and the SDMA
+ *    engines write its boundary planes straight into their ghost planes; no CU
+ *    is used, so the interior launch keeps the whole chip;
+ *  - RCCL send/recv (cfd_comm_init), whose kernel runs on a reserved set of
+ *    CUs beside the interior (CFD_SLAB_COMM_CUS). */
 int cfd_comm_unique_id(void *out, size_t bytes); /* bytes >= 128 */
 int cfd_comm_init(const void *unique_id, int nranks, int rank, void **comm);
+/* Copy-engine comm of rank `rank` of nranks (<= 16), no RCCL.  Before a solve
+ * every rank attaches its two field buffers: cfd_comm_ipc_export(phi,
+ * phi_tmp, n elements each) fills a host blob of cfd_comm_ipc_blob_bytes()
+ * bytes; the caller gathers all ranks' blobs (any out-of-band channel, e.g.
+ * torch.distributed all_gather_object) and passes them in rank order to
+ * cfd_comm_ipc_import, which maps the neighbours' buffers and every rank's
+ * flag block.  The slab solves then take exactly those buffers (phi / phi_tmp
+ * in either order) and ignore comm_stream (the comm owns one copy stream per
+ * direction).  A one-rank comm may name itself as both neighbours: the
+ * per-rank rehearsal of scripts/slab_rehearsal.py (its result is not a
+ * solve).  Waits for a neighbour are bounded (20 s): cfd_comm_status
+ * synchronises the device and returns CFD_E_COMM (timeouts = 1) if one
+ * expired, i.e. a rank stopped or the ranks ran different solves. */
+int cfd_comm_init_ipc(int nranks, int rank, void **comm);
+size_t cfd_comm_ipc_blob_bytes(void);
+int cfd_comm_ipc_export(void *comm, const float *phi, const float *phi_tmp, size_t n, void *blob);
+int cfd_comm_ipc_import(void *comm, const void *blobs, int nblobs);
+int cfd_comm_status(void *comm, int *timeouts);
 int cfd_comm_destroy(void *comm);
 /* An in-process group of nranks (<= 16) communicators for ONE process driving
  * the ranks from nranks host threads on one GPU (RCCL refuses several ranks per
@@ -227,11 +252,12 @@ int cfd_comm_init_local(int nranks, void **comms);
  * (global Dirichlet planes excluded).  After each pass the `ghost` owned
  * planes next to a neighbour go into its ghost planes.  rhs_ws: optional
  * same-size workspace (see cfd_jacobi2d_f32).  overlap != 0: the boundary
- * planes are computed first, their exchange runs on comm_stream while the
- * interior computes on `stream`.  A one-rank RCCL comm may name itself
- * (rank 0) as lo_peer and hi_peer: the exchange is then an RCCL send/recv to
- * self, a timing rehearsal of a middle rank's pass sequence on one GPU (RCCL
- * kernels running beside the interior); its result is not a solve. */
+ * planes are computed first, their exchange runs beside the interior (RCCL:
+ * on comm_stream; copy engines: on the comm's own copy streams) while the
+ * interior computes on `stream`.  A one-rank comm may name itself (rank 0) as
+ * lo_peer and hi_peer: the exchange is then a copy to itself, a timing
+ * rehearsal of a middle rank's pass sequence on one GPU; its result is not a
+ * solve. */
 int cfd_slab_jacobi3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
                           float *rhs_ws, const uint8_t *mask, int nz_local, int ghost, int ny,
                           int nx, int lo_peer, int hi_peer, int z_update_begin, int z_update_end,
@@ -265,12 +291,15 @@ int cfd_jacobi3d_sweep_f32(const float *in, float *out, const float *div, const 
 /* Distributed red-black GS (config 5), same plan arguments as
  * cfd_slab_jacobi3d_f32 plus z_global_offset = global index of local plane 0
  * (SlabPlan.z_lo - ghost): colours are global, so the result is bit-identical
- * to cfd_rbgs3d_f32 on the whole grid.  ghost 2 + no mask + phi_tmp: one fused
- * pass per iteration (boundary planes first, their exchange overlapped with
- * the interior when overlap != 0); otherwise in-place colour passes with a
- * ghost exchange after each colour.  The stop rule uses the global
- * max|change| (ncclAllReduce(max) of one float per iteration; none when
- * tolerance <= 0).  ws / iters_done as in cfd_rbgs3d_f32. */
+ * to cfd_rbgs3d_f32 on the whole grid.  ghost >= 2 + no mask + phi_tmp: fused
+ * out-of-place passes, one iteration each, or two with ghost 4 (the default
+ * at ghost 4; cfd_set_jacobi3d_blocking(2 or 3, ...) keeps one): boundary
+ * planes first, their exchange overlapped with the interior when overlap != 0;
+ * otherwise in-place colour passes with a ghost exchange after each colour.
+ * The stop rule uses the global max|change| of each iteration (RCCL:
+ * ncclAllReduce(max); copy engines: the sync kernel's gather over every
+ * rank's flag block; none when tolerance <= 0).  ws / iters_done as in
+ * cfd_rbgs3d_f32. */
 int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp,
                         const uint8_t *mask, int nz_local, int ghost, int ny, int nx, int lo_peer,
                         int hi_peer, int z_update_begin, int z_update_end, int z_global_offset,
@@ -319,8 +348,9 @@ int cfd_set_jacobi3d_config(int variant, int waves, int zchunk);
  * or residual): steps = sweeps fused per HBM pass (0 = auto, 1 = off, 2..4;
  * a remainder of iters % steps runs as a shorter pass); rows = output rows
  * per tile of the 2-sweep kernel (0 auto, 5, 13); zchunk = planes per tile.
- * Fused or not, results are bit-identical.  The red-black GS solves use the
- * 2-level kernel whenever blocking is not off. */
+ * Fused or not, results are bit-identical.  The red-black GS solves run
+ * fused out-of-place passes whenever blocking is not off: steps = their
+ * half-sweeps per pass on one GPU (auto 4, see cfd_get_rbgs3d_levels). */
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk);
 /* Jacobi sweeps per blocked pass currently in effect (2..4). */
 int cfd_get_jacobi3d_levels(void);

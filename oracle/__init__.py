@@ -64,6 +64,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_jacobi3d_f32_mt.argtypes = [_f32p, _u8p, _f32p, _i, _i, _i, _d, _f, _i]
         L.oracle_rbgs3d_f32_mt.argtypes = [_f32p, _f32p, _u8p, _i, _i, _i, _d, _d, _d, _f, _i, _d]
         L.oracle_rbgs3d_f32_mt.restype = _i
+        L.oracle_rbgs2d_f32_mt.argtypes = [_f32p, _f32p, _u8p, _i, _i, _d, _d, _f, _i, _d]
+        L.oracle_rbgs2d_f32_mt.restype = _i
         L.oracle_threads.restype = _i
         L.oracle_predictor2d_f32.argtypes = [_f32p, _f32p, _f32p, _i, _i, _d, _d, _f, _i] + [_f32p] * 7
         L.oracle_divergence2d_f32.argtypes = [_f32p, _f32p, _f32p, _i, _i, _d, _d]
@@ -110,13 +112,16 @@ def jacobi3d(div, phi0=None, *, h, dt, iters, mask=None, mt=False):
     return phi
 
 
-def rbgs2d(div, phi0=None, *, dx, dy, dt, iters, tol, mask=None):
-    """a3 (v5.py:202-226), serial semantics.  Returns (phi, iterations_done)."""
+def rbgs2d(div, phi0=None, *, dx, dy, dt, iters, tol, mask=None, mt=False):
+    """a3 (v5.py:202-226), serial semantics.  Returns (phi, iterations_done).
+    ``mt``: the OpenMP form (rows of a colour over host threads, as the
+    reference's prange; bit-identical)."""
     div = np.ascontiguousarray(div, dtype=np.float32)
     phi = np.zeros_like(div) if phi0 is None else np.array(phi0, dtype=np.float32, copy=True)
     keep, mp = _mask_ptr(mask, div.shape)
-    done = lib().oracle_rbgs2d_f32(phi, div, mp, div.shape[0], div.shape[1], float(dx), float(dy),
-                                   np.float32(dt), int(iters), float(tol))
+    fn = lib().oracle_rbgs2d_f32_mt if mt else lib().oracle_rbgs2d_f32
+    done = fn(phi, div, mp, div.shape[0], div.shape[1], float(dx), float(dy), np.float32(dt), int(iters),
+              float(tol))
     return phi, done
 
 
@@ -232,6 +237,7 @@ class OracleSolver:
     identical inputs.  Returns dt like the reference."""
 
     numpy_jacobi = False  # True: the Jacobi branch in the reference's NumPy form (jacobi2d_numpy)
+    mt = False            # True: the GS solve on all host threads (oracle_rbgs2d_f32_mt)
 
     def __init__(self, cfg, u, v, cylinder_mask, ibm_mask, y):
         self.cfg = cfg
@@ -301,7 +307,7 @@ class OracleSolver:
         diag = {"pre_div_max": np.max(np.abs(self.div_u_star))}
         if c.use_fast_pressure:
             self.phi, _ = rbgs2d(self.div_u_star, dx=c.dx, dy=c.dy, dt=c.dt, iters=c.pressure_iterations,
-                                 tol=c.pressure_tolerance, mask=self.cylinder_mask)
+                                 tol=c.pressure_tolerance, mask=self.cylinder_mask, mt=self.mt)
         elif self.numpy_jacobi:
             self.phi = jacobi2d_numpy(self.div_u_star, dx=c.dx, dt=c.dt, iters=c.pressure_iterations,
                                       mask=self.cylinder_mask if self.cylinder_mask.any() else None)

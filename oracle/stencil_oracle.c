@@ -293,6 +293,47 @@ int oracle_rbgs3d_f32_mt(float *phi, const float *div, const uint8_t *mask,
     return it;
 }
 
+/* a3 with the rows of each colour split over the host's threads: the
+ * reference's own parallel structure (`for i in prange(1, ny - 1)` inside each
+ * colour, v5.py:211-222).  Bit-identical to oracle_rbgs2d_f32: a cell of one
+ * colour reads only cells of the other, and max|change| is order-free.  The
+ * all-core CPU baseline of the v5 cylinder step. */
+int oracle_rbgs2d_f32_mt(float *phi, const float *div, const uint8_t *mask,
+                         int ny, int nx, double dx, double dy, float dt,
+                         int iters, double tol) {
+    const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy);
+    const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv));
+    const float cx = (float)dx2_inv, cy = (float)dy2_inv, cd = (float)denom_inv;
+    const float dt_inv = 1.0f / dt;
+    const float ftol = (float)tol;
+    int it;
+    for (it = 0; it < iters; ++it) {
+        float max_change = 0.0f;
+        for (int color = 0; color < 2; ++color) {
+#pragma omp parallel
+            {
+                float mloc = 0.0f;
+#pragma omp for schedule(static)
+                for (int i = 1; i < ny - 1; ++i)
+                    for (int j = 1 + (i + color) % 2; j < nx - 1; j += 2) {
+                        if (mask && mask[IDX(i, j)]) continue;
+                        float rhs = -div[IDX(i, j)] * dt_inv;
+                        float a = cx * (phi[IDX(i, j + 1)] + phi[IDX(i, j - 1)]);
+                        float b = cy * (phi[IDX(i + 1, j)] + phi[IDX(i - 1, j)]);
+                        float pn = ((a + b) - rhs) * cd;
+                        float change = fabsf(pn - phi[IDX(i, j)]);
+                        if (change > mloc) mloc = change;
+                        phi[IDX(i, j)] = pn;
+                    }
+#pragma omp critical
+                if (mloc > max_change) max_change = mloc;
+            }
+        }
+        if (max_change < ftol) return it + 1;
+    }
+    return it;
+}
+
 /* ---- a6: compute_supg_stabilization_fast, v5.py:149-162 --------------- */
 static float supg_tau(float u, float v, float nu, double h, float dt) {
     /* NumPy float32 scalar `u**2` and `** 0.5` both go through libm powf,

@@ -11,11 +11,14 @@ gaps) relative to the single-domain solve, without the xGMI links:
 
     python scripts/slab_rehearsal.py [--ranks 8] [--workload jacobi|rbgs] [--n 1024]
 
---rccl-self instead times ONE middle rank of an R-rank job in isolation: a
-one-rank RCCL communicator peered with itself, so the pass sequence is the
-real one (boundary planes, RCCL send/recv kernels on the comm stream beside the
-interior launch, the GS max-allreduce) with local copies for the xGMI
-transfers.  Its result is not a solve (timing only).
+--rccl-self (alias --self) instead times ONE middle rank of an R-rank job in
+isolation: a one-rank comm peered with itself, so the pass sequence is the
+real one (boundary planes, the exchange beside the interior launch, the GS
+max-reduce) with local copies for the xGMI transfers.  --transport ce (the
+default): the copy engines write the boundary planes into the rank's own
+ghost planes at ~58 GB/s per direction (about one xGMI link's rate) and the
+sync kernel waits for them; --transport rccl: RCCL send/recv kernels on the
+reserved CUs.  Its result is not a solve (timing only).
 """
 import argparse
 import json
@@ -44,11 +47,12 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--rccl-self", action="store_true")
+    ap.add_argument("--rccl-self", "--self", dest="rccl_self", action="store_true")
+    ap.add_argument("--transport", default="ce", choices=["ce", "rccl"])
     ap.add_argument("--comm-priority", type=int, default=1, help="1: high-priority comm stream")
     ap.add_argument("--prefetch", type=int, default=0, help="cfd_set_jacobi3d_prefetch (0 auto, 1 DMA, 2 regs)")
     ap.add_argument("--tb", type=int, default=0,
-                    help="--rccl-self red-black GS: 4 = two iterations per pass (4-deep ghosts), else one")
+                    help="--self red-black GS: 0 or 4 = two iterations per pass (4-deep ghosts), 2 = one")
     a = ap.parse_args()
     if a.rccl_self:
         return rccl_self(a)
@@ -116,19 +120,21 @@ def rccl_self(a):
     n, R = a.n, a.ranks
     nz = a.nz or n
     gs = a.workload == "rbgs"
-    G = (4 if a.tb == 4 else 2) if gs else 3
-    if gs and a.tb == 4:
-        call("cfd_set_jacobi3d_blocking", 4, 0, 0)  # rbgs3d_iters_per_pass() = 2
+    G = (4 if a.tb in (0, 4) else 2) if gs else 3
+    if gs and a.tb:
+        call("cfd_set_jacobi3d_blocking", a.tb, 0, 0)  # rbgs3d_iters_per_pass(): 2 at 4, else 1
     nzl = nz // R
     shape = (nzl + 2 * G, n, n)
     h = 1.0 / (n - 1)
     dt = np.float32(5e-5)
-    comm = S.RcclComm(0, 1)
+    comm = S.make_comm(0, 1, a.transport)
     call("cfd_set_jacobi3d_prefetch", a.prefetch)
     g = torch.Generator(device=dev).manual_seed(1234)
     div = torch.randn(shape, generator=g, device=dev) * 1e-3
     phi, tmp = torch.zeros_like(div), torch.zeros_like(div)
     rhs = torch.empty_like(div)
+    if a.transport == "ce":
+        comm.attach(phi, tmp)
     cs = torch.cuda.Stream(device=dev, priority=-1 if a.comm_priority else 0)
     ws = torch.empty(int(lib().cfd_rbgs_workspace_bytes(a.iters)), dtype=torch.uint8, device=dev)
     done = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -152,9 +158,11 @@ def rccl_self(a):
         solve()
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / a.steps
+    if a.transport == "ce":
+        comm.status()  # raises if a sync kernel timed out
     comm.close()
     cells = nzl * (n - 2) * (n - 2) * a.iters
-    print(json.dumps({"workload": a.workload, "mode": "rccl-self (one middle rank of R)", "ranks": R,
+    print(json.dumps({"workload": a.workload, "mode": f"{a.transport}-self (one middle rank of R)", "ranks": R,
                       "grid": [nz, n, n], "nz_local": nzl, "ghost": G, "iters": a.iters,
                       "overlap": not a.no_overlap, "prefetch": a.prefetch,
                       "comm_priority": a.comm_priority, "ms_per_solve": round(t * 1e3, 3),

@@ -327,6 +327,54 @@ def gen_steps_late(ref) -> None:
         print("wrote", name)
 
 
+def gen_steps_f64(ref) -> None:
+    """Three time_step() calls with memory_efficient=False (v5.py:287-296:
+    every field float64, the dtype-generic kernels then run in float64), for
+    both pressure branches, from the potential-flow initial condition."""
+    for fast in (True, False):
+        cfg = make_cfg(ref, nx=120, ny=36, pressure_iterations=200, use_fast_pressure=fast,
+                       memory_efficient=False)
+        with _quiet_cwd():
+            solver = ref.OptimizedTurbulentSolver(cfg)
+        assert solver.u.dtype == np.float64
+        rec = {"u0": solver.u.copy(), "v0": solver.v.copy(), "cylinder_mask": solver.cylinder_mask,
+               "ibm_mask": solver.ibm_mask}
+        for s in range(3):
+            dt = solver.time_step()
+            rec[f"dt{s}"] = np.float64(dt)
+            for f, a in (("u", solver.u), ("v", solver.v), ("phi", solver.phi), ("u_star", solver.u_star),
+                         ("v_star", solver.v_star), ("div", solver.div_u_star), ("tau", solver.tau_supg)):
+                rec[f"{f}{s + 1}"] = a.copy()
+        rec["energy"] = np.array([e for _, e in solver.energy_history], np.float64)
+        name = f"step_v5_120x36_n3_f64_{'gs' if fast else 'jacobi'}.npz"
+        np.savez_compressed(OUT / name, **rec)
+        print("wrote", name, rec["u3"].dtype)
+
+
+def gen_steps_fixed_dt(ref) -> None:
+    """adaptive_dt=False (v5.py:317-318): adaptive_time_step returns the
+    Python float dt_base, which meets the float32 fields under NEP 50 (rounded
+    to float32 per operation); two GS-branch steps, and two from step 1500
+    (where the adaptive branch would otherwise take the CFL dt)."""
+    rec = {}
+    for start in (0, 1500):
+        cfg = make_cfg(ref, nx=120, ny=36, pressure_iterations=200, adaptive_dt=False, dt_base=7e-5)
+        with _quiet_cwd():
+            solver = ref.OptimizedTurbulentSolver(cfg)
+        solver.step = start
+        for s in range(2):
+            dt = solver.time_step()
+            assert type(dt) is float
+            k = f"s{start}_{s + 1}"
+            rec[f"dt_{k}"] = np.float64(dt)
+            for f, a in (("u", solver.u), ("v", solver.v), ("phi", solver.phi), ("u_star", solver.u_star),
+                         ("div", solver.div_u_star), ("tau", solver.tau_supg)):
+                rec[f"{f}_{k}"] = a.copy()
+        rec[f"energy_s{start}"] = np.array([e for _, e in solver.energy_history], np.float64)
+    np.savez_compressed(OUT / "step_v5_120x36_fixed_dt.npz", **rec)
+    print("wrote step_v5_120x36_fixed_dt.npz")
+
+
 def gen_health(ref) -> None:
     """monitor_simulation_health (v5.py:599-613) on crafted states: healthy,
     non-finite u / v, over-speed, and a divergence between the two
@@ -355,18 +403,23 @@ def gen_health(ref) -> None:
     print("wrote health_v5_120x36.npz", {k: bool(v) for k, v in out.items() if "_ok_" in k})
 
 
+GENERATORS = {"jacobi": gen_jacobi, "jacobi_rect": gen_jacobi_rect, "rbgs": gen_rbgs,
+              "predictor": gen_predictor, "steps": gen_steps, "diagnostics": gen_diagnostics,
+              "steps_late": gen_steps_late, "health": gen_health, "steps_f64": gen_steps_f64,
+              "steps_fixed_dt": gen_steps_fixed_dt}
+
+
 def main() -> None:
+    """python tests/golden/make_golden.py [generator ...]  (default: all)"""
     if not REF_FILE.exists():
         raise SystemExit(f"reference not found at {REF_FILE}; fixtures are generated in the build container only")
+    names = sys.argv[1:] or list(GENERATORS)
+    unknown = [n for n in names if n not in GENERATORS]
+    if unknown:
+        raise SystemExit(f"unknown generators {unknown}; choose from {list(GENERATORS)}")
     ref = load_reference()
-    gen_jacobi(ref)
-    gen_jacobi_rect(ref)
-    gen_rbgs(ref)
-    gen_predictor(ref)
-    gen_steps(ref)
-    gen_diagnostics(ref)
-    gen_steps_late(ref)
-    gen_health(ref)
+    for n in names:
+        GENERATORS[n](ref)
 
 
 if __name__ == "__main__":

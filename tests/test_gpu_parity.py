@@ -20,7 +20,7 @@ from cfd_simulations_amd import slab as S
 from cfd_simulations_amd._lib import call, lib, ptr, stream_handle
 from cfd_simulations_amd.solver import OptimizedTurbulentConfig, OptimizedTurbulentSolver
 
-from conftest import rel_linf
+from conftest import ROOT, rel_linf
 
 pytestmark = pytest.mark.gpu
 
@@ -641,6 +641,84 @@ def test_slab_rccl_self_peered_rehearsal(gs):
         comm.close()
     assert np.isfinite(outs[0]).all() and np.abs(outs[0]).max() > 0
     assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
+
+
+@pytest.mark.parametrize("gs", [False, True])
+def test_slab_copy_engine_self_peered_rehearsal(gs):
+    """The copy-engine transport's rehearsal mode (scripts/slab_rehearsal.py
+    --self): a one-rank comm named as both neighbours -- SDMA copies of the
+    boundary planes into its own ghost planes, the sequence words, the sync
+    kernel's waits (and for the GS, its one-rank max gather).  Not a solve, but
+    overlapped must equal serial bit for bit, repeat exactly, and no wait may
+    time out."""
+    nzl, ny, nx, iters = 24, 34, 64, 10
+    G = 4 if gs else 3
+    rng = np.random.default_rng(5)
+    div = dev(rng.standard_normal((nzl + 2 * G, ny, nx)).astype(np.float32) * np.float32(1e-3))
+    comm = S.CopyEngineComm(0, 1)
+    phi, tmp = torch.zeros_like(div), torch.zeros_like(div)
+    comm.attach(phi, tmp)
+    ws = torch.zeros(int(lib().cfd_rbgs_workspace_bytes(iters)), dtype=torch.uint8, device=DEV)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    rhs = torch.empty_like(div)
+    outs = []
+    try:
+        for overlap in (0, 1, 1):
+            phi.zero_()
+            tmp.zero_()
+            if gs:
+                call("cfd_slab_rbgs3d_f32", comm.handle, ptr(div), ptr(phi), ptr(tmp), None, nzl, G, ny, nx,
+                     0, 0, G, nzl + G, 100, 0.05, 0.05, 0.05, 1e-2, iters, 1e-30, ptr(ws), ptr(done),
+                     overlap, stream_handle(), None)
+            else:
+                call("cfd_slab_jacobi3d_zero_f32", comm.handle, ptr(div), ptr(phi), ptr(tmp), ptr(rhs), nzl, G,
+                     ny, nx, 0, 0, G, nzl + G, 0.05, 1e-3, iters, overlap, stream_handle(), None)
+            outs.append(host(phi))
+        assert comm.status() == 0
+    finally:
+        comm.close()
+    assert np.isfinite(outs[0]).all() and np.abs(outs[0]).max() > 0
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
+
+
+@pytest.mark.parametrize("ghost", [1, 2, 3, 4])
+@pytest.mark.parametrize("overlap", [False, True])
+def test_slab_copy_engine_single_rank(overlap, ghost):
+    """cfd_slab_jacobi3d_f32 / cfd_slab_rbgs3d_f32 on a one-rank copy-engine
+    comm (no neighbours: the drivers' pass sequence with nothing to send)."""
+    n, iters = 40, 7
+    rng = np.random.default_rng(10)
+    div = rng.standard_normal((n, n, n + 8)).astype(np.float32)
+    ref = oracle.jacobi3d(div, h=0.05, dt=np.float32(1e-3), iters=iters)
+    comm = S.CopyEngineComm(0, 1)
+    try:
+        plan = S.SlabPlan(n, 1, 0, ghost=ghost)
+        sj = S.SlabJacobi3D(plan, n, n + 8, 0.05, np.float32(1e-3), comm)
+        sj.div.copy_(dev(plan.scatter(div)))
+        sj.solve(iters, overlap=overlap)
+        assert np.array_equal(host(sj.owned()), ref)
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_slab_copy_engine_multiprocess(world):
+    """The copy-engine transport between real processes: `world` ranks, each
+    its own process on this GPU (torch.distributed.run, gloo for the IPC
+    handle blobs), mapping each other's buffers and flag blocks.  Jacobi
+    (ghost 1 and 3, zero and nonzero start, overlap on / off) and red-black GS
+    (one and two iterations per pass, fixed count and early stop through the
+    gathered global maxima): the gathered owned planes equal the single-domain
+    oracle bit for bit (scripts/multirank_check.py)."""
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(29600 + world), str(ROOT / "scripts" /
+                                                                                "multirank_check.py"),
+           "--share-gpu", "--transport", "ce", "--quick", "--n", "48"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT))
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "MULTIRANK OK" in out, out[-4000:]
 
 
 # ------------------------------------------------- multi-rank, one GPU (threads)

@@ -109,3 +109,23 @@ def test_log_lines_match_reference(golden):
         s.time_step()
         lines += s.log_lines()
     assert lines == [str(x) for x in g["log_lines"]]
+
+
+@pytest.mark.parametrize("start", [0, 1500])
+def test_time_step_fixed_dt_bitexact(golden, start):
+    """adaptive_dt=False (v5.py:317-318): dt is the Python float dt_base
+    (7e-5 here), returned as such and rounded to float32 where it meets the
+    fields; two steps from 0 and from 1500, every field bit-exact."""
+    g = golden("step_v5_120x36_fixed_dt.npz")
+    c = OptimizedTurbulentConfig(nx=120, ny=36, pressure_iterations=200, adaptive_dt=False, dt_base=7e-5)
+    s = OptimizedTurbulentSolver(c)
+    s.step = start
+    for k in (1, 2):
+        dt = s.time_step()
+        key = f"s{start}_{k}"
+        assert type(dt) is float and dt == g[f"dt_{key}"]
+        for f, t in (("u", s.u), ("v", s.v), ("phi", s.phi), ("u_star", s.u_star), ("div", s.div_u_star),
+                     ("tau", s.tau_supg)):
+            assert np.array_equal(host(t), g[f"{f}_{key}"]), (f, k)
+    e = np.array([v for _, v in s.energy_history])
+    assert np.allclose(e, g[f"energy_s{start}"], rtol=1e-6, atol=0)

@@ -36,10 +36,14 @@ def test_jacobi_numpy_baseline_bitexact(golden, name):
 
 
 @pytest.mark.parametrize("name", RBGS)
-def test_rbgs_oracle_bitexact(golden, name):
+@pytest.mark.parametrize("mt", [False, True])
+def test_rbgs_oracle_bitexact(golden, name, mt):
+    """The serial restatement and the OpenMP one (rows of a colour over host
+    threads, the reference's prange; the cylinder step's all-core CPU
+    baseline) against the reference's outputs."""
     d = golden(name + ".npz")
     phi, done = oracle.rbgs2d(d["div"], dx=float(d["dx"]), dy=float(d["dy"]), dt=d["dt"],
-                              iters=int(d["iters"]), tol=float(d["tol"]), mask=d["mask"])
+                              iters=int(d["iters"]), tol=float(d["tol"]), mask=d["mask"], mt=mt)
     assert np.array_equal(phi, d["phi"])
     if "iters_done" in d:
         assert done == int(d["iters_done"])
@@ -234,3 +238,25 @@ def test_cavity_cpu_numpy_path_equals_oracle():
     assert (a.u[-1] == 1.0).all() and (a.u[:-1, 0] == 0).all() and (a.u[:-1, -1] == 0).all()
     assert (a.u[0] == 0).all() and (a.v[[0, -1]] == 0).all()
     assert np.abs(a.u[1:-1, 1:-1]).max() > 0  # the lid drives the interior
+
+
+@pytest.mark.parametrize("start", [0, 1500])
+def test_oracle_fixed_dt_steps_bitexact(golden, start):
+    """adaptive_dt=False (v5.py:317-318): adaptive_time_step returns the
+    Python float dt_base, which meets the float32 fields under NEP 50; from
+    step 0 and from step 1500 (where the adaptive branch would take the CFL
+    dt), against the reference's own two steps."""
+    d = golden("step_v5_120x36_n3_gs.npz")
+    g = golden("step_v5_120x36_fixed_dt.npz")
+    c = _cfg(nx=120, ny=36, pressure_iterations=200, adaptive_dt=False, dt_base=7e-5)
+    _, y, _, _ = host_grid(c)
+    s = oracle.OracleSolver(c, d["u0"], d["v0"], d["cylinder_mask"], d["ibm_mask"], y)
+    s.step = start
+    for k in (1, 2):
+        dt = s.time_step()
+        key = f"s{start}_{k}"
+        assert type(dt) is float and dt == g[f"dt_{key}"] == 7e-5
+        for f, a in (("u", s.u), ("v", s.v), ("phi", s.phi), ("u_star", s.u_star), ("div", s.div_u_star),
+                     ("tau", s.tau_supg)):
+            assert np.array_equal(a, g[f"{f}_{key}"]), (f, k)
+    assert np.array_equal(np.array([v for _, v in s.energy_history]), g[f"energy_s{start}"])
