@@ -33,7 +33,7 @@ from cfd_simulations_amd import slab as S  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--share-gpu", action="store_true")
-    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--transport", default="ce", choices=["ce", "rccl"])
     ap.add_argument("--quick", action="store_true", help="fewer cases")
     a = ap.parse_args()
@@ -41,7 +41,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(0 if a.share_gpu else local)
     dist.init_process_group("gloo")
-    n = a.n
+    n = a.size
     nz, ny, nx = n, n - 6, n + 8
     rng = np.random.default_rng(77)
     div = rng.standard_normal((nz, ny, nx)).astype(np.float32)

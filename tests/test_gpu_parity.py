@@ -715,7 +715,7 @@ def test_slab_copy_engine_multiprocess(world):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(29600 + world), str(ROOT / "scripts" /
                                                                                 "multirank_check.py"),
-           "--share-gpu", "--transport", "ce", "--quick", "--n", "48"]
+           "--share-gpu", "--transport", "ce", "--quick", "--size", "48"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT))
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "MULTIRANK OK" in out, out[-4000:]
