@@ -60,6 +60,25 @@ PROTOTYPES = {
     "cfd_vorticity2d_f32": (c_int, [P, P, P, P, c_int, c_int, c_double, c_double, P]),
     "cfd_nonfinite_count_f32": (c_int, [P, P, c_size_t, P, P]),
     "cfd_numpy_powf_f32": (c_int, [P, c_float, P, c_size_t, P]),
+    "cfd_supg_tau2d_f64": (c_int, [P, P, P, c_double, P, c_int, c_int, c_double, c_double, c_double, P]),
+    "cfd_convection_supg2d_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_double, P]),
+    "cfd_convection_upwind2d_f64": (c_int, [P, P, P, P, c_int, c_int, c_double, c_double, P]),
+    "cfd_laplacian2d_f64": (c_int, [P, P, c_double, P, c_int, c_int, c_double, c_double, P]),
+    "cfd_predictor2d_f64": (c_int, [P, P, P, c_double, P, P, P, c_int, c_int, c_double, c_double,
+                                    c_double, c_int, P]),
+    "cfd_divergence2d_f64": (c_int, [P, P, P, c_int, c_int, c_double, c_double, P, P]),
+    "cfd_gradient2d_f64": (c_int, [P, P, P, c_int, c_int, c_double, c_double, P]),
+    "cfd_project2d_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_double, c_double, P, P]),
+    "cfd_clean_divergence2d_f64": (c_int, [P, P, c_int, c_int, c_double, c_double, c_int, P, P]),
+    "cfd_apply_bc2d_f64": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_int, P]),
+    "cfd_apply_lid_bc2d_f64": (c_int, [P, P, c_int, c_int, c_double, P]),
+    "cfd_apply_ibm2d_f64": (c_int, [P, P, P, c_int, c_double, P]),
+    "cfd_clip_f64": (c_int, [P, c_size_t, c_double, c_double, P]),
+    "cfd_absmax2_f64": (c_int, [P, P, c_size_t, P, P]),
+    "cfd_energy_mean2d_f64": (c_int, [P, P, c_size_t, P, P]),
+    "cfd_vorticity2d_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_double, P]),
+    "cfd_nonfinite_count_f64": (c_int, [P, P, c_size_t, P, P]),
+    "cfd_rbgs2d_f64": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_float, c_int, c_double, P, P, P]),
     "cfd_comm_unique_id": (c_int, [P, c_size_t]),
     "cfd_comm_init": (c_int, [P, c_int, c_int, ctypes.POINTER(c_void_p)]),
     "cfd_comm_destroy": (c_int, [P]),

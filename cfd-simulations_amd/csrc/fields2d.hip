@@ -714,7 +714,8 @@ int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star
 }
 
 size_t cfd_clean_divergence_workspace_bytes(int ny, int nx) {
-    return 2 * sizeof(float) * (size_t)(ny > 0 ? ny : 0) * (size_t)(nx > 0 ? nx : 0);
+    // phi and div scratch fields, sized for float64 (cfd_clean_divergence2d_f64)
+    return 2 * sizeof(double) * (size_t)(ny > 0 ? ny : 0) * (size_t)(nx > 0 ? nx : 0);
 }
 
 int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, double dy,

@@ -362,7 +362,11 @@ __device__ __noinline__ void tbr_halo_wave_call(const TbrArgs a, float *smem, in
 // MODE kRbgs: K red-black half-sweeps per pass, level l = half-sweep h0+l-1
 // (colour (h0+l-1) & 1, iteration (h0+l-1) / 2), so a pass may start or end
 // inside an iteration; see rbgs3d_tbr_pass for the stop rule and the rollback.
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F = 0>
+// SHIFTQ: shifting register queues instead of the rotated ones (below) --
+// for short z-chunks whose step count is no multiple of 6, where the rotated
+// march would run up to 5 steps that store nothing (the slab boundary
+// launches: 7 steps of which 12 would run)
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F = 0, bool SHIFTQ = false>
 __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     constexpr int NR = NWR * RPW + 2;  // level-0 rows per tile
     constexpr int W = NR - 2 * K;      // output rows
@@ -482,7 +486,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // to 3 levels: -2.3 % per pass for the Jacobi at K = 3, -2.9 % for the
     // red-black GS (whose level queues hold pairs, so its two march copies fit
     // with them at 2 rows per wave); K = 4 spills with them
-    constexpr bool ROT = DMA && K <= 3 && (MODE == kJacobi || RPW <= 2);
+    constexpr bool ROT = DMA && K <= 3 && (MODE == kJacobi || RPW <= 2) && !SHIFTQ;
     const int zl = ROT ? zs + 6 * ((zl0 - zs + 6) / 6) - 1 : zl0;
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
@@ -1032,6 +1036,12 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
     g_last_shape[2] = best->rpw;
     g_last_shape[3] = best_zlen;
     const int blocks = a.nseg * a.ntile_y * ceil_div(L, best_zlen);
+    // short Jacobi chunks whose step count (zlen + 2K - 2) is no multiple of
+    // 6: shifting queues (SHIFTQ) run exactly their steps; the rotated ones
+    // save ~2 % per step but would run up to 5 extra (the slab boundary
+    // launches: 3 planes = 7 steps, 12 rotated)
+    const int nsteps = best_zlen + 2 * best->K - 2;
+    const bool shiftq = MODE == kJacobi && pd == 1 && best->K == 3 && nsteps % 6 != 0 && nsteps < 216;
 #define CFD_TBR_L(KV, NW, RP, PR, PDV) \
     hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, PR, PDV, MODE>), dim3(blocks), dim3((NW + 1) * 64), 0, s, a)
 #define CFD_TBR(KV, NW, RP)                                                                   \
@@ -1044,9 +1054,27 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
             if (pre) CFD_TBR_L(KV, NW, RP, true, 1); else CFD_TBR_L(KV, NW, RP, false, 1);      \
         }                                                                                     \
     } while (0)
-    // shapes with a first-pass variant (all on the LDS-DMA path)
+    // shapes with a first-pass variant (all on the LDS-DMA path); K = 3 ones
+    // also with shifting queues
 #define CFD_TBRF(KV, NW, RP)                                                                 \
     do {                                                                                     \
+        if constexpr (MODE == kJacobi && KV == 3) {                                          \
+            if (shiftq) {                                                                    \
+                if (first == (kFirstRhs | kFirstZero))                                       \
+                    hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, false, 1, MODE, kFirstRhs | kFirstZero, true>), \
+                                       dim3(blocks), dim3((NW + 1) * 64), 0, s, a);          \
+                else if (first == kFirstRhs)                                                 \
+                    hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, false, 1, MODE, kFirstRhs, true>), \
+                                       dim3(blocks), dim3((NW + 1) * 64), 0, s, a);          \
+                else if (pre)                                                                \
+                    hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, true, 1, MODE, 0, true>),   \
+                                       dim3(blocks), dim3((NW + 1) * 64), 0, s, a);          \
+                else                                                                         \
+                    hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, false, 1, MODE, 0, true>),  \
+                                       dim3(blocks), dim3((NW + 1) * 64), 0, s, a);          \
+                break;                                                                       \
+            }                                                                                \
+        }                                                                                    \
         if constexpr (MODE == kJacobi) {                                                     \
             if (first == (kFirstRhs | kFirstZero)) {                                         \
                 hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, false, 1, MODE, kFirstRhs | kFirstZero>), \

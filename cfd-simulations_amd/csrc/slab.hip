@@ -124,18 +124,25 @@ struct CeState {
     hipStream_t xs[2] = {nullptr, nullptr};  // copy streams: to lo, to hi
     hipEvent_t xev[2] = {nullptr, nullptr};
     bool used[2] = {false, false};
-    std::vector<CeBlob> blobs;      // every rank's, after import
     struct Map {
         int rank;
         hipIpcMemHandle_t h;
         char *base;
     };
     std::vector<Map> maps;          // IPC mappings opened by this process
-    std::vector<unsigned *> peer_flags;
-    float *mine[2] = {nullptr, nullptr};
-    size_t mine_n = 0;
+    std::vector<unsigned *> peer_flags;  // every rank's flag block, mapped (after the first import)
+    // attached buffer pairs, in the (collective) order of their imports: a
+    // solve finds its pair among them; every rank holds the same list
+    struct Attachment {
+        float *mine[2];
+        size_t n;
+        std::vector<CeBlob> blobs;  // every rank's export of this pair
+    };
+    std::vector<Attachment> att;
+    int cur = -1;                   // the attachment of the solve in progress
+    float *pend[2] = {nullptr, nullptr};  // exported, not yet imported
+    size_t pend_n = 0;
     unsigned sent[2] = {0, 0}, recvd[2] = {0, 0}, gathered = 0;
-    bool attached = false;
 };
 
 struct SlabComm {
@@ -441,12 +448,13 @@ static int ce_map(CeState &ce, int rank, const hipIpcMemHandle_t &h, char **base
 // buffer bi (0 = phi, 1 = phi_tmp as attached) of rank `peer`, as mapped here
 static int ce_peer_buf(SlabComm *c, int peer, int bi, float **buf, size_t *n) {
     CeState &ce = *c->ce;
+    const CeState::Attachment &at = ce.att[ce.cur];
     if (peer == c->rank) {
-        *buf = ce.mine[bi];
-        *n = ce.mine_n;
+        *buf = at.mine[bi];
+        *n = at.n;
         return CFD_OK;
     }
-    const CeBlob &b = ce.blobs[peer];
+    const CeBlob &b = at.blobs[peer];
     char *base = nullptr;
     int rc = ce_map(ce, peer, b.buf_h[bi], &base);
     if (rc) return rc;
@@ -462,7 +470,8 @@ static int ce_peer_buf(SlabComm *c, int peer, int bi, float **buf, size_t *n) {
 static int exchange_ce(SlabComm *c, const float *a, int nzl, int G, size_t plane, int lo, int hi,
                        hipEvent_t ready) {
     CeState &ce = *c->ce;
-    const int bi = a == ce.mine[0] ? 0 : a == ce.mine[1] ? 1 : -1;
+    const CeState::Attachment &at = ce.att[ce.cur];
+    const int bi = a == at.mine[0] ? 0 : a == at.mine[1] ? 1 : -1;
     CFD_REQUIRE(bi >= 0, "slab (copy engines): exchange of a buffer that was not attached");
     const size_t n = (size_t)G * plane;
     for (int d = 0; d < 2; ++d) {
@@ -521,12 +530,19 @@ static int ce_join(SlabComm *c, hipStream_t s) {
     return CFD_OK;
 }
 
+// selects the attachment of phi / phi_tmp (either order; phi_tmp NULL: any
+// pair holding phi) for the solve that follows
 static int ce_check_attached(SlabComm *c, const float *phi, const float *phi_tmp) {
     CeState &ce = *c->ce;
-    CFD_REQUIRE(ce.attached && (phi == ce.mine[0] || phi == ce.mine[1]) &&
-                    (!phi_tmp || phi_tmp == (phi == ce.mine[0] ? ce.mine[1] : ce.mine[0])),
-                "slab (copy engines): phi / phi_tmp are not the buffers attached with "
-                "cfd_comm_ipc_import");
+    ce.cur = -1;
+    for (int k = (int)ce.att.size() - 1; k >= 0 && ce.cur < 0; --k) {
+        const CeState::Attachment &at = ce.att[k];
+        if ((phi == at.mine[0] || phi == at.mine[1]) &&
+            (!phi_tmp || phi_tmp == (phi == at.mine[0] ? at.mine[1] : at.mine[0])))
+            ce.cur = k;
+    }
+    CFD_REQUIRE(ce.cur >= 0,
+                "slab (copy engines): phi / phi_tmp are not a pair attached with cfd_comm_ipc_import");
     return CFD_OK;
 }
 
@@ -607,7 +623,7 @@ int cfd_comm_init_ipc(int nranks, int rank, void **comm) {
         CFD_CHECK_HIP(hipStreamCreateWithFlags(&ce.xs[d], hipStreamNonBlocking));
         CFD_CHECK_HIP(hipEventCreateWithFlags(&ce.xev[d], hipEventDisableTiming));
     }
-    CFD_CHECK_HIP(hipEventCreateWithFlags(&c->ev_boundary, hipEventDisableTiming));
+    CFD_CHECK_HIP(hipEventCreateWithFlags(&c->ev_boundary, hipEventDisableTiming | hipEventReleaseToDevice));
     CFD_CHECK_HIP(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
     CFD_CHECK_HIP(hipDeviceSynchronize());
     *comm = c.release();
@@ -639,10 +655,9 @@ int cfd_comm_ipc_export(void *comm, const float *phi, const float *phi_tmp, size
         b.buf_n[i] = n;
     }
     CFD_CHECK_HIP(hipIpcGetMemHandle(&b.flags_h, ce.flags));
-    ce.mine[0] = const_cast<float *>(phi);
-    ce.mine[1] = const_cast<float *>(phi_tmp);
-    ce.mine_n = n;
-    ce.attached = false;  // until the import
+    ce.pend[0] = const_cast<float *>(phi);
+    ce.pend[1] = const_cast<float *>(phi_tmp);
+    ce.pend_n = n;
     memcpy(blob, &b, sizeof b);
     return CFD_OK;
 }
@@ -652,42 +667,40 @@ int cfd_comm_ipc_import(void *comm, const void *blobs, int nblobs) {
     CFD_REQUIRE(c && c->ce && blobs && nblobs == c->nranks,
                 "comm_ipc_import: needs a copy-engine comm and one blob per rank (%d)", c ? c->nranks : 0);
     CeState &ce = *c->ce;
-    CFD_REQUIRE(ce.mine[0], "comm_ipc_import: export this rank's buffers first");
-    // every solve of the previous attachment is complete before its mappings go
-    CFD_CHECK_HIP(hipDeviceSynchronize());
+    CFD_REQUIRE(ce.pend[0], "comm_ipc_import: export this rank's buffers first");
     std::vector<CeBlob> in((size_t)nblobs);
     memcpy(in.data(), blobs, sizeof(CeBlob) * (size_t)nblobs);
     for (int r = 0; r < nblobs; ++r)
         CFD_REQUIRE(in[r].magic == kCeMagic && in[r].version == 1 && in[r].rank == r &&
                         in[r].nranks == c->nranks,
                     "comm_ipc_import: blob %d is not rank %d's export of a %d-rank comm", r, r, c->nranks);
-    // buffer mappings of an earlier attachment are dropped (flag blocks stay)
-    std::vector<CeState::Map> keep;
-    for (const CeState::Map &m : ce.maps) {
-        bool flags = false;
-        for (const CeBlob &b : ce.blobs)
-            if (b.rank == m.rank && !memcmp(&b.flags_h, &m.h, sizeof m.h)) flags = true;
-        if (flags)
-            keep.push_back(m);
-        else
-            CFD_CHECK_HIP(hipIpcCloseMemHandle(m.base));
-    }
-    ce.maps.swap(keep);
-    ce.blobs.swap(in);
-    ce.peer_flags.assign((size_t)c->nranks, nullptr);
-    for (int r = 0; r < c->nranks; ++r) {
-        if (r == c->rank) {
-            ce.peer_flags[r] = ce.flags;
-            continue;
+    // every rank's flag block, mapped once (it lives as long as the comm)
+    if (ce.peer_flags.empty()) {
+        ce.peer_flags.assign((size_t)c->nranks, nullptr);
+        for (int r = 0; r < c->nranks; ++r) {
+            if (r == c->rank) {
+                ce.peer_flags[r] = ce.flags;
+                continue;
+            }
+            char *base = nullptr;
+            int rc = ce_map(ce, r, in[r].flags_h, &base);
+            if (rc) return rc;
+            ce.peer_flags[r] = reinterpret_cast<unsigned *>(base);
         }
-        char *base = nullptr;
-        int rc = ce_map(ce, r, ce.blobs[r].flags_h, &base);
-        if (rc) return rc;
-        ce.peer_flags[r] = reinterpret_cast<unsigned *>(base);
+        CFD_CHECK_HIP(hipMemcpy(ce.peers_dev, ce.peer_flags.data(), sizeof(unsigned *) * c->nranks,
+                                hipMemcpyHostToDevice));
     }
-    CFD_CHECK_HIP(hipMemcpy(ce.peers_dev, ce.peer_flags.data(), sizeof(unsigned *) * c->nranks,
-                            hipMemcpyHostToDevice));
+    // a re-attached pair replaces its entry (its peers' buffers may be new)
+    CeState::Attachment at{{ce.pend[0], ce.pend[1]}, ce.pend_n, std::move(in)};
+    int k = 0;
+    while (k < (int)ce.att.size() && !(ce.att[k].mine[0] == at.mine[0] && ce.att[k].mine[1] == at.mine[1])) ++k;
+    if (k == (int)ce.att.size())
+        ce.att.push_back(std::move(at));
+    else
+        ce.att[k] = std::move(at);
+    ce.pend[0] = ce.pend[1] = nullptr;
     // the z-neighbours' buffers are mapped now (others on first use)
+    ce.cur = k;
     for (int r : {c->rank - 1, c->rank + 1}) {
         if (r < 0 || r >= c->nranks) continue;
         for (int bi = 0; bi < 2; ++bi) {
@@ -697,7 +710,6 @@ int cfd_comm_ipc_import(void *comm, const void *blobs, int nblobs) {
             if (rc) return rc;
         }
     }
-    ce.attached = true;
     return CFD_OK;
 }
 

@@ -32,6 +32,29 @@ def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
     return t
 
 
+_SFX = {torch.float32: "_f32", torch.float64: "_f64"}
+
+
+def _fields(name, *ts):
+    """Entry point `name` + _f32 / _f64 for the fields' dtype: float32
+    (memory_efficient=True, v5.py:287) or float64 (False); every field of one
+    call must share it."""
+    dt = ts[0].dtype
+    if dt not in _SFX:
+        raise TypeError(f"{name}: fields must be float32 or float64, got {dt}")
+    for t in ts[1:]:
+        if t is not None and t.dtype != dt:
+            raise TypeError(f"{name}: mixed field dtypes {dt} and {t.dtype}")
+    return name + _SFX[dt]
+
+
+def _dt_arg(dt, field_dtype):
+    """The step's dt as it meets the fields (NEP 50): float32 fields round it
+    to float32 (np.float32 or a Python float dt_base alike); float64 fields
+    take it exactly (the f64 entry points take a double)."""
+    return float(np.float32(dt)) if field_dtype == torch.float32 else float(dt)
+
+
 def _like(phi: torch.Tensor, t, name: str):
     """A companion array of phi (div, scratch, workspace): same shape, dtype,
     device, C-contiguous -- the kernels index it with phi's strides, so a
@@ -61,21 +84,24 @@ def _mask_u8(mask, shape):
     return m.contiguous()
 
 
-def _nu(nu_eff):
+def _nu(nu_eff, dtype=torch.float32):
     """nu_eff as (array_or_None, scalar): an array is passed through, a scalar
-    (LES off: nu + 0 + art_visc, v5.py:388) is broadcast by the kernel."""
+    (LES off: nu + 0 + art_visc, v5.py:388) is broadcast by the kernel, in the
+    fields' precision."""
     if isinstance(nu_eff, torch.Tensor) and nu_eff.dim() > 0:
-        return _f32(nu_eff, "nu_eff").contiguous(), 0.0
-    return None, float(np.float32(nu_eff))
+        if nu_eff.dtype != dtype:
+            raise TypeError(f"nu_eff must be {dtype}, got {nu_eff.dtype}")
+        return nu_eff.contiguous(), 0.0
+    return None, float(np.float32(nu_eff)) if dtype == torch.float32 else float(nu_eff)
 
 
 def compute_supg_stabilization_fast(u, v, dx, dy, dt, nu_eff):
     """v5.py:149-162."""
     ny, nx = _shape2d(u)
     tau = torch.empty_like(u)
-    nu_a, nu_s = _nu(nu_eff)
-    call("cfd_supg_tau2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(nu_a), nu_s, ptr(tau), ny, nx,
-         float(dx), float(dy), float(np.float32(dt)), stream_handle())
+    nu_a, nu_s = _nu(nu_eff, u.dtype)
+    call(_fields("cfd_supg_tau2d", u, v), ptr(u), ptr(v), ptr(nu_a), nu_s, ptr(tau), ny, nx, float(dx), float(dy),
+         _dt_arg(dt, u.dtype), stream_handle())
     return tau
 
 
@@ -83,8 +109,8 @@ def compute_convection_supg_fast(u, v, phi, dx, dy, tau_supg):
     """v5.py:127-147 (derivative factors 1/(4dx), 1/(4dx^2): the reference's quirk)."""
     ny, nx = _shape2d(phi)
     conv = torch.empty_like(phi)
-    call("cfd_convection_supg2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(_f32(phi, "phi")),
-         ptr(_f32(tau_supg, "tau_supg")), ptr(conv), ny, nx, float(dx), float(dy), stream_handle())
+    call(_fields("cfd_convection_supg2d", phi, u, v, tau_supg), ptr(u), ptr(v), ptr(phi), ptr(tau_supg), ptr(conv),
+         ny, nx, float(dx), float(dy), stream_handle())
     return conv
 
 
@@ -92,8 +118,8 @@ def compute_convection_fast(u, v, phi, dx, dy):
     """First-order upwind convection, v5.py:112-125."""
     ny, nx = _shape2d(phi)
     conv = torch.empty_like(phi)
-    call("cfd_convection_upwind2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(_f32(phi, "phi")),
-         ptr(conv), ny, nx, float(dx), float(dy), stream_handle())
+    call(_fields("cfd_convection_upwind2d", phi, u, v), ptr(u), ptr(v), ptr(phi), ptr(conv), ny, nx, float(dx),
+         float(dy), stream_handle())
     return conv
 
 
@@ -101,19 +127,20 @@ def compute_laplacian_fast(phi, dx, dy, nu_eff):
     """v5.py:164-176."""
     ny, nx = _shape2d(phi)
     lap = torch.empty_like(phi)
-    nu_a, nu_s = _nu(nu_eff)
-    call("cfd_laplacian2d_f32", ptr(_f32(phi, "phi")), ptr(nu_a), nu_s, ptr(lap), ny, nx, float(dx),
-         float(dy), stream_handle())
+    nu_a, nu_s = _nu(nu_eff, phi.dtype)
+    call(_fields("cfd_laplacian2d", phi), ptr(phi), ptr(nu_a), nu_s, ptr(lap), ny, nx, float(dx), float(dy),
+         stream_handle())
     return lap
 
 
 def compute_divergence_fast(u, v, dx, dy, absmax=None):
-    """v5.py:178-187.  ``absmax``: optional zeroed device float32 scalar that
-    receives max|div| (the v5.py:410 diagnostic) without a host sync."""
+    """v5.py:178-187.  ``absmax``: optional zeroed device scalar of the
+    fields' dtype that receives max|div| (the v5.py:410 diagnostic) without a
+    host sync."""
     ny, nx = _shape2d(u)
     div = torch.empty_like(u)
-    call("cfd_divergence2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(div), ny, nx, float(dx),
-         float(dy), ptr(absmax), stream_handle())
+    call(_fields("cfd_divergence2d", u, v, absmax), ptr(u), ptr(v), ptr(div), ny, nx, float(dx), float(dy),
+         ptr(absmax), stream_handle())
     return div
 
 
@@ -121,8 +148,7 @@ def compute_gradient_fast(phi, dx, dy):
     """v5.py:189-200."""
     ny, nx = _shape2d(phi)
     gx, gy = torch.empty_like(phi), torch.empty_like(phi)
-    call("cfd_gradient2d_f32", ptr(_f32(phi, "phi")), ptr(gx), ptr(gy), ny, nx, float(dx), float(dy),
-         stream_handle())
+    call(_fields("cfd_gradient2d", phi), ptr(phi), ptr(gx), ptr(gy), ny, nx, float(dx), float(dy), stream_handle())
     return gx, gy
 
 
@@ -130,17 +156,22 @@ def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iteratio
                                      workspace=None, iters_done=None, phi_tmp=None):
     """v5.py:202-226: red-black GS, in place on ``phi``; returns ``phi``.
     ``iters_done`` (optional int32 device scalar) receives the iteration count.
-    ``phi_tmp`` (same-size scratch field, allocated if omitted) lets every
-    iteration run as one fused out-of-place pass; the result still lands in
-    ``phi``, bit-identical to the in-place colour passes."""
+    float32: ``phi_tmp`` (same-size scratch field, allocated if omitted) lets
+    every iteration run as one fused out-of-place pass; the result still lands
+    in ``phi``, bit-identical to the in-place colour passes.  float64
+    (memory_efficient=False): in-place colour passes (phi_tmp unused)."""
     ny, nx = _shape2d(phi)
     m = _mask_u8(mask, phi.shape)
     ws = workspace
     need = int(lib().cfd_rbgs_workspace_bytes(int(iterations)))
     if ws is None or ws.numel() * ws.element_size() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
-    tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
     _like(phi, div_u_star, "div_u_star")
+    if phi.dtype == torch.float64:
+        call("cfd_rbgs2d_f64", ptr(phi), ptr(div_u_star), ptr(m), ny, nx, float(dx), float(dy),
+             float(np.float32(dt)), int(iterations), float(tolerance), ptr(ws), ptr(iters_done), stream_handle())
+        return phi
+    tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
     call("cfd_rbgs2d_f32", ptr(_f32(phi, "phi")), ptr(_f32(div_u_star, "div_u_star")), ptr(m), ny, nx,
          float(dx), float(dy), float(np.float32(dt)), int(iterations), float(tolerance), ptr(_f32(tmp, "phi_tmp")),
          ptr(ws), ptr(iters_done), stream_handle())
@@ -222,8 +253,8 @@ def apply_ibm_fast(u, v, ibm_mask, force_strength):
     """v5.py:228-237, in place; ``ibm_mask`` is the float64 mask. Returns (u, v)."""
     if ibm_mask.dtype != torch.float64:
         raise TypeError("ibm_mask is float64 in the reference (v5.py:281-283)")
-    call("cfd_apply_ibm2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(ibm_mask), int(u.numel()),
-         float(force_strength), stream_handle())
+    call(_fields("cfd_apply_ibm2d", u, v), ptr(u), ptr(v), ptr(ibm_mask), int(u.numel()), float(force_strength),
+         stream_handle())
     return u, v
 
 
@@ -234,8 +265,8 @@ def clean_divergence_fast(u, v, dx, dy, iterations=2, workspace=None):
     ws = workspace
     if ws is None or ws.numel() * ws.element_size() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=u.device)
-    call("cfd_clean_divergence2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ny, nx, float(dx), float(dy),
-         int(iterations), ptr(ws), stream_handle())
+    call(_fields("cfd_clean_divergence2d", u, v), ptr(u), ptr(v), ny, nx, float(dx), float(dy), int(iterations),
+         ptr(ws), stream_handle())
     return u, v
 
 
@@ -246,10 +277,10 @@ def predictor_fused(u, v, dx, dy, dt, nu_eff, use_supg=True, u_star=None, v_star
     vs = torch.empty_like(v) if v_star is None else v_star
     if tau is None and use_supg:
         tau = torch.empty_like(u)
-    nu_a, nu_s = _nu(nu_eff)
-    call("cfd_predictor2d_f32", ptr(_f32(u, "u")), ptr(_f32(v, "v")), ptr(nu_a), nu_s, ptr(us), ptr(vs),
-         ptr(tau) if use_supg else None, ny, nx, float(dx), float(dy), float(np.float32(dt)),
-         int(bool(use_supg)), stream_handle())
+    nu_a, nu_s = _nu(nu_eff, u.dtype)
+    call(_fields("cfd_predictor2d", u, v, us, vs, tau), ptr(u), ptr(v), ptr(nu_a), nu_s, ptr(us), ptr(vs),
+         ptr(tau) if use_supg else None, ny, nx, float(dx), float(dy), _dt_arg(dt, u.dtype), int(bool(use_supg)),
+         stream_handle())
     return us, vs, tau
 
 
@@ -258,6 +289,6 @@ def project_velocity(phi, u_star, v_star, dx, dy, dt, u=None, v=None, gradmax=No
     ny, nx = _shape2d(phi)
     u = torch.empty_like(u_star) if u is None else u
     v = torch.empty_like(v_star) if v is None else v
-    call("cfd_project2d_f32", ptr(phi), ptr(u_star), ptr(v_star), ptr(u), ptr(v), ny, nx, float(dx),
-         float(dy), float(np.float32(dt)), ptr(gradmax), stream_handle())
+    call(_fields("cfd_project2d", phi, u_star, v_star, u, v, gradmax), ptr(phi), ptr(u_star), ptr(v_star), ptr(u),
+         ptr(v), ny, nx, float(dx), float(dy), _dt_arg(dt, phi.dtype), ptr(gradmax), stream_handle())
     return u, v

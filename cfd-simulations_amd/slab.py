@@ -184,15 +184,13 @@ class CopyEngineComm:
         call("cfd_comm_init_ipc", int(nranks), int(rank), ctypes.byref(handle))
         self.handle = handle
         self.rank, self.nranks, self.group = rank, nranks, group
-        self._attached = None
 
     def attach(self, phi: torch.Tensor, phi_tmp: torch.Tensor):
         """Export this rank's two field buffers, gather every rank's blob (a
-        collective over the process group), map the neighbours' buffers."""
+        collective over the process group), map the neighbours' buffers.  A
+        comm holds every pair attached so far (a re-attached pair replaces its
+        entry); a solve uses the pair its phi / phi_tmp belong to."""
         import ctypes
-        key = (phi.data_ptr(), phi_tmp.data_ptr(), phi.numel())
-        if self._attached == key:
-            return
         if phi.shape != phi_tmp.shape or phi.dtype != torch.float32 or not phi.is_cuda:
             raise ValueError("attach: two float32 device arrays of one shape")
         nb = int(lib().cfd_comm_ipc_blob_bytes())
@@ -217,7 +215,6 @@ class CopyEngineComm:
         except Exception as e:  # noqa: BLE001
             err = e
         self._agree(err, "import")
-        self._attached = key
 
     def _agree(self, err, what):
         """Collective: raise on every rank if `what` failed on any (so that no

@@ -3,7 +3,9 @@
 ``OptimizedTurbulentConfig`` and ``OptimizedTurbulentSolver`` keep the field
 names, method names and return values of
 ``python/flow_over_cylinder (Fischer)/v5.py:41-441``.  The fields (``u``, ``v``,
-``phi``, ``u_star``, ...) are torch tensors on the HIP device.  Every
+``phi``, ``u_star``, ...) are torch tensors on the HIP device, float32
+(``memory_efficient=True``, the reference default) or float64 (False,
+v5.py:287).  Every
 per-step array pass runs in libcfdsim's gfx950 kernels, and the step needs no
 host synchronisation (except adaptive dt after step 1000, which, like the
 reference, reads max|V|).
@@ -97,13 +99,31 @@ def host_masks(cfg, X, Y):
     return dist, cyl, ibm
 
 
-def host_potential_flow(cfg, X, Y, dist, ibm_mask):
+def host_potential_flow(cfg, X, Y, dist, ibm_mask, dtype=np.float32):
     """initialize_potential_flow, v5.py:299-314, vectorised (same formulas,
-    float64 then cast to float32 on assignment)."""
+    float64 then cast to the fields' dtype on assignment: float32, or float64
+    when memory_efficient=False)."""
     x_c, y_c = cfg.cylinder_center
     r, m = dist, ibm_mask
-    u = np.zeros((cfg.ny, cfg.nx), np.float32)
-    v = np.zeros((cfg.ny, cfg.nx), np.float32)
+    u = np.zeros((cfg.ny, cfg.nx), dtype)
+    v = np.zeros((cfg.ny, cfg.nx), dtype)
+    if dtype == np.float64:
+        # float64 keeps every bit of the per-cell scalar arithmetic: NumPy
+        # float64 scalar `**` is libm pow and scalar sin / cos take the scalar
+        # loops, which the vectorised array forms below do not reproduce to
+        # the last bit (float32 rounding hides that), so restate the loop
+        for i in range(cfg.ny):
+            for j in range(cfg.nx):
+                rij, mv = r[i, j], m[i, j]
+                if rij > cfg.R_cylinder + 4 * cfg.dx:
+                    theta = np.arctan2(Y[i, j] - y_c, X[i, j] - x_c)
+                    factor = (cfg.R_cylinder / rij) ** 2
+                    u[i, j] = cfg.V_inf * (1 - factor * np.cos(2 * theta)) * (1 - mv)
+                    v[i, j] = -cfg.V_inf * factor * np.sin(2 * theta) * (1 - mv)
+                else:
+                    blend = min(1.0, ((rij - cfg.R_cylinder) / (4 * cfg.dx)) ** 2)
+                    u[i, j] = cfg.V_inf * blend * (1 - mv)
+        return u, v
     far = r > cfg.R_cylinder + 4 * cfg.dx
     with np.errstate(divide="ignore", invalid="ignore"):
         theta = np.arctan2(Y - y_c, X - x_c)
@@ -124,11 +144,11 @@ class OptimizedTurbulentSolver:
     def __init__(self, config: OptimizedTurbulentConfig):
         if config.use_les:
             raise NotImplementedError("use_les=True is out of scope (LES is off in v3-v5, v5.py:60)")
-        if not config.memory_efficient:
-            raise NotImplementedError("time_step() runs float32 fields (memory_efficient=True, the "
-                                      "reference default); float64 Poisson solves are available "
-                                      "through kernels.solve_pressure_jacobi")
         self.config = config
+        # v5.py:287: float32 fields when memory_efficient, else float64
+        self.dtype = torch.float32 if config.memory_efficient else torch.float64
+        self._sfx = "_f32" if config.memory_efficient else "_f64"
+        self._np = np.float32 if config.memory_efficient else np.float64
         self.device = torch.device(config.device)
         if self.device.type != "cuda":
             raise TypeError("OptimizedTurbulentSolver runs on the HIP device only")
@@ -157,7 +177,7 @@ class OptimizedTurbulentSolver:
     def initialize_fields(self):  # v5.py:285-297
         cfg = self.config
         shape = (cfg.ny, cfg.nx)
-        z = lambda: torch.zeros(shape, dtype=torch.float32, device=self.device)  # noqa: E731
+        z = lambda: torch.zeros(shape, dtype=self.dtype, device=self.device)  # noqa: E731
         self.u, self.v, self.p, self.nu_t, self.tau_supg = z(), z(), z(), z(), z()
         self.u_star, self.v_star, self.div_u_star, self.phi = z(), z(), z(), z()
         self._phi_tmp = z()
@@ -167,11 +187,11 @@ class OptimizedTurbulentSolver:
         self._gs_done = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._clean_ws = torch.empty(int(lib().cfd_clean_divergence_workspace_bytes(cfg.ny, cfg.nx)),
                                      dtype=torch.uint8, device=self.device)
-        self._scal = torch.zeros(8, dtype=torch.float32, device=self.device)  # diagnostics
+        self._scal = torch.zeros(8, dtype=self.dtype, device=self.device)  # diagnostics
         self.initialize_potential_flow()
 
     def initialize_potential_flow(self):  # v5.py:299-314 (host, one-time)
-        u, v = host_potential_flow(self.config, self.X, self.Y, self.dist, self.ibm_mask_host)
+        u, v = host_potential_flow(self.config, self.X, self.Y, self.dist, self.ibm_mask_host, self._np)
         self.u.copy_(torch.from_numpy(u))
         self.v.copy_(torch.from_numpy(v))
 
@@ -184,11 +204,11 @@ class OptimizedTurbulentSolver:
             return np.float32(0.00002)
         out = self._scal[0:1]
         out.zero_()
-        call("cfd_absmax2_f32", ptr(self.u), ptr(self.v), self.u.numel(), ptr(out), stream_handle())
-        vmax = np.float32(out.item())  # the one host read of the step (as in the reference)
+        call("cfd_absmax2" + self._sfx, ptr(self.u), ptr(self.v), self.u.numel(), ptr(out), stream_handle())
+        vmax = self._np(out.item())  # the one host read of the step (as in the reference)
         vel_max = max(vmax, 1e-10)
         dt_cfl = cfg.cfl_target * min(cfg.dx, cfg.dy) / vel_max
-        nu_total = cfg.nu + np.float32(0.0) + cfg.artificial_viscosity  # mean(nu_t) == 0
+        nu_total = cfg.nu + self._np(0.0) + cfg.artificial_viscosity  # np.mean(nu_t) == 0 in the fields' dtype
         dt_visc = 0.4 * min(cfg.dx, cfg.dy) ** 2 / nu_total
         return np.float32(np.clip(min(dt_cfl, dt_visc), cfg.dt_min, cfg.dt_max))
 
@@ -207,7 +227,7 @@ class OptimizedTurbulentSolver:
 
     def apply_boundary_conditions(self, u, v):  # v5.py:349-360
         cfg = self.config
-        call("cfd_apply_bc2d_f32", ptr(u), ptr(v), ptr(self._y_dev), cfg.ny, cfg.nx, float(cfg.y_max),
+        call("cfd_apply_bc2d" + self._sfx, ptr(u), ptr(v), ptr(self._y_dev), cfg.ny, cfg.nx, float(cfg.y_max),
              float(cfg.V_inf), int(self.step), stream_handle())
 
     def compute_energy(self):  # v5.py:362-363
@@ -216,8 +236,12 @@ class OptimizedTurbulentSolver:
     def compute_vorticity(self):  # v5.py:365-373
         cfg = self.config
         w = torch.empty_like(self.u)
-        call("cfd_vorticity2d_f32", ptr(self.u), ptr(self.v), ptr(self._mask_u8), ptr(w), cfg.ny, cfg.nx,
-             float(cfg.dx), float(cfg.dy), stream_handle())
+        if self.dtype == torch.float64:
+            call("cfd_vorticity2d_f64", ptr(self.u), ptr(self.v), ptr(self._mask_u8), ptr(w), None, cfg.ny,
+                 cfg.nx, float(cfg.dx), float(cfg.dy), stream_handle())
+        else:
+            call("cfd_vorticity2d_f32", ptr(self.u), ptr(self.v), ptr(self._mask_u8), ptr(w), cfg.ny, cfg.nx,
+                 float(cfg.dx), float(cfg.dy), stream_handle())
         return w
 
     @property
@@ -265,8 +289,9 @@ class OptimizedTurbulentSolver:
         dt = self.adaptive_time_step()
         if diag:
             self._scal[1:5].zero_()
-        # predictor (v5.py:378-403): u_old/v_old are read-only here, so u/v are used directly
-        nu_eff = np.float32(cfg.nu + np.float32(0.0)) + cfg.artificial_viscosity
+        # predictor (v5.py:378-403): u_old/v_old are read-only here, so u/v are used directly;
+        # nu_eff = nu + nu_t + art_visc with nu_t == 0 in the fields' dtype (v5.py:388)
+        nu_eff = self._np(self._np(cfg.nu) + self._np(0.0)) + self._np(cfg.artificial_viscosity)
         K.predictor_fused(self.u, self.v, cfg.dx, cfg.dy, dt, nu_eff, cfg.use_supg,
                           u_star=self.u_star, v_star=self.v_star, tau=self.tau_supg)
         if not cfg.use_supg:
@@ -275,29 +300,33 @@ class OptimizedTurbulentSolver:
         force_strength = min(1.0, self.step / cfg.initial_steps)
         if self._has_ibm:
             K.apply_ibm_fast(self.u_star, self.v_star, self.ibm_mask, force_strength)
-        call("cfd_divergence2d_f32", ptr(self.u_star), ptr(self.v_star), ptr(self.div_u_star), cfg.ny,
+        call("cfd_divergence2d" + self._sfx, ptr(self.u_star), ptr(self.v_star), ptr(self.div_u_star), cfg.ny,
              cfg.nx, float(cfg.dx), float(cfg.dy), ptr(self._scal[1:2]) if diag else None, s)
         self.solve_pressure_fast(self.div_u_star)
         K.project_velocity(self.phi, self.u_star, self.v_star, cfg.dx, cfg.dy, dt, u=self.u, v=self.v,
                            gradmax=self._scal[2:3] if diag else None)
         K.clean_divergence_fast(self.u, self.v, cfg.dx, cfg.dy, iterations=2, workspace=self._clean_ws)
         if diag:
-            call("cfd_divergence2d_f32", ptr(self.u), ptr(self.v), ptr(self.div_u_star), cfg.ny, cfg.nx,
+            call("cfd_divergence2d" + self._sfx, ptr(self.u), ptr(self.v), ptr(self.div_u_star), cfg.ny, cfg.nx,
                  float(cfg.dx), float(cfg.dy), ptr(self._scal[3:4]), s)
             # the reference recomputes div for logging only; keep div_u_star as the pre-pressure one
-            call("cfd_divergence2d_f32", ptr(self.u_star), ptr(self.v_star), ptr(self.div_u_star),
+            call("cfd_divergence2d" + self._sfx, ptr(self.u_star), ptr(self.v_star), ptr(self.div_u_star),
                  cfg.ny, cfg.nx, float(cfg.dx), float(cfg.dy), None, s)
         self.apply_boundary_conditions(self.u, self.v)
         if self._has_ibm:
             K.apply_ibm_fast(self.u, self.v, self.ibm_mask, force_strength)
-        if diag:
+        if diag and self.dtype == torch.float64:
+            call("cfd_vorticity2d_f64", ptr(self.u), ptr(self.v), ptr(self._mask_u8), None, ptr(self._scal[4:5]),
+                 cfg.ny, cfg.nx, float(cfg.dx), float(cfg.dy), s)
+        elif diag:
             call("cfd_vorticity_absmax2d_f32", ptr(self.u), ptr(self.v), ptr(self._mask_u8), cfg.ny,
                  cfg.nx, float(cfg.dx), float(cfg.dy), ptr(self._scal[4:5]), s)
-        call("cfd_energy_mean2d_f32", ptr(self.u), ptr(self.v), self.u.numel(), ptr(self._energy_slot()), s)
+        call("cfd_energy_mean2d" + self._sfx, ptr(self.u), ptr(self.v), self.u.numel(), ptr(self._energy_slot()),
+             s)
         self._energy_steps.append(self.step)
         self.times.append(self.step * dt)
-        call("cfd_clip_f32", ptr(self.u), self.u.numel(), -float(cfg.max_velocity), float(cfg.max_velocity), s)
-        call("cfd_clip_f32", ptr(self.v), self.v.numel(), -float(cfg.max_velocity), float(cfg.max_velocity), s)
+        call("cfd_clip" + self._sfx, ptr(self.u), self.u.numel(), -float(cfg.max_velocity), float(cfg.max_velocity), s)
+        call("cfd_clip" + self._sfx, ptr(self.v), self.v.numel(), -float(cfg.max_velocity), float(cfg.max_velocity), s)
         self.step += 1
         return dt
 
@@ -412,20 +441,21 @@ class LidDrivenCavitySolver(OptimizedTurbulentSolver):
         self.v.zero_()
 
     def apply_boundary_conditions(self, u, v):
-        call("cfd_apply_lid_bc2d_f32", ptr(u), ptr(v), self.config.ny, self.config.nx,
-             float(np.float32(self.config.lid_velocity)), stream_handle())
+        call("cfd_apply_lid_bc2d" + self._sfx, ptr(u), ptr(v), self.config.ny, self.config.nx,
+             float(self._np(self.config.lid_velocity)), stream_handle())
 
 
 def monitor_simulation_health(solver: OptimizedTurbulentSolver, step: int) -> bool:
     """v5.py:599-613 as device reductions with one host read."""
     cfg = solver.config
     s = stream_handle()
+    sfx = "_f32" if solver.u.dtype == torch.float32 else "_f64"
     cnt = torch.zeros(1, dtype=torch.int32, device=solver.device)
-    red = torch.zeros(2, dtype=torch.float32, device=solver.device)
-    call("cfd_nonfinite_count_f32", ptr(solver.u), ptr(solver.v), solver.u.numel(), ptr(cnt), s)
-    call("cfd_absmax2_f32", ptr(solver.u), ptr(solver.v), solver.u.numel(), ptr(red[0:1]), s)
+    red = torch.zeros(2, dtype=solver.u.dtype, device=solver.device)
+    call("cfd_nonfinite_count" + sfx, ptr(solver.u), ptr(solver.v), solver.u.numel(), ptr(cnt), s)
+    call("cfd_absmax2" + sfx, ptr(solver.u), ptr(solver.v), solver.u.numel(), ptr(red[0:1]), s)
     div = torch.empty_like(solver.u)
-    call("cfd_divergence2d_f32", ptr(solver.u), ptr(solver.v), ptr(div), cfg.ny, cfg.nx, float(cfg.dx),
+    call("cfd_divergence2d" + sfx, ptr(solver.u), ptr(solver.v), ptr(div), cfg.ny, cfg.nx, float(cfg.dx),
          float(cfg.dy), ptr(red[1:2]), s)
     n_bad = int(cnt.item())
     vel_max, div_max = (float(x) for x in red.cpu().numpy())

@@ -203,6 +203,59 @@ int cfd_numpy_powf_f32(const float *x, float y, float *out, size_t n, void *stre
 /* count of non-finite values in a and b (v5.py:601), into a device int. */
 int cfd_nonfinite_count_f32(const float *a, const float *b, size_t n, int *out, void *stream);
 
+/* --------------------------------------------------- float64 fields */
+/* memory_efficient=False (v5.py:287-296): every field float64; the kernels
+ * below are the *_f32 ones above with float64 arrays, the same argument
+ * meaning, and the reference's float64 arithmetic (Python-float constants
+ * unrounded).  dt is a double here: the step's dt (np.float32, or the Python
+ * float dt_base when adaptive_dt=False) meets float64 fields exactly; the
+ * pressure solves keep cfg.dt's float32.  The SUPG tau's
+ * |V| is the correctly rounded sqrt(u*u + v*v) where the reference calls
+ * glibc pow (1 ulp apart on ~1e-3 of cells, fields.hip file comment): a
+ * float64 time_step matches the reference within a relative L-inf of 1e-12
+ * instead of bit for bit.  cfd_jacobi2d_f64 is above. */
+int cfd_supg_tau2d_f64(const double *u, const double *v, const double *nu_eff, double nu_eff_scalar,
+                       double *tau, int ny, int nx, double dx, double dy, double dt, void *stream);
+int cfd_convection_supg2d_f64(const double *u, const double *v, const double *phi, const double *tau,
+                              double *conv, int ny, int nx, double dx, double dy, void *stream);
+int cfd_convection_upwind2d_f64(const double *u, const double *v, const double *phi, double *conv,
+                                int ny, int nx, double dx, double dy, void *stream);
+int cfd_laplacian2d_f64(const double *phi, const double *nu_eff, double nu_eff_scalar, double *lap,
+                        int ny, int nx, double dx, double dy, void *stream);
+int cfd_predictor2d_f64(const double *u, const double *v, const double *nu_eff, double nu_eff_scalar,
+                        double *u_star, double *v_star, double *tau, int ny, int nx, double dx,
+                        double dy, double dt, int use_supg, void *stream);
+int cfd_divergence2d_f64(const double *u, const double *v, double *div, int ny, int nx, double dx,
+                         double dy, double *absmax, void *stream);
+int cfd_gradient2d_f64(const double *phi, double *grad_x, double *grad_y, int ny, int nx, double dx,
+                       double dy, void *stream);
+int cfd_project2d_f64(const double *phi, const double *u_star, const double *v_star, double *u,
+                      double *v, int ny, int nx, double dx, double dy, double dt, double *gradmax,
+                      void *stream);
+/* ws: cfd_clean_divergence_workspace_bytes(ny, nx) (sized for float64) */
+int cfd_clean_divergence2d_f64(double *u, double *v, int ny, int nx, double dx, double dy,
+                               int iterations, void *ws, void *stream);
+int cfd_apply_bc2d_f64(double *u, double *v, const double *y, int ny, int nx, double y_max,
+                       double v_inf, int step, void *stream);
+int cfd_apply_lid_bc2d_f64(double *u, double *v, int ny, int nx, double u_lid, void *stream);
+int cfd_apply_ibm2d_f64(double *u, double *v, const double *ibm_mask, int n, double force_strength,
+                        void *stream);
+int cfd_clip_f64(double *a, size_t n, double lo, double hi, void *stream);
+/* max(|a|, |b|) (b may be NULL) into a zeroed device double */
+int cfd_absmax2_f64(const double *a, const double *b, size_t n, double *out, void *stream);
+int cfd_energy_mean2d_f64(const double *u, const double *v, size_t n, double *out, void *stream);
+/* compute_vorticity into w (may be NULL) and/or nanmax|w| into a zeroed
+ * device double absmax (may be NULL) */
+int cfd_vorticity2d_f64(const double *u, const double *v, const uint8_t *mask, double *w,
+                        double *absmax, int ny, int nx, double dx, double dy, void *stream);
+int cfd_nonfinite_count_f64(const double *a, const double *b, size_t n, int *out, void *stream);
+/* solve_pressure_gauss_seidel_fast (v5.py:202-226) on float64 fields: in-place
+ * colour passes (two launches per iteration), the device-side stop rule, ws
+ * of cfd_rbgs_workspace_bytes(iterations), *iters_done as in cfd_rbgs2d_f32. */
+int cfd_rbgs2d_f64(double *phi, const double *div, const uint8_t *mask, int ny, int nx, double dx,
+                   double dy, float dt, int iterations, double tolerance, void *ws, int *iters_done,
+                   void *stream);
+
 /* ------------------------------------------------- multi-GPU slab Jacobi */
 /* One process per GPU.  The global (nz, ny, nx) grid is split on z; rank r
  * holds nz_local owned planes plus `ghost` (1..4) ghost planes on each side:

@@ -260,3 +260,17 @@ def test_oracle_fixed_dt_steps_bitexact(golden, start):
                      ("tau", s.tau_supg)):
             assert np.array_equal(a, g[f"{f}_{key}"]), (f, k)
     assert np.array_equal(np.array([v for _, v in s.energy_history]), g[f"energy_s{start}"])
+
+
+@pytest.mark.parametrize("branch", ["gs", "jacobi"])
+def test_host_setup_f64_matches_reference(golden, branch):
+    """memory_efficient=False: the float64 initial condition (v5.py:299-314,
+    per-cell scalar arithmetic) equals the reference's bit for bit."""
+    d = golden(f"step_v5_120x36_n3_f64_{branch}.npz")
+    c = _cfg(nx=120, ny=36, pressure_iterations=200, memory_efficient=False)
+    x, y, X, Y = host_grid(c)
+    dist, cyl, ibm = host_masks(c, X, Y)
+    u, v = host_potential_flow(c, X, Y, dist, ibm, np.float64)
+    assert u.dtype == np.float64
+    assert np.array_equal(cyl, d["cylinder_mask"]) and np.array_equal(ibm, d["ibm_mask"])
+    assert np.array_equal(u, d["u0"]) and np.array_equal(v, d["v0"])
