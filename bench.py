@@ -411,8 +411,6 @@ def main():
         spl = levels if blocked else 1
     elif use_slab:  # slab passes: two iterations with 4-deep ghosts, else one
         spl = 2 if blocked and plan.ghost == 4 else 1
-    elif ARGS.tb_rows in (5, 13):  # the tb2 kernel: one iteration per pass
-        spl = 1
     else:  # single GPU: half-sweeps per pass (--tb, or the library's auto: 4 = two iterations)
         spl = int(lib().cfd_get_rbgs3d_levels()) / 2 if blocked else 1
     launch_ms = sweep_ms * spl
@@ -442,8 +440,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": (("jacobi3d_tb2<MODE_RBGS>" if ARGS.tb_rows in (5, 13) else
-                                 f"jacobi3d_tbr<{int(2 * spl)}, MODE_RBGS>") if blocked else "rbgs3d_color x2") if gs
+                     "kernel": (f"jacobi3d_tbr<{int(2 * spl)}, MODE_RBGS>" if blocked else "rbgs3d_color x2") if gs
                      else (blocked_kernel_name(levels, ARGS.tb_rows) if blocked
                            else "jacobi3d_march") if len(shape) == 3
                      else (f"jacobi2d_tbk<{levels}>" if blocked else "jacobi2d_march"),
@@ -503,11 +500,7 @@ def make_comm(S, rank, world):
 
 def blocked_kernel_name(levels, rows):
     """The kernel cfd_jacobi3d_f32 dispatches for (levels, rows) -- mirrors
-    jacobi3d_blocked_pass in poisson3d.hip."""
-    if levels == 2:
-        return "jacobi3d_tb2" if rows in (5, 13) else "jacobi3d_tbk<2>"
-    if (levels, rows) in ((3, 11), (4, 9)):
-        return f"jacobi3d_tbk<{levels}>"
+    jacobi3d_blocked_pass in poisson3d.hip (the tall-tile kernel for 2..4)."""
     if rows == 0:
         return f"jacobi3d_tbr<{levels}> (tile shape by the launcher's cost model)"
     return f"jacobi3d_tbr<{levels}> ({rows}-row tiles)"
@@ -611,27 +604,10 @@ def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):
                             "GBps": round(cells * bpc / per / 1e6, 1)})
                 print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
-    for rows, zchunk, pf in [(r, z, p) for p in (1, 2) for r in (5, 13) for z in (32, 64, 128)]:
-            call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
-            call("cfd_set_jacobi3d_prefetch", pf)
-            phi.zero_()
-            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 4, phi_tmp=tmp, rhs_ws=rhs)
-            torch.cuda.synchronize()
-            call("cfd_timing_enable", 1)
-            K.solve_pressure_jacobi3d(phi, div, h, dt, None, 20, phi_tmp=tmp, rhs_ws=rhs)
-            ms = ctypes.c_double()
-            n = ctypes.c_longlong()
-            call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(n), 1)
-            call("cfd_timing_enable", 0)
-            per = ms.value / n.value
-            res.append({"tb_rows": rows, "zchunk": zchunk, "prefetch": pf, "ms_per_sweep": round(per, 4),
-                        "GBps_pass": round(cells * 12 / (2 * per) / 1e6, 1),
-                        "Gcell_per_s": round(cells / per / 1e6, 1)})
-            print(json.dumps({"tile": res[-1]}), file=sys.stderr, flush=True)
     # the tall-tile kernels (the default family): levels per pass x output rows
     # per tile (the shape) x z-chunk (0: the launcher's cost model)
     call("cfd_set_jacobi3d_prefetch", 0)
-    for lv, rows in [(3, 16), (3, 18), (3, 17), (4, 16), (4, 14), (4, 15)]:
+    for lv, rows in [(2, 16), (2, 18), (2, 20), (2, 28), (3, 16), (3, 18), (3, 17), (4, 16), (4, 14), (4, 15)]:
         for zchunk in (0, 64, 128, 256, 512):
             call("cfd_set_jacobi3d_blocking", lv, rows, zchunk)
             phi.zero_()

@@ -36,7 +36,6 @@ int jacobi3d_sweep(const float *in, float *out, const float *div, const uint8_t 
                    int ny, int nx, int zb, int ze, float h2, float dt, bool pre, float *resid,
                    hipStream_t s);
 int launch_rhs_f32(const float *div, float *rhs, size_t n, float h2, float dt, hipStream_t s);
-int jacobi3d_tb_rows();      // configured rows per temporally blocked tile
 int jacobi3d_tb_zchunk();
 bool jacobi3d_tb_enabled();
 int jacobi3d_tb_levels();    // Jacobi sweeps per blocked pass (2..4)
@@ -45,15 +44,7 @@ int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, 
                           int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt,
                           bool pre, hipStream_t s);
 int jacobi3d_tb_prefetch();  // planes of prefetch in the blocked kernel (1 or 2)
-// jacobi3d_tb.hip
-int jacobi3d_tb2_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
-                      int ze, int fixed_lo, int fixed_hi, float h2, float dt, int W, int zchunk,
-                      bool pre, hipStream_t s);
-// jacobi3d_tbk.hip: K = 2..4 sweeps per pass
-int jacobi3d_tbk_pass(int K, const float *in, float *out, const float *div, int nz, int ny, int nx,
-                      int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt, int zchunk,
-                      bool pre, hipStream_t s);
-// jacobi3d_tbr.hip: K = 3, 4 with several rows per wave (tall tiles)
+// jacobi3d_tbr.hip: K = 2..4 sweeps per pass with several rows per wave (tall tiles)
 // CUs the tall-tile launches may plan for on this host thread: all of them,
 // minus those a slab solve reserved for its exchange stream (set_cu_reserve).
 int tbr_cus();
@@ -120,9 +111,4 @@ int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int
 int rbgs3d_half_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                      int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int h0,
                      int levels, RbgsWs *ws, hipStream_t s, int lag);
-// one fused iteration (both colours) of planes [zb, ze) of `out` from `in`;
-// max|change| into ws->maxc[it], stop counter ws->flags[1]
-int rbgs3d_tb_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
-                   int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
-                   RbgsWs *ws, hipStream_t s);
 }  // namespace cfd

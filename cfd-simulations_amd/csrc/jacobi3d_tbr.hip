@@ -1,10 +1,10 @@
 // jacobi3d_tbr.hip -- K Jacobi sweeps per HBM pass with TALL tiles: several
 // rows per wave and single-buffered LDS level tiles (two barriers per step).
 //
-// jacobi3d_tbk (one row per wave, double-buffered tiles) is limited to 16
-// waves = W + 2K - 1, so a tile of W output rows re-reads 2K halo rows of its
-// neighbours (W = 11 rows for K = 3: 17 rows of phi and 15 of rhs are fetched
-// per 11 output rows, mostly from HBM).  Here a row wave owns RPW rows (its
+// The round-1 design (one row per wave, double-buffered tiles, since
+// removed) was limited to 16 waves = W + 2K - 1, so a tile of W output rows
+// re-read 2K halo rows of its neighbours (W = 11 rows for K = 3: 17 rows of
+// phi and 15 of rhs fetched per 11 output rows).  Here a row wave owns RPW rows (its
 // register queues are RPW times as large; 8-12 waves per workgroup leave
 // 168-256 VGPRs per wave), and the level tiles are single-buffered so that
 // the taller tile still fits in LDS:
@@ -19,7 +19,7 @@
 // Shapes (K, row waves, rows per wave) -> output rows W = NWR*RPW + 2 - 2K:
 // (3, 11, 2) W = 18; (4, 7, 3) W = 15; (3, 7, 3) W = 17.  Everything else --
 // the halo wave, the z-march bounds, Dirichlet copies, erosion of garbage --
-// is as in jacobi3d_tbk.hip, and the result is bit-identical to K single
+// is as in that design, and the result is bit-identical to K single
 // sweeps (tests/test_gpu_parity.py).
 #include <type_traits>
 

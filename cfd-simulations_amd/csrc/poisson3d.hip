@@ -95,9 +95,7 @@ int launch_zero_faces3d(float *a, float *b, int nz, int ny, int nx, hipStream_t 
 // K=3 1010-1030, K=4 1000 Gcell/s)
 constexpr int kDefaultLevels = 3;
 
-// defaults from the r01 tile sweep (1024^3): 13 output rows per tile, prefetch
-// 1 plane ahead; planes per tile chosen by jacobi3d_tb2_pass (0 = auto)
-int jacobi3d_tb_rows() { return tuning().tb_rows ? tuning().tb_rows : 13; }
+// planes per tile of the blocked kernels (0 = the launcher's cost model)
 int jacobi3d_tb_zchunk() { return tuning().tb_zchunk; }
 bool jacobi3d_tb_enabled() { return tuning().tb_steps != 1; }
 int jacobi3d_tb_levels() { return tuning().tb_steps >= 2 ? tuning().tb_steps : kDefaultLevels; }
@@ -482,8 +480,6 @@ int rbgs3d_half_per_pass() { return tuning().tb_steps >= 2 ? tuning().tb_steps :
 int rbgs3d_fused_pass(const float *in, float *out, const float *div, int nz, int ny, int nx, int zb,
                       int ze, int fixed_lo, int fixed_hi, int zoff, const RbgsConsts &k, int it,
                       int iters, RbgsWs *ws, hipStream_t s, int lag) {
-    if (iters == 1 && !lag && (tuning().tb_rows == 5 || tuning().tb_rows == 13))
-        return rbgs3d_tb_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, it, ws, s);
     return rbgs3d_half_pass(in, out, div, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, zoff, k, 2 * it,
                             2 * iters, ws, s, lag);
 }
@@ -502,11 +498,10 @@ int rbgs3d_half_pass(const float *in, float *out, const float *div, int nz, int 
                            ws, 0, 0, shape_ok ? r : 0, s, lag);
 }
 
-// One pass of k Jacobi sweeps over planes [zb, ze) (k = 1..4), with the tile
-// shape cfd_set_jacobi3d_blocking selected: rows 5 / 13 -> jacobi3d_tb2 for
-// k = 2; rows 11 (k = 3) / 9 (k = 4) -> jacobi3d_tbk; otherwise the tall-tile
-// jacobi3d_tbr for k >= 3 (16, 17 or 18 rows for k = 3, 15 or 16 for k = 4;
-// 0 = chosen by its cost model) and jacobi3d_tbk for k = 2.
+// One pass of k Jacobi sweeps over planes [zb, ze) (k = 1..4): the single
+// sweep for k = 1, else the tall-tile jacobi3d_tbr with the tile shape
+// cfd_set_jacobi3d_blocking selected (16, 18, 20 or 28 rows for k = 2; 16, 17
+// or 18 for k = 3; 14, 15 or 16 for k = 4; 0 = chosen by its cost model).
 int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, int nz, int ny,
                           int nx, int zb, int ze, int fixed_lo, int fixed_hi, float h2, float dt,
                           bool pre, hipStream_t s) {
@@ -514,16 +509,6 @@ int jacobi3d_blocked_pass(int k, const float *in, float *out, const float *src, 
     // remainder pass picks its own tile
     const int rows = k == jacobi3d_tb_levels() ? tuning().tb_rows : 0, zc = tuning().tb_zchunk;
     if (k == 1) return jacobi3d_sweep(in, out, src, nullptr, nz, ny, nx, zb, ze, h2, dt, pre, nullptr, s);
-    if (k == 2) {
-        if (rows == 5 || rows == 13)
-            return jacobi3d_tb2_pass(in, out, src, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, h2, dt, rows,
-                                     zc, pre, s);
-        return jacobi3d_tbk_pass(2, in, out, src, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, h2, dt, zc,
-                                 pre, s);
-    }
-    if ((k == 3 && rows == 11) || (k == 4 && rows == 9))
-        return jacobi3d_tbk_pass(k, in, out, src, nz, ny, nx, zb, ze, fixed_lo, fixed_hi, h2, dt, zc,
-                                 pre, s);
     return jacobi3d_tbr_pass(k, rows, in, out, src, nz, ny, nx, zb, ze,
                              fixed_lo, fixed_hi, h2, dt, zc, pre, s);
 }
@@ -593,10 +578,9 @@ int cfd_set_jacobi3d_prefetch(int planes) {
 
 int cfd_set_jacobi3d_blocking(int steps, int rows, int zchunk) {
     CFD_REQUIRE(steps >= 0 && steps <= 4, "blocking steps must be 0 (auto), 1 (off) or 2..4");
-    CFD_REQUIRE(rows == 0 || rows == 5 || rows == 13 || rows == 9 || rows == 11 || rows == 14 || rows == 15 ||
-                    rows == 16 || rows == 17 || rows == 18 || rows == 20 || rows == 28,
-                "blocking rows must be 0 (auto), 5, 13, 16, 18, 20, 28 (2 levels), 11, 16, 17, 18 (3), "
-                "9, 14, 15, 16 (4)");
+    CFD_REQUIRE(rows == 0 || rows == 14 || rows == 15 || rows == 16 || rows == 17 || rows == 18 || rows == 20 ||
+                    rows == 28,
+                "blocking rows must be 0 (auto), 16, 18, 20, 28 (2 levels), 16, 17, 18 (3), 14, 15, 16 (4)");
     CFD_REQUIRE(zchunk >= 0, "zchunk must be >= 0");
     tuning().tb_steps = steps;
     tuning().tb_rows = rows;
@@ -731,21 +715,13 @@ int cfd_rbgs3d_f32(float *phi, const float *div, const uint8_t *mask, int nz, in
         // passes of P half-sweeps (colour levels), the last one shorter
         const int P = rbgs3d_half_per_pass(), H = 2 * iterations;
         float *a = phi, *b = phi_tmp;
-        if (iterations > 0 && tuning().tb_rows != 5 && tuning().tb_rows != 13) {
-            for (int h = 0; h < H; h += P) {
-                const int m = H - h >= P ? P : H - h;
-                if ((rc = rbgs3d_half_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, h, m, w, s, 0)))
-                    return rc;
-                float *t = a; a = b; b = t;
-            }
-        } else {
-            for (int it = 0; it < iterations; ++it) {  // the 2-level tb2 kernel (rows 5, 13)
-                if ((rc = rbgs3d_fused_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, it, 1, w, s)))
-                    return rc;
-                float *t = a; a = b; b = t;
-            }
+        for (int h = 0; h < H; h += P) {
+            const int m = H - h >= P ? P : H - h;
+            if ((rc = rbgs3d_half_pass(a, b, div, nz, ny, nx, 1, nz - 1, 1, 1, 0, k, h, m, w, s, 0)))
+                return rc;
+            float *t = a; a = b; b = t;
         }
-        const int hpp = tuning().tb_rows == 5 || tuning().tb_rows == 13 ? 2 : P;
+        const int hpp = P;
         timing_end(tk, s, iterations);
         if ((rc = launch_rbgs_count(w, iters_done, s))) return rc;
         // a stop inside a pass: re-run its half-sweeps up to the stop, one

@@ -45,7 +45,7 @@ for s in "$@"; do
     testslocal) step pytest_local 900 python -m pytest tests -m gpu -q -x -k "local_group" ;;
     testsgs) step pytest_gs 900 python -m pytest tests -m gpu -q -k "rbgs or slab" ;;
     benchgs) step benchgs 600 python bench.py --workload rbgs3d_1024 ;;
-    gssweep) step gssweep 900 bash -c 'for cfg in ${GSSWEEP:-0:0 2:13 4:0 4:16 2:18 2:20 2:28}; do set -- ${cfg/:/ }; echo "tb=$1 rows=$2"; python bench.py --workload rbgs3d_1024 --no-cpu-baseline --steps 3 --tb $1 --tb-rows $2 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*\|iterations_done_last_step\": [0-9]*" | tr "\n" " "; echo; done' ;;
+    gssweep) step gssweep 900 bash -c 'for cfg in ${GSSWEEP:-0:0 2:16 4:0 4:16 2:18 2:20 2:28}; do set -- ${cfg/:/ }; echo "tb=$1 rows=$2"; python bench.py --workload rbgs3d_1024 --no-cpu-baseline --steps 3 --tb $1 --tb-rows $2 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*\|iterations_done_last_step\": [0-9]*" | tr "\n" " "; echo; done' ;;
     benchgs_inplace) step benchgs_inplace 600 python bench.py --workload rbgs3d_1024 --tb 1 --no-cpu-baseline --steps 3 ;;
     slab1gs) step slab1gs 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29542 bench.py --gpus 1 --force-slab --workload rbgs3d_1024 --steps 3 --warmup 1 ;;
     prof2d) step prof2d 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof2d -o run --output-format csv -- python3 bench.py --workload jacobi2d_8192_f64 --steps 3 --warmup 1 --no-cpu-baseline ;;

@@ -149,12 +149,13 @@ def test_jacobi3d_bitexact(shape, masked, variant, waves, zchunk):
 
 
 @pytest.mark.parametrize("prefetch", [1, 2])
-@pytest.mark.parametrize("rows,zchunk", [(5, 0), (13, 0), (5, 3), (13, 1), (5, 1), (13, 5)])
+@pytest.mark.parametrize("rows,zchunk", [(16, 0), (18, 0), (20, 3), (28, 1), (16, 1), (20, 5)])
 @pytest.mark.parametrize("shape,iters", [((10, 12, 16), 6), ((9, 11, 20), 7), ((34, 40, 260), 4),
                                          ((6, 7, 520), 5), ((20, 19, 8), 2), ((5, 33, 768), 9),
                                          ((3, 3, 4), 4)])
 def test_jacobi3d_temporal_blocking_bitexact(shape, iters, rows, zchunk, prefetch):
-    """Two sweeps fused per pass (jacobi3d_tb2) == two single sweeps, bitwise."""
+    """Two sweeps fused per pass (jacobi3d_tbr<2>, every 2-level tile shape)
+    == two single sweeps, bitwise."""
     call("cfd_set_jacobi3d_blocking", 2, rows, zchunk)
     call("cfd_set_jacobi3d_prefetch", prefetch)
     rng = np.random.default_rng(sum(shape) + iters)
@@ -166,15 +167,15 @@ def test_jacobi3d_temporal_blocking_bitexact(shape, iters, rows, zchunk, prefetc
     assert np.array_equal(host(phi), ref)
 
 
-@pytest.mark.parametrize("levels,rows", [(3, 11), (3, 16), (3, 17), (3, 18), (3, 0), (4, 9), (4, 15), (4, 16),
+@pytest.mark.parametrize("levels,rows", [(3, 16), (3, 17), (3, 18), (3, 0), (4, 14), (4, 15), (4, 16),
                                          (2, 0)])
 @pytest.mark.parametrize("shape,iters", [((9, 10, 12), 7), ((21, 30, 264), 8), ((40, 31, 520), 12),
                                          ((5, 4, 8), 4), ((13, 40, 16), 9), ((12, 47, 264), 8)])
 @pytest.mark.parametrize("zchunk", [0, 1, 5])
 @pytest.mark.parametrize("prefetch", [1, 2])
 def test_jacobi3d_k_levels_bitexact(shape, iters, levels, rows, zchunk, prefetch):
-    """K = 2..4 sweeps per HBM pass (jacobi3d_tbk: one row per wave;
-    jacobi3d_tbr: tall tiles, several rows per wave): bit-identical to the
+    """K = 2..4 sweeps per HBM pass (jacobi3d_tbr: tall tiles, several rows
+    per wave, every tile shape): bit-identical to the
     oracle for tile-edge shapes, several x-segments and y-tiles, z-chunks of
     1..5 planes (march start/end clipping) and remainders (iters % K)."""
     call("cfd_set_jacobi3d_blocking", levels, rows, zchunk)
@@ -224,10 +225,10 @@ def test_jacobi3d_variants_agree_at_1024():
     div = torch.randn((n, n, n), generator=g, device=DEV, dtype=torch.float32)
     outs = []
     for cfgv, tb, *pf in [((1, 4, 0), 1), ((2, 4, 0), 1), ((1, 8, 64), 1), ((2, 16, 0), 1), ((0, 0, 0), 2),
-                     ((0, 0, 0), (2, 13, 0)), ((0, 0, 0), (2, 5, 40)), ((0, 0, 0), 3),
+                     ((0, 0, 0), (2, 18, 0)), ((0, 0, 0), (2, 16, 40)), ((0, 0, 0), 3),
                      ((0, 0, 0), 4), ((0, 0, 0), (3, 0, 70)), ((0, 0, 0), (3, 0, 0), 2),
-                     ((0, 0, 0), (4, 0, 0), 2), ((0, 0, 0), (3, 11, 0)), ((0, 0, 0), (3, 17, 0)),
-                     ((0, 0, 0), (4, 9, 0)), ((0, 0, 0), (4, 15, 0), 1)]:
+                     ((0, 0, 0), (4, 0, 0), 2), ((0, 0, 0), (3, 18, 0)), ((0, 0, 0), (3, 17, 0)),
+                     ((0, 0, 0), (4, 14, 0)), ((0, 0, 0), (4, 15, 0), 1)]:
         call("cfd_set_jacobi3d_config", *cfgv)
         call("cfd_set_jacobi3d_blocking", *(tb if isinstance(tb, tuple) else (tb, 0, 0)))
         call("cfd_set_jacobi3d_prefetch", pf[0] if pf else 0)
@@ -320,10 +321,10 @@ def test_rbgs3d_random_bitexact(shape, masked, fused):
     assert int(host(done)[0]) == n_ref
 
 
-# (blocking steps, rows): tuned 2-level kernel (rows 5 / 13), tall tiles with
-# one iteration per pass (steps 2), one and a half (steps 0 = auto, 3: passes
-# that end inside an iteration), two (steps 4)
-GS_FUSED = [(2, 5), (2, 13), (0, 0), (2, 0), (3, 0), (4, 0)]
+# (blocking steps, rows): tall tiles with one iteration per pass (steps 2; the
+# 16- and 20-row shapes explicitly), one and a half (steps 3: passes that end
+# inside an iteration), two (steps 4, and 0 = auto)
+GS_FUSED = [(2, 16), (2, 20), (0, 0), (2, 0), (3, 0), (4, 0)]
 
 
 @pytest.mark.parametrize("steps,rows", GS_FUSED)
@@ -590,7 +591,7 @@ def test_slab_rbgs_passes_emulated_on_one_gpu(tol, iters):
 def test_slab_rbgs_rccl_single_rank(overlap, ghost, steps, tol):
     """cfd_slab_rbgs3d_f32 with a one-rank communicator equals the oracle
     (one or two iterations per fused pass, early stop included)."""
-    call("cfd_set_jacobi3d_blocking", steps, 13 if steps == 2 else 0, 0)
+    call("cfd_set_jacobi3d_blocking", steps, 0, 0)
     nz, ny, nx, iters = 30, 26, 40, 300 if tol > 0 else 9
     rng = np.random.default_rng(11)
     div = rng.standard_normal((nz, ny, nx)).astype(np.float32) * np.float32(1e-3)
@@ -790,7 +791,7 @@ def test_slab_rbgs_local_group_multirank(R, ghost, steps, overlap, tol, iters):
     """cfd_slab_rbgs3d_f32 with R real ranks on one GPU: global colours, the
     global stop rule through the max-allreduce, the rollback of a stop inside
     a pair pass -- bit-identical to the oracle, same count on every rank."""
-    blocking = (steps, 13 if steps == 2 else 0, 0)
+    blocking = (steps, 0, 0)
     call("cfd_set_jacobi3d_blocking", *blocking)
     nz, ny, nx = 30, 26, 40
     rng = np.random.default_rng(11)

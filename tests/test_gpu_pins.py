@@ -142,10 +142,11 @@ def test_rbgs3d_explicit_gs_tiles_ragged(levels, rows, shape, tol, iters):
     assert np.array_equal(host(phi), ref)
 
 
-@pytest.mark.parametrize("iters", [3, 4])
+@pytest.mark.parametrize("iters", [4, 9, 10])
 def test_channel_1024x1024x512_slab_rccl_bitexact(iters):
     """Config 4's grid (nz = 512, ny = nx = 1024) through the RCCL slab driver
-    with a one-rank communicator: 3-deep ghosts, blocked pass, overlap on."""
+    with a one-rank communicator: 3-deep ghosts, blocked passes (9 sweeps =
+    three full tall-tile passes; 10 = three and a remainder), overlap on."""
     nz, ny, nx = 512, 1024, 1024
     h, dt = 1.0 / (nx - 1), np.float32(5e-5)
     rng = np.random.default_rng(77)
@@ -161,6 +162,26 @@ def test_channel_1024x1024x512_slab_rccl_bitexact(iters):
         assert np.array_equal(host(sj.owned()), ref)
     finally:
         comm.close()
+
+
+def test_jacobi3d_512_bench_step_200_sweeps_bitexact():
+    """Config 3's whole bench step at full size: phi = 0 and 200 sweeps
+    (cfd_jacobi3d_zero_f32: the fused first pass of 2 sweeps, then 66 passes
+    of jacobi3d_tbr<3> on the cost model's 512^3 shape -- 16-row tiles, four
+    z-chunks of 128 planes, 256 workgroups) against the oracle's 200 sweeps
+    (OpenMP form, bit-identical to the serial one)."""
+    n, iters = 512, 200
+    h, dt = 1.0 / (n - 1), np.float32(5e-5)
+    rng = np.random.default_rng(512)
+    div = rng.standard_normal((n, n, n), dtype=np.float32)
+    ref = oracle.jacobi3d(div, h=h, dt=dt, iters=iters, mt=True)
+    d = dev(div)
+    del div
+    phi = torch.empty_like(d)
+    tmp, rhs = torch.empty_like(d), torch.empty_like(d)
+    K.solve_pressure_jacobi3d_zero(phi, d, h, dt, iters, phi_tmp=tmp, rhs_ws=rhs)
+    assert last_shape() == (3, 10, 2, 128), last_shape()
+    assert np.array_equal(host(phi), ref)
 
 
 # ------------------------------------------------------------- device powf
