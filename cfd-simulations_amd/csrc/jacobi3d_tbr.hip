@@ -82,6 +82,7 @@ struct TbrArgs {
     const int *count;  // GS rollback: iterations done (device)
     int lag;         // GS: the stop test reads maxc[it-1-lag], maxc[it-2-lag] (see rbgs3d_tbr_pass)
     float *rhs_out;  // first pass (F & kFirstRhs): the rhs of the owned cells goes here
+    int xbw;         // XCD block width in x-segments (0: each XCD takes whole tile rows), see tbr_launch
 };
 // First-pass flags (template F of jacobi3d_tbr, Jacobi on the LDS-DMA path):
 // kFirstRhs: `div` is raw; the row waves form f32(h*h)*div/dt once per cell
@@ -467,9 +468,15 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // from it stay scalar
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int t = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int seg = t % a.nseg;
-    const int ty = (t / a.nseg) % a.ntile_y;
+    int seg = t % a.nseg;
+    int ty = (t / a.nseg) % a.ntile_y;
     const int zc = t / (a.nseg * a.ntile_y);
+    if (a.xbw) {  // XCD x takes a block of xbw segments x (per / xbw) tile rows
+        const int per = gridDim.x / kNumXcd, x = t / per, k = t - x * per;
+        const int nbx = a.nseg / a.xbw, bh = per / a.xbw;
+        seg = (x % nbx) * a.xbw + k % a.xbw;
+        ty = (x / nbx) * bh + k / a.xbw;
+    }
     const int z0 = a.zb + zc * a.zchunk;
     if (z0 >= a.ze) return;  // workgroup-uniform
     const int z1 = min(z0 + a.zchunk, a.ze);
@@ -1031,6 +1038,21 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
     a.nseg = nseg;
     a.ntile_y = ceil_div(a.ny - 2, best->rows());
     a.zchunk = best_zlen;
+    // CFD_TBR_XBW = w (A/B knob): each XCD takes a block of w x-segments x
+    // (its share / w) tile rows instead of whole tile rows, which changes how
+    // many halo rows / columns two XCDs both fetch; only for one z-chunk and
+    // block counts that tile the plane exactly
+    {
+        static const int xbw_env = [] {
+            const char *e = getenv("CFD_TBR_XBW");
+            return e ? atoi(e) : 0;
+        }();
+        const int tiles = nseg * a.ntile_y, per = tiles / kNumXcd;
+        a.xbw = 0;
+        if (xbw_env > 0 && best_zlen >= L && tiles % kNumXcd == 0 && nseg % xbw_env == 0 && per % xbw_env == 0 &&
+            (kNumXcd / (nseg / xbw_env)) * (per / xbw_env) == a.ntile_y && kNumXcd % (nseg / xbw_env) == 0)
+            a.xbw = xbw_env;
+    }
     g_last_shape[0] = best->K;
     g_last_shape[1] = best->nwr;
     g_last_shape[2] = best->rpw;
@@ -1041,7 +1063,12 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
     // save ~2 % per step but would run up to 5 extra (the slab boundary
     // launches: 3 planes = 7 steps, 12 rotated)
     const int nsteps = best_zlen + 2 * best->K - 2;
-    const bool shiftq = MODE == kJacobi && pd == 1 && best->K == 3 && nsteps % 6 != 0 && nsteps < 216;
+    static const bool shiftq_all = [] {  // CFD_TBR_SHIFTQ=1 (A/B knob): shifting queues everywhere
+        const char *e = getenv("CFD_TBR_SHIFTQ");
+        return e && atoi(e) == 1;
+    }();
+    const bool shiftq = MODE == kJacobi && pd == 1 && best->K == 3 &&
+                        (shiftq_all || (nsteps % 6 != 0 && nsteps < 216));
 #define CFD_TBR_L(KV, NW, RP, PR, PDV) \
     hipLaunchKernelGGL((jacobi3d_tbr<KV, NW, RP, PR, PDV, MODE>), dim3(blocks), dim3((NW + 1) * 64), 0, s, a)
 #define CFD_TBR(KV, NW, RP)                                                                   \

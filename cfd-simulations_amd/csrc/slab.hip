@@ -623,7 +623,7 @@ int cfd_comm_init_ipc(int nranks, int rank, void **comm) {
         CFD_CHECK_HIP(hipStreamCreateWithFlags(&ce.xs[d], hipStreamNonBlocking));
         CFD_CHECK_HIP(hipEventCreateWithFlags(&ce.xev[d], hipEventDisableTiming));
     }
-    CFD_CHECK_HIP(hipEventCreateWithFlags(&c->ev_boundary, hipEventDisableTiming | hipEventReleaseToDevice));
+    CFD_CHECK_HIP(hipEventCreateWithFlags(&c->ev_boundary, hipEventDisableTiming));
     CFD_CHECK_HIP(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
     CFD_CHECK_HIP(hipDeviceSynchronize());
     *comm = c.release();

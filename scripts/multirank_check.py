@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--size", type=int, default=64)
     ap.add_argument("--transport", default="ce", choices=["ce", "rccl"])
     ap.add_argument("--quick", action="store_true", help="fewer cases")
+    ap.add_argument("--repeat", type=int, default=1, help="run the whole case list this many times")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -61,6 +62,20 @@ def main():
             print(f"world={world} {a.transport} {tag}: {'bit-exact' if same else 'MISMATCH'}", flush=True)
 
     try:
+        for _ in range(a.repeat):
+            run_cases(a, S, comm, rank, world, nz, ny, nx, div, rng, gather, report)
+        if hasattr(comm, "status"):
+            comm.status()
+    finally:
+        comm.close()
+        dist.destroy_process_group()
+    if rank == 0:
+        print("MULTIRANK", "OK" if ok else "FAIL", flush=True)
+        sys.exit(0 if ok else 1)
+
+
+def run_cases(a, S, comm, rank, world, nz, ny, nx, div, rng, gather, report):
+    if True:
         ghosts = (1, 3) if a.quick else (1, 2, 3, 4)
         for ghost in ghosts:
             planes = [S.SlabPlan(nz, world, r, ghost).nz_local for r in range(world)]
@@ -104,14 +119,6 @@ def main():
                 else:
                     same = True
                 report(f"rbgs ghost={ghost} overlap={overlap} tol={tol} iters={iters} count={cnt}", same)
-        if hasattr(comm, "status"):
-            comm.status()
-    finally:
-        comm.close()
-        dist.destroy_process_group()
-    if rank == 0:
-        print("MULTIRANK", "OK" if ok else "FAIL", flush=True)
-        sys.exit(0 if ok else 1)
 
 
 if __name__ == "__main__":
