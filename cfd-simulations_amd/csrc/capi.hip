@@ -46,6 +46,8 @@ static Tuning process_defaults() {
         t.j2s_k = k >= 1 && k <= 8 ? k : 4;
         t.j2s_rw = env_int("CFD_J2_SMALL_RW", 1) == 2 ? 2 : 1;
         t.j2s_vec = env_int("CFD_J2_SMALL_VEC", 1) == 1 ? 1 : 0;  // 0: 16 bytes per lane
+        const int dd = env_int("CFD_J2_DMA", t.j2_dma);
+        t.j2_dma = dd == 0 || dd == 4 || dd == 6 ? dd : t.j2_dma;
         t.gs_rw = env_int("CFD_GS_SMALL_RW", 2) == 1 ? 1 : 2;
         t.gs_vec = env_int("CFD_GS_SMALL_VEC", 1) == 4 ? 4 : 1;
         t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;

@@ -16,6 +16,10 @@ struct Tuning {
     int tb_steps = 0, tb_rows = 0, tb_zchunk = 0, tb_prefetch = 0;
     // 2-D Jacobi sweeps per pass: 0 auto, 1 off, 2..6, 8, 10, 12
     int j2_blocking = 0;
+    // 2-D blocked Jacobi without a mask: rows staged through a per-wave LDS
+    // ring this many rows ahead (jacobi2d_tbd: 6 or 4; 0 = register prefetch
+    // one row ahead, jacobi2d_tbk)
+    int j2_dma = 6;
     // small-grid 2-D Jacobi: sweeps per launch (1..8), rows per wave, cells per lane
     int j2s_k = 4, j2s_rw = 1, j2s_vec = 1;
     // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per

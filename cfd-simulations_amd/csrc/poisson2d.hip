@@ -1176,6 +1176,13 @@ int cfd_set_jacobi2d_blocking(int steps) {
     return CFD_OK;
 }
 
+int cfd_set_jacobi2d_staging(int rows_ahead) {
+    CFD_REQUIRE(rows_ahead == 0 || rows_ahead == 4 || rows_ahead == 6,
+                "2-D staging depth must be 0 (register prefetch), 4 or 6 rows");
+    tuning().j2_dma = rows_ahead;
+    return CFD_OK;
+}
+
 size_t cfd_rbgs_workspace_bytes(int iterations) {
     // flags, maxc[iterations], then the small-grid kernel's kGsSlots slot rows
     return 16 + sizeof(float) * (size_t)(1 + kGsSlots) * (size_t)(iterations > 0 ? iterations : 1);

@@ -89,10 +89,17 @@ struct LocalGroup {
 // 13 % slower interiors, and the 256-workgroup 4-level GS tile in two rounds).
 // The copy engines take no CU at all, so the interior keeps the single-GPU
 // plan.  Ordering: counts are monotonic per direction and every rank runs the
-// same exchanges, so no host handshake is needed; a copy into a neighbour's
-// buffer can only start after that neighbour's previous sync (its boundary
-// launches, the only readers of ghost planes, precede the planes it sends,
-// which our next pass waits for), so no ghost plane is overwritten while read.
+// same exchanges, so no host handshake is needed; inside a solve a copy into
+// a neighbour's buffer can only start after that neighbour's previous sync
+// (its boundary launches, the only readers of ghost planes, precede the planes
+// it sends, which our next pass waits for), so no ghost plane is overwritten
+// while read.  Across solves nothing orders a neighbour's first copy after
+// this rank's earlier work on its buffers (a zero start has no initial
+// exchange; a fill of phi_tmp queued just before the solve was seen to land
+// over the ghosts a fast neighbour had already sent), so each solve begins
+// with a ready word per direction: written to the neighbour's flag block on
+// the compute stream behind all earlier work (ce_begin), and waited for on
+// the copy stream before that solve's first copy into the neighbour.
 // The red-black GS stop rule needs the global max|change| of each iteration:
 // the same sync kernel stores this rank's maxima into every rank's gather ring
 // (8-byte {tag, value} granules, system-scope stores into the uncached flag
@@ -103,6 +110,8 @@ constexpr int kCeMaxRanks = 16;
 constexpr int kCeRing = 256;             // gather slots, iterations in flight
 constexpr int kCeFromLo = 0;             // u32 word: exchanges received from the lo neighbour
 constexpr int kCeFromHi = 32;            // ... from the hi neighbour (own 128-B line)
+constexpr int kCeReadyFromLo = 64;       // solves the lo neighbour has begun (its buffers free)
+constexpr int kCeReadyFromHi = 96;       // ... the hi neighbour
 constexpr int kCeGatherWord = 256;       // gather ring (u64 granules) at byte 1024
 constexpr size_t kCeFlagBytes = 4 * (size_t)kCeGatherWord + 8 * (size_t)kCeRing * kCeMaxRanks;
 constexpr uint32_t kCeMagic = 0x43464445u;  // "CFDE"
@@ -143,6 +152,10 @@ struct CeState {
     float *pend[2] = {nullptr, nullptr};  // exported, not yet imported
     size_t pend_n = 0;
     unsigned sent[2] = {0, 0}, recvd[2] = {0, 0}, gathered = 0;
+    // solves begun per direction: every rank begins the same solves, so the
+    // neighbour's ready word reaches this count when it has begun this one
+    unsigned ready_sent[2] = {0, 0};
+    bool need_ready[2] = {false, false};  // the solve's first copy in that direction is pending
 };
 
 struct SlabComm {
@@ -432,6 +445,20 @@ __global__ __launch_bounds__(64) void k_ce_sync(CeSyncArgs a) {
     if (!ok) atomicOr(a.status, 1);
 }
 
+// a copy stream's wait for a neighbour's ready word (bounded, as k_ce_sync)
+__global__ __launch_bounds__(64) void k_ce_wait_ready(const unsigned *w, unsigned want, int *status) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = wall_clock64();
+    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    while ((int)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - want) < 0) {
+        if (wall_clock64() - t0 > kCeSpinLimit) {
+            atomicOr(status, 1);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 static int ce_map(CeState &ce, int rank, const hipIpcMemHandle_t &h, char **base) {
     for (const CeState::Map &m : ce.maps)
         if (m.rank == rank && !memcmp(&m.h, &h, sizeof h)) {
@@ -488,6 +515,13 @@ static int exchange_ce(SlabComm *c, const float *a, int nzl, int G, size_t plane
         if (d == 0) dst += pn - n;
         unsigned *word = ce.peer_flags[peer] + (d == 0 ? kCeFromHi : kCeFromLo);
         CFD_CHECK_HIP(hipStreamWaitEvent(ce.xs[d], ready, 0));
+        if (ce.need_ready[d]) {  // the neighbour has begun this solve (ce_begin)
+            hipLaunchKernelGGL(k_ce_wait_ready, dim3(1), dim3(64), 0, ce.xs[d],
+                               ce.flags + (d == 0 ? kCeReadyFromLo : kCeReadyFromHi), ce.ready_sent[d],
+                               ce.status);
+            CFD_LAUNCH_CHECK();
+            ce.need_ready[d] = false;
+        }
         CFD_CHECK_HIP(hipMemcpyAsync(dst, src, n * sizeof(float), kCopyEngine, ce.xs[d]));
         CFD_CHECK_HIP(hipStreamWriteValue32(ce.xs[d], word, ++ce.sent[d], 0));
         ce.used[d] = true;
@@ -515,6 +549,21 @@ static int ce_sync(SlabComm *c, hipStream_t s, int lo, int hi, float *maxc, int 
     if (!a.want_lo && !a.want_hi && !a.cnt) return CFD_OK;
     hipLaunchKernelGGL(k_ce_sync, dim3(1), dim3(64), 0, s, a);
     CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// start of a solve, after ce_check_attached: tell each neighbour, behind
+// everything queued on s so far, that this rank's buffers may be written
+static int ce_begin(SlabComm *c, hipStream_t s, int lo, int hi) {
+    CeState &ce = *c->ce;
+    for (int d = 0; d < 2; ++d) {
+        const int peer = d == 0 ? lo : hi;
+        if (peer < 0) continue;
+        // to lo: we are its hi neighbour
+        unsigned *word = ce.peer_flags[peer] + (d == 0 ? kCeReadyFromHi : kCeReadyFromLo);
+        CFD_CHECK_HIP(hipStreamWriteValue32(s, word, ++ce.ready_sent[d], 0));
+        ce.need_ready[d] = true;
+    }
     return CFD_OK;
 }
 
@@ -836,7 +885,7 @@ static int slab_jacobi3d(SlabComm *c, const float *div, float *phi, float *phi_t
         src = rhs_ws;
     }
     if (c->grp && (rc = register_local(c, phi, phi_tmp, nullptr, nz_local, G, plane))) return rc;
-    if (c->ce && (rc = ce_check_attached(c, phi, phi_tmp))) return rc;
+    if (c->ce && ((rc = ce_check_attached(c, phi, phi_tmp)) || (rc = ce_begin(c, s, lo_peer, hi_peer)))) return rc;
     // ghosts of the initial guess (a zero start reads none)
     if (!zero) {
         if (c->ce) {
@@ -1021,7 +1070,7 @@ int cfd_slab_rbgs3d_f32(void *comm, const float *div, float *phi, float *phi_tmp
         if ((r = exchange_ce(c, a, nz_local, G, plane, lo_peer, hi_peer, c->ev_boundary))) return r;
         return ce_sync(c, s, lo_peer, hi_peer, reduce ? w->maxc : nullptr, it, cnt);
     };
-    if (c->ce && (rc = ce_check_attached(c, phi, phi_tmp))) return rc;
+    if (c->ce && ((rc = ce_check_attached(c, phi, phi_tmp)) || (rc = ce_begin(c, s, lo_peer, hi_peer)))) return rc;
     // ghosts of the initial guess
     if (c->ce) {
         if ((rc = ce_step(phi, 0, 0))) return rc;

@@ -80,6 +80,11 @@ int cfd_set_jacobi2d_blocking(int steps);
 /* 2-D Jacobi sweeps per blocked pass: the set depth, or the large-grid auto
  * depth (8). */
 int cfd_get_jacobi2d_levels(void);
+/* Blocked 2-D passes at 4, 6 or 8 sweeps without a mask stage their rows
+ * through a per-wave LDS ring filled by LDS-DMA this many rows ahead (4 or 6,
+ * the default 6); 0 = the register march that prefetches one row ahead.  Same
+ * bits either way (a tuning knob, per host thread like the others). */
+int cfd_set_jacobi2d_staging(int rows_ahead);
 int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, double *resid_out, void *stream);

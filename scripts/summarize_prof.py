@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--bytes-per-update", type=float, default=12.0)
     ap.add_argument("--trace", help="run_kernel_trace.csv: keep one mid-run window of the timeline")
     ap.add_argument("--window", type=int, default=10, help="kernels in the --trace window")
+    ap.add_argument("--skip", type=int, default=0,
+                    help="drop the first N launches of the kernel (the cold launches at process start)")
     a = ap.parse_args()
     out_dir = ROOT / "profiles"
     out_dir.mkdir(exist_ok=True)
@@ -87,12 +89,14 @@ def main():
         f = counter(a.fetch, "FETCH_SIZE")
         w = counter(a.write, "WRITE_SIZE")
         k = max(f, key=lambda n: sum(f[n]))
-        fetch = sum(f[k]) / len(f[k]) * 1024.0
-        write = sum(w[k]) / len(w[k]) * 1024.0
+        fk, wk = f[k][a.skip:], w[k][a.skip:]
+        fetch = sum(fk) / len(fk) * 1024.0
+        write = sum(wk) / len(wk) * 1024.0
         hbm = 2.0 * fetch + write
-        entry = {"kernel": k, "launches": len(f[k]), "n_gpus": a.n_gpus,
+        entry = {"kernel": k, "launches": len(fk), "skipped_first": a.skip, "n_gpus": a.n_gpus,
                  "fetch_size_bytes_raw": fetch, "write_size_bytes": write,
                  "hbm_bytes_per_launch": hbm,
+                 "fetch_x2_range_bytes": [2048.0 * min(fk), 2048.0 * max(fk)],
                  "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of 16-B streaming reads)",
                  "source": f"{a.tag}: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes"}
         if a.cell_updates:

@@ -75,6 +75,32 @@ def test_jacobi2d_random_bitexact(dtype, shape, iters, blocking):
     assert np.array_equal(host(phi), ref)
 
 
+@pytest.mark.parametrize("staging", [0, 4, 6])
+@pytest.mark.parametrize("blocking", [4, 6, 8])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("shape,iters,pre", [((37, 53), 17, False), ((130, 260), 31, True), ((9, 124), 6, True),
+                                             ((71, 1000), 12, False), ((300, 124), 9, True), ((517, 40), 7, False),
+                                             ((4, 600), 8, True), ((1030, 244), 16, True)])
+def test_jacobi2d_staged_rows_bitexact(dtype, shape, iters, pre, blocking, staging):
+    """Unmasked blocked passes, whose rows come through the per-wave LDS ring
+    (jacobi2d_tbd, `staging` rows ahead) or the register march (0): bit-exact
+    against the oracle with and without the rhs workspace."""
+    call("cfd_set_jacobi2d_blocking", blocking)
+    call("cfd_set_jacobi2d_staging", staging)
+    try:
+        rng = np.random.default_rng(21)
+        div = rng.standard_normal(shape).astype(dtype)
+        phi0 = rng.standard_normal(shape).astype(dtype)
+        ref = oracle.jacobi2d(div, phi0, dx=0.017, dt=np.float32(2e-4), iters=iters)
+        phi = dev(phi0)
+        K.solve_pressure_jacobi(phi, dev(div), 0.017, np.float32(2e-4), None, iters,
+                                rhs_ws=torch.empty_like(phi) if pre else None)
+        assert np.array_equal(host(phi), ref)
+    finally:
+        call("cfd_set_jacobi2d_staging", 6)
+        call("cfd_set_jacobi2d_blocking", 0)
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_jacobi2d_rhs_workspace_bitexact(dtype):
     """The RHS prologue (rhs_ws) gives the same bits as the in-register RHS."""
