@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--tb-rows", type=int, default=0)
     ap.add_argument("--tb-zchunk", type=int, default=0)
     ap.add_argument("--tb-prefetch", type=int, default=0, help="planes of prefetch in the blocked kernel")
+    ap.add_argument("--j2-staging", type=int, default=-1,
+                    help="2-D blocked Jacobi: rows staged ahead through the LDS ring (0 = register march, -1 = library default)")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--transport", default="ce", choices=["ce", "rccl"],
                     help="slab halo transport: copy engines over IPC (default) or RCCL send/recv")
@@ -282,6 +284,8 @@ def main():
         call("cfd_set_jacobi3d_prefetch", ARGS.tb_prefetch)
     else:
         call("cfd_set_jacobi2d_blocking", ARGS.tb)
+        if ARGS.j2_staging >= 0:
+            call("cfd_set_jacobi2d_staging", ARGS.j2_staging)
     dt = np.float32(5e-5)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
 

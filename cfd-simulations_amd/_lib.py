@@ -34,8 +34,11 @@ PROTOTYPES = {
                                  P]),
     "cfd_jacobi3d_zero_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_double, c_float, c_int, P]),
     "cfd_rbgs_workspace_bytes": (c_size_t, [c_int]),
+    "cfd_rbgs2d_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "cfd_rbgs2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_float, c_int, c_double,
                                P, P, P, P]),
+    "cfd_rbgs2d_f32_ws": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_float, c_int, c_double,
+                                  P, P, c_size_t, P, P]),
     "cfd_rbgs3d_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_double, c_double, c_double, c_float,
                                c_int, c_double, P, P, P, P]),
     "cfd_supg_tau2d_f32": (c_int, [P, P, P, c_float, P, c_int, c_int, c_double, c_double, c_float, P]),
@@ -103,6 +106,7 @@ PROTOTYPES = {
     "cfd_rbgs_init": (c_int, [P, c_int, c_double, P, P]),
     "cfd_rbgs_finish": (c_int, [P, P, P, c_size_t, P, P]),
     "cfd_set_small2d_gs_iters": (c_int, [c_int, c_int]),
+    "cfd_set_small2d_gs_persistent": (c_int, [c_int]),
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_blocking": (c_int, [c_int, c_int, c_int]),
     "cfd_get_jacobi3d_levels": (c_int, []),

@@ -52,6 +52,7 @@ static Tuning process_defaults() {
         t.gs_vec = env_int("CFD_GS_SMALL_VEC", 1) == 4 ? 4 : 1;
         t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;
         t.gs_wg = env_int("CFD_GS_SMALL_WG", t.gs_wg) != 0;
+        t.gs_persist = env_int("CFD_GS_PERSIST", t.gs_persist) != 0;
         const int ni = env_int("CFD_GS_SMALL_NI", t.gs_ni);
         t.gs_ni = ni >= 1 && ni <= 4 ? ni : t.gs_ni;
         return t;
@@ -126,6 +127,12 @@ int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows) {
     const Tuning d = process_defaults();
     tuning().gs_ni = iters_per_launch ? iters_per_launch : d.gs_ni;
     tuning().gs_wg = shared_rows ? shared_rows == 2 : d.gs_wg;
+    return CFD_OK;
+}
+
+int cfd_set_small2d_gs_persistent(int mode) {
+    CFD_REQUIRE(mode >= 0 && mode <= 2, "small-grid GS persistent mode must be 0 (default), 1 (off) or 2 (on)");
+    tuning().gs_persist = mode ? mode == 2 : process_defaults().gs_persist;
     return CFD_OK;
 }
 

@@ -18,8 +18,9 @@ struct Tuning {
     int j2_blocking = 0;
     // 2-D blocked Jacobi without a mask: rows staged through a per-wave LDS
     // ring this many rows ahead (jacobi2d_tbd: 6 or 4; 0 = register prefetch
-    // one row ahead, jacobi2d_tbk)
-    int j2_dma = 6;
+    // one row ahead, jacobi2d_tbk, the default: r03 8192^2 f64 0.337 ms per
+    // pass against 0.355 (6 ahead) and 0.362 (4 ahead), same box)
+    int j2_dma = 0;
     // small-grid 2-D Jacobi: sweeps per launch (1..8), rows per wave, cells per lane
     int j2s_k = 4, j2s_rw = 1, j2s_vec = 1;
     // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per
@@ -30,6 +31,10 @@ struct Tuning {
     // by iterations per launch 2 / 3 / 4: shared 3.04 / 2.33 / 1.97; per-wave
     // (2 rows per wave) 2.46 / 2.10 / 2.63, (1 row) 2.54 / 2.33 / 2.24
     int gs_wg = 1;
+    // small-grid GS as one persistent launch (rbgs2d_persist) when the caller's
+    // workspace holds its exchange rings (cfd_rbgs2d_workspace_bytes) and
+    // every tile fits on the chip at once; 0 = one launch per gs_ni iterations
+    int gs_persist = 1;
 };
 Tuning &tuning();
 
@@ -94,6 +99,20 @@ int launch_rbgs_copy(const RbgsWs *ws, float *phi, const float *phi_tmp, size_t 
 // ran, and *iters_done <- the count (both read on device: no host sync)
 int launch_rbgs_finish(RbgsWs *ws, float *phi, const float *phi_tmp, size_t n,
                        int *iters_done, hipStream_t s);  // count + copy, one iteration per pass
+
+// rbgs2d_persist.hip: the small-grid 2-D red-black GS as one persistent
+// launch.  Bytes of its exchange rings past the base workspace (0 when the
+// grid is not a small grid); the solve returns 1 when it ran, 0 when it does
+// not apply (too small a workspace, tiles not all resident, knob off), so the
+// caller takes the launch-per-block path.
+size_t rbgs2d_persist_extra_bytes(int ny, int nx);
+int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int ny, int nx, float cx,
+                         float cy, float cd, float dt_inv, float tol, float *phi_tmp, RbgsWs *ws,
+                         size_t ws_bytes, int iterations, int *iters_done, hipStream_t s, int *rc);
+constexpr int kGsSlotRows = 16;  // rbgs2d_small's per-iteration maxima slots
+inline size_t rbgs_base_bytes(int iterations) {
+    return 16 + sizeof(float) * (size_t)(1 + kGsSlotRows) * (size_t)(iterations > 0 ? iterations : 1);
+}
 
 // 3-D red-black GS (poisson3d.hip / jacobi3d_tb.hip)
 struct RbgsConsts {

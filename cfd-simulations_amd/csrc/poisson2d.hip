@@ -1185,12 +1185,27 @@ int cfd_set_jacobi2d_staging(int rows_ahead) {
 
 size_t cfd_rbgs_workspace_bytes(int iterations) {
     // flags, maxc[iterations], then the small-grid kernel's kGsSlots slot rows
-    return 16 + sizeof(float) * (size_t)(1 + kGsSlots) * (size_t)(iterations > 0 ? iterations : 1);
+    static_assert(kGsSlots == kGsSlotRows, "one slot-row count");
+    return rbgs_base_bytes(iterations);
+}
+
+size_t cfd_rbgs2d_workspace_bytes(int ny, int nx, int iterations) {
+    // the base workspace, then (small grids) the persistent solve's exchange rings
+    const size_t base = rbgs_base_bytes(iterations);
+    if (ny < 3 || nx < 3 || !rbgs2d_small_grid(ny, nx)) return base;
+    return ((base + 255) & ~(size_t)255) + rbgs2d_persist_extra_bytes(ny, nx);
 }
 
 int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
                    double dy, float dt, int iterations, double tolerance, float *phi_tmp, void *ws,
                    int *iters_done, void *stream) {
+    return cfd_rbgs2d_f32_ws(phi, div, mask, ny, nx, dx, dy, dt, iterations, tolerance, phi_tmp, ws,
+                             cfd_rbgs_workspace_bytes(iterations), iters_done, stream);
+}
+
+int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
+                      double dy, float dt, int iterations, double tolerance, float *phi_tmp, void *ws,
+                      size_t ws_bytes, int *iters_done, void *stream) {
     CFD_REQUIRE(phi && div && ws, "rbgs2d: null pointer");
     CFD_REQUIRE(ny >= 1 && nx >= 1 && iterations >= 0, "rbgs2d: bad arguments");
     hipStream_t s = as_stream(stream);
@@ -1211,7 +1226,14 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
         if ((rc = fix_edge_rows<float>(phi, phi_tmp, nullptr, ny, nx, s))) return rc;
         float *a = phi, *b = phi_tmp;
         if (rbgs2d_small_grid(ny, nx)) {
-            // small grid (the v5 cylinder): P iterations per launch (the last
+            // small grid (the v5 cylinder): one persistent launch when the
+            // workspace holds its rings and every tile is resident at once
+            if (rbgs2d_persist_solve(phi, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, phi_tmp, w, ws_bytes,
+                                     iterations, iters_done, s, &rc)) {
+                timing_end(tk, s, iterations);
+                return rc;
+            }
+            // else P iterations per launch (the last
             // launch shorter), then the rollback of a stop inside a launch
             const int P = tuning().gs_ni;
             CFD_CHECK_HIP(hipMemsetAsync(w->maxc + iterations, 0, sizeof(float) * kGsSlots * (size_t)iterations, s));

@@ -1,0 +1,423 @@
+// rbgs2d_persist.hip -- the small-grid 2-D red-black Gauss-Seidel solve
+// (v5.py:202-226, the v5 cylinder's 600 x 180 pressure solve) as ONE
+// persistent launch.
+//
+// Why: at 600 x 180 a GS launch is latency, not bytes.  The launch-per-block
+// path (rbgs2d_wg, poisson2d.hip) pays per launch ~4.2 us of fixed cost (the
+// kernel boundary, the tile's load latency, the stores and slot atomics) for
+// 4 iterations; here the tiles stay resident for the whole solve and the
+// kernel boundary between two blocks of iterations becomes a neighbour
+// hand-off of 8-byte {value, tag} granules (~1 us, MI355X_MICROARCH.md,
+// handoff-1to1), which needs no flag, fence or barrier: a granule is valid when
+// its tag is the block that wrote it.
+//
+// Geometry and arithmetic are rbgs2d_wg's, so the two paths are bit-identical
+// block for block: a workgroup is one 32-row x 64-column tile (16 waves x 2
+// rows, one cell per lane) that advances NI iterations (L = 2 NI colour
+// levels) per block, the intermediate levels eroding into an L-row / L-lane
+// halo, and owns its inner (32 - 2L) x (64 - 2L) cells.  Own cells stay in
+// registers from block to block; after a block the tile publishes them to a
+// ring of granule planes (slot = block mod 3, tag = block + 1), and before the
+// next block it polls its halo cells (all owned by its 8 neighbour tiles) in
+// the previous block's slot.  Rows 0 and ny-1 and cells outside the grid never
+// change, so they keep the values loaded at the start.
+//
+// Stop rule (v5.py:224-225): each tile publishes its per-iteration max|change|
+// of own cells as granules (ring of 4 blocks).  At the end of block k, before
+// block k is published, wave 0 folds every tile's maxima of block k - 2 (their
+// loads were issued at the block's start, so their latency hides behind the
+// levels) and the first iteration n whose global max is < tol stops the solve:
+// every tile then re-runs block B = n / NI from its input (block B - 1's slot,
+// which no tile has overwritten: nobody publishes block k without having ruled
+// out a stop in block k - 2) for the n - B NI + 1 iterations it needs.  The
+// last two blocks are checked after the loop.  With tol <= 0 nothing is
+// published or polled for the stop rule (it can never fire).
+//
+// Ordering of the granule ring (3 slots): a tile publishes block k over block
+// k - 3's granules only after it has consumed its neighbours' block k - 1
+// output, which they published after reading their block k - 2 input, the
+// last read of block k - 3's granules.  Every poll is bounded (20 s of the
+// 100 MHz clock from the kernel's start, as the slab sync kernel), so a tile
+// that never arrives (another kernel holding the CUs) ends the solve with a
+// status bit instead of a hang; the launcher also checks that every tile is
+// resident at once before choosing this path.
+#include "internal.hpp"
+
+namespace cfd {
+namespace {
+
+constexpr int kPW = 16, kPRW = 2, kPT0 = kPW * kPRW;  // waves, rows per wave, tile rows
+constexpr int kPGSlots = 3;                            // granule planes (block outputs)
+constexpr int kPMSlots = 4;                            // per-block maxima ring
+constexpr int kPMaxTiles = 256;                        // one tile per CU at most
+constexpr int kPMaxNI = 4;
+constexpr unsigned long long kPSpinLimit = 2000000000ull;  // 20 s at 100 MHz
+
+struct PersistArgs {
+    const float *in;
+    float *out;
+    const float *div;
+    const uint8_t *mask;
+    unsigned long long *G;  // kPGSlots planes of ny * nx granules
+    unsigned long long *M;  // kPMSlots x NI x ntiles granules
+    RbgsWs *ws;
+    int ny, nx, nseg, ntiles, niters;
+    float cx, cy, cd, dt_inv, tol;
+};
+
+__device__ inline unsigned long long gload(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load sc1
+}
+__device__ inline void gstore(unsigned long long *p, float v, unsigned tag) {
+    __hip_atomic_store(p, ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store sc1
+}
+__device__ inline unsigned gtag(unsigned long long g) { return (unsigned)(g >> 32); }
+__device__ inline float gval(unsigned long long g) { return __uint_as_float((unsigned)g); }
+// LDS writes done, then the workgroup barrier; global loads stay in flight
+// (the compiler's __syncthreads would wait for them too)
+__device__ inline void lds_barrier_p() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool MASK, int NI>
+__global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
+    constexpr int L = 2 * NI, HL = L, SOUT = 64 - 2 * HL, OUT = kPT0 - 2 * L;
+    constexpr int MT = kPMaxTiles / 64;  // maxima granules per lane and iteration (wave 0)
+    static_assert(OUT >= 2, "too many levels for the tile");
+    __shared__ float S[2][kPT0][64];
+    __shared__ float red[NI][kPW];
+    __shared__ int sh_stop;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int seg = bid % a.nseg, ty = bid / a.nseg;
+    const int ytop = 1 + ty * OUT - L;  // global row of tile row 0
+    const int x = seg * SOUT - HL + lane;
+    const bool valid = x >= 0 && x < a.nx;
+    const bool writer = lane >= HL && lane < 64 - HL && valid;
+    const bool check = a.tol > 0.f;
+    const unsigned long long t0 = wall_clock64();
+    bool broken = false;  // a poll expired (per wave; the result is garbage then)
+    auto expired = [&]() {
+        broken = broken || wall_clock64() - t0 > kPSpinLimit;
+        return broken;
+    };
+
+    float A[kPRW], RH[kPRW];
+    bool U0[kPRW], U1[kPRW], own[kPRW], inner[kPRW];
+    size_t off[kPRW];
+#pragma unroll
+    for (int j = 0; j < kPRW; ++j) {
+        const int i = kPRW * w + j, y = ytop + i;
+        const bool in_ = valid && y >= 0 && y <= a.ny - 1;
+        off[j] = (size_t)min(max(y, 0), a.ny - 1) * a.nx + (valid ? x : 0);
+        const float v = a.in[off[j]];
+        const float d = a.div[off[j]];
+        const bool mk = MASK ? a.mask[off[j]] != 0 : false;
+        const bool edge = y <= 0 || y >= a.ny - 1;
+        A[j] = in_ ? v : 0.f;
+        RH[j] = -(in_ ? d : 0.f) * a.dt_inv;
+        const bool ok = in_ && !edge && x >= 1 && x < a.nx - 1 && !mk;
+        const bool even = ((y + x + 1) & 1) == 0;
+        U0[j] = ok && even;
+        U1[j] = ok && !even;
+        own[j] = writer && i >= L && i < kPT0 - L && y <= a.ny - 2;
+        inner[j] = in_ && !edge;  // cells some tile owns (all others never change)
+    }
+    const size_t plane = (size_t)a.ny * a.nx;
+
+    // cells of block k's input (block k-1's granules): the halo cells, or all
+    // inner cells of the tile (a rollback, whose registers hold a later block)
+    auto fetch = [&](int k, bool all) {
+        const unsigned long long *Gk = a.G + (size_t)((k - 1) % kPGSlots) * plane;
+        const unsigned want = (unsigned)k;
+        bool need[kPRW];
+#pragma unroll
+        for (int j = 0; j < kPRW; ++j) need[j] = inner[j] && (all || !own[j]);
+        while (true) {
+            unsigned long long g[kPRW];
+#pragma unroll
+            for (int j = 0; j < kPRW; ++j) g[j] = need[j] ? gload(Gk + off[j]) : 0ull;
+            bool more = false;
+#pragma unroll
+            for (int j = 0; j < kPRW; ++j) {
+                if (need[j] && gtag(g[j]) == want) {
+                    A[j] = gval(g[j]);
+                    need[j] = false;
+                }
+                more = more || need[j];
+            }
+            if (!__any(more) || expired()) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+
+    // colour levels 1..2m of one block (m = iterations, block-uniform); own
+    // cells' max|change| per iteration into mx
+    float mx[NI];
+    auto levels = [&](int m) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) mx[q] = 0.f;
+#pragma unroll
+        for (int j = 0; j < kPRW; ++j) S[0][kPRW * w + j][lane] = A[j];
+        lds_barrier_p();
+#pragma unroll
+        for (int l = 1; l <= L; ++l) {
+            if (l > 2 * m) break;
+            const int par = (l - 1) & 1;  // colour of this level
+            const int rb = (l - 1) & 1, wb = l & 1;
+            float B[kPRW];
+#pragma unroll
+            for (int j = 0; j < kPRW; ++j) {
+                const int i = kPRW * w + j;
+                const float Nn = j + 1 < kPRW ? A[j + 1] : (i + 1 < kPT0 ? S[rb][i + 1][lane] : 0.f);
+                const float Sv = j > 0 ? A[j - 1] : (i > 0 ? S[rb][i - 1][lane] : 0.f);
+                const float W = dpp_from_lower(A[j]);
+                const float E = dpp_from_upper(A[j]);
+                const bool live = i >= l && i < kPT0 - l;
+                const bool upd = live && (par ? U1[j] : U0[j]);
+                const float nv = ((a.cx * (E + W) + a.cy * (Nn + Sv)) - RH[j]) * a.cd;
+                B[j] = upd ? nv : A[j];
+                const float ch = upd ? fabsf(nv - A[j]) : 0.f;
+                if (own[j]) mx[(l - 1) / 2] = fmaxf(mx[(l - 1) / 2], ch);
+            }
+#pragma unroll
+            for (int j = 0; j < kPRW; ++j) {
+                A[j] = B[j];
+                S[wb][kPRW * w + j][lane] = B[j];
+            }
+            lds_barrier_p();
+        }
+    };
+
+    // wave 0: every tile's maxima of block kb (issued early, folded late)
+    unsigned long long mg[NI][MT];
+    auto issue_maxima = [&](int kb) {
+        const unsigned long long *Mk = a.M + (size_t)(kb % kPMSlots) * NI * a.ntiles;
+#pragma unroll
+        for (int q = 0; q < NI; ++q)
+#pragma unroll
+            for (int r = 0; r < MT; ++r) {
+                const int t = lane + 64 * r;
+                mg[q][r] = t < a.ntiles ? gload(Mk + (size_t)q * a.ntiles + t) : 0ull;
+            }
+    };
+    // first iteration of block kb (m iterations) whose global max < tol, else -1
+    auto fold_maxima = [&](int kb, int m) {
+        const unsigned long long *Mk = a.M + (size_t)(kb % kPMSlots) * NI * a.ntiles;
+        const unsigned want = (unsigned)(kb + 1);
+        while (true) {
+            bool more = false;
+#pragma unroll
+            for (int q = 0; q < NI; ++q)
+#pragma unroll
+                for (int r = 0; r < MT; ++r) {
+                    const int t = lane + 64 * r;
+                    if (q < m && t < a.ntiles && gtag(mg[q][r]) != want) {
+                        mg[q][r] = gload(Mk + (size_t)q * a.ntiles + t);
+                        more = more || gtag(mg[q][r]) != want;
+                    }
+                }
+            if (!__any(more) || expired()) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        int hit = -1;
+#pragma unroll
+        for (int q = NI - 1; q >= 0; --q) {
+            float v = 0.f;
+#pragma unroll
+            for (int r = 0; r < MT; ++r) v = fmaxf(v, gval(mg[q][r]));
+            v = wave_max(v);
+            if (q < m && v < a.tol) hit = q;
+        }
+        return hit < 0 ? -1 : kb * NI + hit;
+    };
+
+    const int nb = (a.niters + NI - 1) / NI;
+    int stop = -1;  // first iteration meeting the tolerance (workgroup-uniform)
+    if (w == 0) sh_stop = -1;
+    for (int k = 0; k < nb; ++k) {
+        const int m = min(NI, a.niters - k * NI);
+        if (k > 0) fetch(k, false);
+        if (check && k >= 2 && w == 0) issue_maxima(k - 2);
+        levels(m);
+        if (check) {
+#pragma unroll
+            for (int q = 0; q < NI; ++q) {
+                const float v = wave_max(mx[q]);
+                if (lane == 0) red[q][w] = v;
+            }
+            if (k >= 2 && w == 0) {
+                const int n = fold_maxima(k - 2, NI);
+                if (lane == 0) sh_stop = n;
+            }
+            lds_barrier_p();  // red and sh_stop visible
+            stop = sh_stop;
+            if (stop >= 0) break;
+            if (threadIdx.x < NI && (int)threadIdx.x < m) {
+                const int q = threadIdx.x;
+                float b = red[q][0];
+#pragma unroll
+                for (int v = 1; v < kPW; ++v) b = fmaxf(b, red[q][v]);
+                gstore(a.M + ((size_t)(k % kPMSlots) * NI + q) * a.ntiles + bid, b, (unsigned)(k + 1));
+            }
+        }
+        if (k + 1 < nb || check) {  // the last block's granules are read only by a rollback
+#pragma unroll
+            for (int j = 0; j < kPRW; ++j)
+                if (own[j]) gstore(a.G + (size_t)(k % kPGSlots) * plane + off[j], A[j], (unsigned)(k + 1));
+        }
+    }
+    if (check && stop < 0) {
+        // the blocks no in-loop check covered
+        for (int kb = max(0, nb - 2); kb < nb && stop < 0; ++kb) {
+            if (w == 0) {
+                issue_maxima(kb);
+                const int n = fold_maxima(kb, min(NI, a.niters - kb * NI));
+                if (lane == 0) sh_stop = n;
+            }
+            lds_barrier_p();
+            stop = sh_stop;
+            lds_barrier_p();  // every wave has read sh_stop before wave 0 may rewrite it
+        }
+    }
+    if (stop >= 0) {
+        // re-run block B from its input for the iterations up to the stop
+        const int B = stop / NI, need = stop - B * NI + 1;
+        if (B == 0) {
+#pragma unroll
+            for (int j = 0; j < kPRW; ++j)
+                if (inner[j]) A[j] = a.in[off[j]];
+        } else {
+            fetch(B, true);
+        }
+        levels(need);
+    }
+#pragma unroll
+    for (int j = 0; j < kPRW; ++j)
+        if (own[j]) a.out[off[j]] = A[j];
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ws->flags[1] = stop >= 0 ? stop + 1 : a.niters;
+    if (broken) atomicOr(&a.ws->flags[3], 1);
+}
+
+// phi <- out (the solve's result), and the count (or -1 after an expired poll)
+__global__ void rbgs_persist_finish(const RbgsWs *__restrict__ ws, float *__restrict__ phi,
+                                    const float *__restrict__ src, size_t n, int *iters_done) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t n4 = n / 4;
+    for (size_t k = t0; k < n4; k += stride)
+        reinterpret_cast<float4 *>(phi)[k] = reinterpret_cast<const float4 *>(src)[k];
+    for (size_t k = 4 * n4 + t0; k < n; k += stride) phi[k] = src[k];
+    if (t0 == 0 && iters_done) *iters_done = ws->flags[3] ? -1 : ws->flags[1];
+}
+
+int tiles_for(int NI, int ny, int nx, int *nseg) {
+    const int L = 2 * NI, OUT = kPT0 - 2 * L, SOUT = 64 - 2 * L;
+    *nseg = ceil_div(nx, SOUT);
+    return *nseg * ceil_div(ny - 2, OUT);
+}
+
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// workgroups of rbgs2d_persist<MASK, NI> the chip holds at once (-1: query failed)
+template <bool MASK, int NI>
+int resident_tiles() {
+    static int resident = 0;
+    if (resident == 0) {
+        int dev = 0, per_cu = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rbgs2d_persist<MASK, NI>, 1024, 0) != hipSuccess)
+            return -1;
+        resident = per_cu * cus;
+    }
+    return resident;
+}
+
+}  // namespace
+
+size_t rbgs2d_persist_extra_bytes(int ny, int nx) {
+    int nseg;
+    const int nt = tiles_for(kPMaxNI, ny, nx, &nseg);  // the most tiles of any NI
+    return align256(sizeof(unsigned long long) * kPGSlots * (size_t)ny * nx) +
+           sizeof(unsigned long long) * kPMSlots * kPMaxNI * (size_t)nt + 256;
+}
+
+int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int ny, int nx, float cx,
+                         float cy, float cd, float dt_inv, float tol, float *phi_tmp, RbgsWs *ws,
+                         size_t ws_bytes, int iterations, int *iters_done, hipStream_t s, int *rc) {
+    *rc = CFD_OK;
+    const int NI = tuning().gs_ni;
+    if (!tuning().gs_persist || !tuning().gs_wg || !phi_tmp || iterations < 1 || ny < 3 || nx < 3) return 0;
+    const size_t base = align256(rbgs_base_bytes(iterations));
+    if (ws_bytes < base + rbgs2d_persist_extra_bytes(ny, nx)) return 0;
+    PersistArgs a;
+    a.in = phi;
+    a.out = phi_tmp;
+    a.div = div;
+    a.mask = mask;
+    a.ws = ws;
+    a.ny = ny;
+    a.nx = nx;
+    a.ntiles = tiles_for(NI, ny, nx, &a.nseg);
+    a.niters = iterations;
+    a.cx = cx;
+    a.cy = cy;
+    a.cd = cd;
+    a.dt_inv = dt_inv;
+    a.tol = tol;
+    char *p = reinterpret_cast<char *>(ws) + base;
+    a.G = reinterpret_cast<unsigned long long *>(p);
+    const size_t gbytes = align256(sizeof(unsigned long long) * kPGSlots * (size_t)ny * nx);
+    a.M = reinterpret_cast<unsigned long long *>(p + gbytes);
+    const size_t mbytes = sizeof(unsigned long long) * kPMSlots * NI * (size_t)a.ntiles;
+    // every tile must be resident at once (they wait on each other)
+    int resident = 0;
+#define CFD_PERS_N(F)                                         \
+    switch (NI) {                                             \
+        case 4: F(4); break;                                  \
+        case 3: F(3); break;                                  \
+        case 2: F(2); break;                                  \
+        default: F(1); break;                                 \
+    }
+#define CFD_RES(N_) resident = mask ? resident_tiles<true, N_>() : resident_tiles<false, N_>()
+    CFD_PERS_N(CFD_RES)
+#undef CFD_RES
+    if (resident < 0) {
+        *rc = CFD_E_HIP;
+        set_error("rbgs2d persistent: occupancy query failed");
+        return 1;
+    }
+    if (a.ntiles > resident || a.ntiles > kPMaxTiles) return 0;  // the launch-per-block path
+    // a stale granule of an earlier solve carries a valid-looking tag: reset the rings
+    if (hipMemsetAsync(p, 0, gbytes + mbytes, s) != hipSuccess) {
+        *rc = CFD_E_HIP;
+        set_error("rbgs2d persistent: ring reset failed");
+        return 1;
+    }
+#define CFD_LAUNCH(N_)                                                                                     \
+    do {                                                                                                   \
+        if (mask) hipLaunchKernelGGL((rbgs2d_persist<true, N_>), dim3(a.ntiles), dim3(1024), 0, s, a);      \
+        else hipLaunchKernelGGL((rbgs2d_persist<false, N_>), dim3(a.ntiles), dim3(1024), 0, s, a);          \
+    } while (0)
+    CFD_PERS_N(CFD_LAUNCH)
+#undef CFD_LAUNCH
+#undef CFD_PERS_N
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *rc = CFD_E_HIP;
+        set_error("rbgs2d persistent launch failed: %s", hipGetErrorString(e));
+        return 1;
+    }
+    const size_t n = (size_t)ny * nx;
+    hipLaunchKernelGGL(rbgs_persist_finish, dim3(ceil_div((long)(n / 4 + 1), 256)), dim3(256), 0, s, ws, phi,
+                       phi_tmp, n, iters_done);
+    const hipError_t e2 = hipGetLastError();
+    if (e2 != hipSuccess) {
+        *rc = CFD_E_HIP;
+        set_error("rbgs2d persistent finish failed: %s", hipGetErrorString(e2));
+    }
+    return 1;
+}
+
+}  // namespace cfd

@@ -163,7 +163,10 @@ def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iteratio
     ny, nx = _shape2d(phi)
     m = _mask_u8(mask, phi.shape)
     ws = workspace
-    need = int(lib().cfd_rbgs_workspace_bytes(int(iterations)))
+    # the grid-sized workspace (small grids: the persistent solve's exchange
+    # rings, cfd_rbgs2d_workspace_bytes) when float32, the base one otherwise
+    need = int(lib().cfd_rbgs2d_workspace_bytes(ny, nx, int(iterations)) if phi.dtype == torch.float32
+               else lib().cfd_rbgs_workspace_bytes(int(iterations)))
     if ws is None or ws.numel() * ws.element_size() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
     _like(phi, div_u_star, "div_u_star")
@@ -172,9 +175,9 @@ def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iteratio
              float(np.float32(dt)), int(iterations), float(tolerance), ptr(ws), ptr(iters_done), stream_handle())
         return phi
     tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
-    call("cfd_rbgs2d_f32", ptr(_f32(phi, "phi")), ptr(_f32(div_u_star, "div_u_star")), ptr(m), ny, nx,
+    call("cfd_rbgs2d_f32_ws", ptr(_f32(phi, "phi")), ptr(_f32(div_u_star, "div_u_star")), ptr(m), ny, nx,
          float(dx), float(dy), float(np.float32(dt)), int(iterations), float(tolerance), ptr(_f32(tmp, "phi_tmp")),
-         ptr(ws), ptr(iters_done), stream_handle())
+         ptr(ws), ws.numel() * ws.element_size(), ptr(iters_done), stream_handle())
     return phi
 
 

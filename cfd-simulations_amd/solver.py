@@ -182,7 +182,8 @@ class OptimizedTurbulentSolver:
         self.u_star, self.v_star, self.div_u_star, self.phi = z(), z(), z(), z()
         self._phi_tmp = z()
         self._rhs_ws = z()
-        self._gs_ws = torch.empty(int(lib().cfd_rbgs_workspace_bytes(cfg.pressure_iterations)),
+        # the GS workspace (small float32 grids: with the persistent solve's rings)
+        self._gs_ws = torch.empty(int(lib().cfd_rbgs2d_workspace_bytes(cfg.ny, cfg.nx, cfg.pressure_iterations)),
                                   dtype=torch.uint8, device=self.device)
         self._gs_done = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._clean_ws = torch.empty(int(lib().cfd_clean_divergence_workspace_bytes(cfg.ny, cfg.nx)),

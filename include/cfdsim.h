@@ -80,10 +80,11 @@ int cfd_set_jacobi2d_blocking(int steps);
 /* 2-D Jacobi sweeps per blocked pass: the set depth, or the large-grid auto
  * depth (8). */
 int cfd_get_jacobi2d_levels(void);
-/* Blocked 2-D passes at 4, 6 or 8 sweeps without a mask stage their rows
- * through a per-wave LDS ring filled by LDS-DMA this many rows ahead (4 or 6,
- * the default 6); 0 = the register march that prefetches one row ahead.  Same
- * bits either way (a tuning knob, per host thread like the others). */
+/* Blocked 2-D passes at 4, 6 or 8 sweeps without a mask may stage their rows
+ * through a per-wave LDS ring filled by LDS-DMA this many rows ahead (4 or 6);
+ * 0 = the register march that prefetches one row ahead (the default: it is
+ * the faster of the two on MI355X).  Same bits either way (a tuning knob, per
+ * host thread like the others). */
 int cfd_set_jacobi2d_staging(int rows_ahead);
 int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
@@ -122,6 +123,19 @@ size_t cfd_rbgs_workspace_bytes(int iterations);
 int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, int nx,
                    double dx, double dy, float dt, int iterations, double tolerance,
                    float *phi_tmp, void *ws, int *iters_done, void *stream);
+/* The same solve with the workspace's size given.  On small grids (the v5
+ * cylinder's 600 x 180) a workspace of cfd_rbgs2d_workspace_bytes(ny, nx,
+ * iterations) bytes (with phi_tmp given) lets the whole solve run as ONE
+ * persistent launch whose tiles hand their edge cells to each other through
+ * the workspace instead of ending a launch every 4 iterations (same bits);
+ * a smaller one (>= cfd_rbgs_workspace_bytes(iterations)) takes the
+ * launch-per-block path, as cfd_rbgs2d_f32 does.  *iters_done is -1 if a
+ * persistent solve's tiles could not all run at once (another kernel held the
+ * CUs for 20 s); phi is then garbage. */
+size_t cfd_rbgs2d_workspace_bytes(int ny, int nx, int iterations);
+int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny, int nx,
+                      double dx, double dy, float dt, int iterations, double tolerance,
+                      float *phi_tmp, void *ws, size_t ws_bytes, int *iters_done, void *stream);
 /* 3-D red-black generalisation: colour c updates (z+i+j) parity == (1+c)%2.
  * The fused 3-D path runs cfd_get_rbgs3d_levels() half-sweeps per HBM pass
  * (default 4: two iterations; cfd_set_jacobi3d_blocking(2..4, ...) sets it),
@@ -398,6 +412,11 @@ int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec
  * shared_rows: 1 = each wave recomputes its halo rows (rbgs2d_small), 2 = the
  * rows of a 16-wave workgroup are shared through LDS (rbgs2d_wg), 0 = default. */
 int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows);
+/* Small-grid GS as one persistent launch (cfd_rbgs2d_f32_ws with a workspace
+ * of cfd_rbgs2d_workspace_bytes): 0 = default (on), 1 = off (one launch per
+ * block of iterations), 2 = on.  Its blocks are the shared-row tile's
+ * (iterations per block as cfd_set_small2d_gs_iters). */
+int cfd_set_small2d_gs_persistent(int mode);
 /* Select the 3-D Jacobi kernel variant (bench / tile sweep):
  * variant 0 = auto, 1 = LDS plane tile, 2 = cache (no LDS); waves = rows per
  * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */

@@ -97,7 +97,7 @@ def test_jacobi2d_staged_rows_bitexact(dtype, shape, iters, pre, blocking, stagi
                                 rhs_ws=torch.empty_like(phi) if pre else None)
         assert np.array_equal(host(phi), ref)
     finally:
-        call("cfd_set_jacobi2d_staging", 6)
+        call("cfd_set_jacobi2d_staging", 0)
         call("cfd_set_jacobi2d_blocking", 0)
 
 

@@ -272,14 +272,17 @@ def test_rbgs2d_small_shapes_bitexact(shape, iters, tol):
     assert np.array_equal(host(phi), ref)
 
 
+@pytest.mark.parametrize("persistent", [1, 2])
 @pytest.mark.parametrize("ni", [2, 3, 4])
 @pytest.mark.parametrize("iters,tol", [(37, 0.0), (400, 3e-5), (401, 1.5e-5)])
-def test_rbgs2d_shared_rows_cylinder_grid(ni, iters, tol):
-    """The shared-row small-grid GS (rbgs2d_wg, the default) with 2..4
-    iterations per launch on the v5 cylinder's grid shape: several tiles in
-    x and y, solid cells, counts not a multiple of the launch depth, early
-    stops of both parities."""
+def test_rbgs2d_shared_rows_cylinder_grid(ni, iters, tol, persistent):
+    """The shared-row small-grid GS with 2..4 iterations per block on the v5
+    cylinder's grid shape, one launch per block (rbgs2d_wg, persistent = 1)
+    or the whole solve as one persistent launch (rbgs2d_persist, 2, the
+    default): several tiles in x and y, solid cells, counts not a multiple of
+    the block depth, early stops of both parities."""
     call("cfd_set_small2d_gs_iters", ni, 2)
+    call("cfd_set_small2d_gs_persistent", persistent)
     rng = np.random.default_rng(31 + ni)
     div = rng.standard_normal((180, 600)).astype(np.float32) * np.float32(1e-3)
     mask = rng.random(div.shape) < 0.03
@@ -421,6 +424,79 @@ def test_rbgs3d_stop_at_every_iteration(levels):
             assert np.array_equal(host(phi), ref), (c, N)
             seen.add(n_ref)
     assert len(seen) >= 10, seen
+
+
+@pytest.mark.parametrize("ni", [1, 2, 3, 4])
+@pytest.mark.parametrize("masked", [True, False])
+def test_rbgs2d_persistent_stop_at_every_iteration(ni, masked):
+    """The persistent small-grid GS (one launch, tiles handing their edge
+    cells to each other): a stop at every iteration 1..N of solves of N = 22
+    and 23 iterations on a grid of 3 x 4 .. 5 x 7 tiles.  A stop is seen two
+    blocks late (or after the loop, for the last two blocks) and the block it
+    fell in is re-run from its input granules; the count and every value must
+    be the oracle's.  Then the same solve with tol = 0 and a stop-free tol."""
+    call("cfd_set_small2d_gs_iters", ni, 2)
+    call("cfd_set_small2d_gs_persistent", 2)
+    rng = np.random.default_rng(70 + ni)
+    div = rng.standard_normal((75, 170)).astype(np.float32) * np.float32(1e-2)
+    mask = (rng.random(div.shape) < 0.05) if masked else None
+    kw = dict(dx=0.1, dy=0.1, dt=np.float32(1.0), mask=mask)
+    _, _, mc = oracle.rbgs2d_maxc(div, iters=23, tol=0.0, **kw)
+    d = dev(div)
+    m = None if mask is None else dev(mask)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    seen = set()
+    for c in range(1, 24):
+        lo = mc[c - 1]
+        hi = mc[:c - 1].min() if c > 1 else np.float32(np.inf)
+        if not lo < hi:
+            continue
+        tol = float(lo) * 1.0000005 if not np.isfinite(hi) else float((np.float64(lo) + np.float64(hi)) / 2)
+        if not (lo < np.float32(tol) <= hi):
+            continue
+        for N in (22, 23):
+            ref, n_ref = oracle.rbgs2d(div, iters=N, tol=tol, **kw)
+            phi = torch.zeros_like(d)
+            K.solve_pressure_gauss_seidel_fast(phi, d, 0.1, 0.1, np.float32(1.0), m, N, tol, iters_done=done)
+            assert int(host(done)[0]) == n_ref, (c, N)
+            assert np.array_equal(host(phi), ref), (c, N)
+            seen.add(n_ref)
+    assert len(seen) >= 8, seen
+    for tol in (0.0, 1e-30):
+        for N in (1, 2, 5, 23):
+            ref, n_ref = oracle.rbgs2d(div, iters=N, tol=tol, **kw)
+            phi = torch.zeros_like(d)
+            K.solve_pressure_gauss_seidel_fast(phi, d, 0.1, 0.1, np.float32(1.0), m, N, tol, iters_done=done)
+            assert int(host(done)[0]) == n_ref == N, (tol, N)
+            assert np.array_equal(host(phi), ref), (tol, N)
+
+
+def test_rbgs2d_persistent_repeated_solves_reuse_workspace():
+    """Back-to-back persistent solves on one workspace (the time-step loop's
+    pattern): a stale granule of the previous solve must never be taken for
+    this one's (the rings are reset per solve); then the C entry without
+    the workspace size (cfd_rbgs2d_f32) on the same workspace, which takes
+    the launch-per-block path: same bits."""
+    rng = np.random.default_rng(99)
+    shape = (180, 600)
+    ws = torch.empty(int(lib().cfd_rbgs2d_workspace_bytes(*shape, 50)), dtype=torch.uint8, device=DEV)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for rep in range(3):
+        div = rng.standard_normal(shape).astype(np.float32) * np.float32(1e-3)
+        phi0 = rng.standard_normal(shape).astype(np.float32) * np.float32(1e-4)
+        ref, n_ref = oracle.rbgs2d(div, phi0, dx=0.05, dy=0.05, dt=np.float32(1e-2), iters=50, tol=1e-8)
+        phi = dev(phi0)
+        K.solve_pressure_gauss_seidel_fast(phi, dev(div), 0.05, 0.05, np.float32(1e-2), None, 50, 1e-8,
+                                           workspace=ws, iters_done=done)
+        assert int(host(done)[0]) == n_ref, rep
+        assert np.array_equal(host(phi), ref), rep
+        phi = dev(phi0)
+        tmp = torch.empty_like(phi)
+        dv = dev(div)
+        call("cfd_rbgs2d_f32", ptr(phi), ptr(dv), None, shape[0], shape[1], 0.05, 0.05, float(np.float32(1e-2)),
+             50, 1e-8, ptr(tmp), ptr(ws), ptr(done), stream_handle())
+        assert int(host(done)[0]) == n_ref, rep
+        assert np.array_equal(host(phi), ref), rep
 
 
 @pytest.mark.parametrize("ni", [1, 2, 3, 4])
