@@ -53,6 +53,7 @@ static Tuning process_defaults() {
         t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;
         t.gs_wg = env_int("CFD_GS_SMALL_WG", t.gs_wg) != 0;
         t.gs_persist = env_int("CFD_GS_PERSIST", t.gs_persist) != 0;
+        t.gs_pairs = env_int("CFD_GS_PAIRS", t.gs_pairs) != 0;
         const int ni = env_int("CFD_GS_SMALL_NI", t.gs_ni);
         t.gs_ni = ni >= 1 && ni <= 4 ? ni : t.gs_ni;
         return t;
@@ -130,9 +131,18 @@ int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows) {
     return CFD_OK;
 }
 
+int cfd_set_small2d_gs_trace(void *buf, size_t bytes) {
+    tuning().gs_trace = buf;
+    tuning().gs_trace_bytes = buf ? bytes : 0;
+    return CFD_OK;
+}
+
 int cfd_set_small2d_gs_persistent(int mode) {
-    CFD_REQUIRE(mode >= 0 && mode <= 2, "small-grid GS persistent mode must be 0 (default), 1 (off) or 2 (on)");
-    tuning().gs_persist = mode ? mode == 2 : process_defaults().gs_persist;
+    CFD_REQUIRE(mode >= 0 && mode <= 3,
+                "small-grid GS persistent mode must be 0 (default), 1 (off), 2 (on) or 3 (on, one exchange per level)");
+    const Tuning d = process_defaults();
+    tuning().gs_persist = mode ? mode >= 2 : d.gs_persist;
+    tuning().gs_pairs = mode >= 2 ? mode == 2 : d.gs_pairs;
     return CFD_OK;
 }
 

@@ -71,6 +71,24 @@ __device__ inline double wave_max(double v) {
     for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
     return v;
 }
+// The same max over the wave by DPP (quad perms, row mirrors, row broadcasts
+// 15 / 31, each a VALU modifier of a few cycles) instead of wave_max's six
+// dependent ds_bpermute round trips through the LDS crossbar; every lane gets
+// the result.  fmaxf ignores a NaN operand, as wave_max does.
+template <int CTRL, int ROW_MASK>
+__device__ inline float dpp_max_step(float v) {
+    const int o = __float_as_int(v);
+    return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(o, o, CTRL, ROW_MASK, 0xf, false)));
+}
+__device__ inline float wave_max_dpp(float v) {
+    v = dpp_max_step<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_max_step<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_max_step<0x141, 0xf>(v);  // row_half_mirror
+    v = dpp_max_step<0x140, 0xf>(v);  // row_mirror: every lane holds its row's max
+    v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3: lane 63 has it all
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 __device__ inline void atomic_max_nonneg(float *dst, float v) {
     atomicMax(reinterpret_cast<unsigned int *>(dst), __float_as_uint(v));
 }

@@ -35,6 +35,14 @@ struct Tuning {
     // workspace holds its exchange rings (cfd_rbgs2d_workspace_bytes) and
     // every tile fits on the chip at once; 0 = one launch per gs_ni iterations
     int gs_persist = 1;
+    // persistent GS: one LDS exchange per iteration (each wave also updates
+    // the rows on either side of its two at the colour-0 level) instead of
+    // one per colour level
+    int gs_pairs = 1;
+    // diagnostics: per-block timestamps of the persistent GS (4 per tile and
+    // block, the 100 MHz clock) into this device buffer when it is big enough
+    void *gs_trace = nullptr;
+    size_t gs_trace_bytes = 0;
 };
 Tuning &tuning();
 

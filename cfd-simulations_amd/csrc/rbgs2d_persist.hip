@@ -22,21 +22,30 @@
 // the previous block's slot.  Rows 0 and ny-1 and cells outside the grid never
 // change, so they keep the values loaded at the start.
 //
-// Stop rule (v5.py:224-225): each tile publishes its per-iteration max|change|
-// of own cells as granules (ring of 4 blocks).  At the end of block k, before
-// block k is published, wave 0 folds every tile's maxima of block k - 2 (their
-// loads were issued at the block's start, so their latency hides behind the
-// levels) and the first iteration n whose global max is < tol stops the solve:
+// Stop rule (v5.py:224-225): the solve stops after the first iteration whose
+// max|change| < tol, i.e. the first iteration in which no cell changed by >=
+// tol (a NaN change never raises the reference's max).  So a tile publishes,
+// per block, one granule of flags (bit q: did any own cell change by >= tol in
+// iteration q; ring of 8 blocks; block k's go out at block k + 1's start).  At the end
+// of block k, before block k is published, wave 0 folds every tile's flags of
+// block k - 3 by ballots (their loads were issued at the block's second level,
+// so their latency hides behind the levels; two blocks of slack cover the
+// tiles' skew, ~0.5 block); the first flag-free iteration n stops the solve:
 // every tile then re-runs block B = n / NI from its input (block B - 1's slot,
 // which no tile has overwritten: nobody publishes block k without having ruled
-// out a stop in block k - 2) for the n - B NI + 1 iterations it needs.  The
-// last two blocks are checked after the loop.  With tol <= 0 nothing is
+// out a stop in block k - 3, and the ring holds 4 blocks) for the n - B NI + 1
+// iterations it needs.  The last three blocks are checked after the loop.  With tol <= 0 nothing is
 // published or polled for the stop rule (it can never fire).
 //
-// Ordering of the granule ring (3 slots): a tile publishes block k over block
-// k - 3's granules only after it has consumed its neighbours' block k - 1
-// output, which they published after reading their block k - 2 input, the
-// last read of block k - 3's granules.  Every poll is bounded (20 s of the
+// Ordering of the granule ring (4 slots): a tile publishes block k over block
+// k - 4's granules only after it has consumed its neighbours' block k - 1
+// output, which they published after reading their block k - 2 input, later
+// than the last read of block k - 4's granules (their block k - 3 input, or a
+// rollback of block k - 3, ruled out before block k is published).  The flag
+// ring (8 blocks): block j's flags go out at block j + 1, after this tile
+// ruled out a stop in block j - 2, so every tile has published block j - 2's
+// flags, i.e. is in block j - 1 or later and reads flags of block j - 4 or
+// later.  Every poll is bounded (20 s of the
 // 100 MHz clock from the kernel's start, as the slab sync kernel), so a tile
 // that never arrives (another kernel holding the CUs) ends the solve with a
 // status bit instead of a hang; the launcher also checks that every tile is
@@ -47,8 +56,9 @@ namespace cfd {
 namespace {
 
 constexpr int kPW = 16, kPRW = 2, kPT0 = kPW * kPRW;  // waves, rows per wave, tile rows
-constexpr int kPGSlots = 3;                            // granule planes (block outputs)
-constexpr int kPMSlots = 4;                            // per-block maxima ring
+constexpr int kPLag = 3;                               // the stop test looks kPLag blocks back
+constexpr int kPGSlots = kPLag + 1;                    // granule planes (block outputs)
+constexpr int kPMSlots = 8;                            // per-block flag ring (>= kPLag + 2)
 constexpr int kPMaxTiles = 256;                        // one tile per CU at most
 constexpr int kPMaxNI = 4;
 constexpr unsigned long long kPSpinLimit = 2000000000ull;  // 20 s at 100 MHz
@@ -59,8 +69,9 @@ struct PersistArgs {
     const float *div;
     const uint8_t *mask;
     unsigned long long *G;  // kPGSlots planes of ny * nx granules
-    unsigned long long *M;  // kPMSlots x NI x ntiles granules
+    unsigned long long *M;  // kPMSlots x ntiles flag granules
     RbgsWs *ws;
+    unsigned long long *trace;  // optional: 4 timestamps per tile and block
     int ny, nx, nseg, ntiles, niters;
     float cx, cy, cd, dt_inv, tol;
 };
@@ -78,13 +89,13 @@ __device__ inline float gval(unsigned long long g) { return __uint_as_float((uns
 // (the compiler's __syncthreads would wait for them too)
 __device__ inline void lds_barrier_p() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <bool MASK, int NI>
+template <bool MASK, int NI, bool PAIRS>
 __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
     constexpr int L = 2 * NI, HL = L, SOUT = 64 - 2 * HL, OUT = kPT0 - 2 * L;
     constexpr int MT = kPMaxTiles / 64;  // maxima granules per lane and iteration (wave 0)
     static_assert(OUT >= 2, "too many levels for the tile");
     __shared__ float S[2][kPT0][64];
-    __shared__ float red[NI][kPW];
+    __shared__ int busy[NI];  // some own cell changed by >= tol in iteration q of the block
     __shared__ int sh_stop;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -123,6 +134,24 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         own[j] = writer && i >= L && i < kPT0 - L && y <= a.ny - 2;
         inner[j] = in_ && !edge;  // cells some tile owns (all others never change)
     }
+    // PAIRS: the rhs and colour masks of the rows just outside the wave's two
+    // (tile rows 2w - 1 and 2w + 2), which the pair schedule updates too
+    float RHh[2] = {0.f, 0.f};
+    bool U0h[2] = {false, false};
+    if (PAIRS) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = kPRW * w + (h ? kPRW : -1), y = ytop + i;
+            const bool in_ = valid && y >= 0 && y <= a.ny - 1 && i >= 0 && i < kPT0;
+            const size_t o = (size_t)min(max(y, 0), a.ny - 1) * a.nx + (valid ? x : 0);
+            const float d = a.div[o];
+            const bool mk = MASK ? a.mask[o] != 0 : false;
+            const bool edge = y <= 0 || y >= a.ny - 1;
+            RHh[h] = -(in_ ? d : 0.f) * a.dt_inv;
+            const bool ok = in_ && !edge && x >= 1 && x < a.nx - 1 && !mk;
+            U0h[h] = ok && ((y + x + 1) & 1) == 0;  // these rows are updated only at colour-0 levels
+        }
+    }
     const size_t plane = (size_t)a.ny * a.nx;
 
     // cells of block k's input (block k-1's granules): the halo cells, or all
@@ -151,114 +180,201 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         }
     };
 
-    // colour levels 1..2m of one block (m = iterations, block-uniform); own
-    // cells' max|change| per iteration into mx
-    float mx[NI];
-    auto levels = [&](int m) {
+    // wave 0: the tile's flags of block kb as one granule (bit q: some own
+    // cell changed by >= tol in iteration q of the block), then cleared
+    auto publish_flags = [&](int kb) {
+        if (lane == 0) {
+            unsigned bits = 0;
 #pragma unroll
-        for (int q = 0; q < NI; ++q) mx[q] = 0.f;
+            for (int q = 0; q < NI; ++q) bits |= busy[q] ? 1u << q : 0u;
+            __hip_atomic_store(a.M + (size_t)(kb % kPMSlots) * a.ntiles + bid,
+                               ((unsigned long long)(kb + 1) << 32) | bits, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane < NI) busy[lane] = 0;
+    };
+    // wave 0: every tile's flag granule of block kb (issued early, folded late)
+    unsigned long long mg[MT];
+    auto issue_maxima = [&](int kb) {
+        const unsigned long long *Mk = a.M + (size_t)(kb % kPMSlots) * a.ntiles;
+#pragma unroll
+        for (int r = 0; r < MT; ++r) {
+            const int t = lane + 64 * r;
+            mg[r] = t < a.ntiles ? gload(Mk + t) : 0ull;
+        }
+    };
+    // first iteration of block kb (m iterations) in which no tile was hot, else -1
+    auto fold_maxima = [&](int kb, int m) {
+        const unsigned long long *Mk = a.M + (size_t)(kb % kPMSlots) * a.ntiles;
+        const unsigned want = (unsigned)(kb + 1);
+        while (true) {
+            bool late[MT], more = false;
+#pragma unroll
+            for (int r = 0; r < MT; ++r) {
+                late[r] = lane + 64 * r < a.ntiles && gtag(mg[r]) != want;
+                more = more || late[r];
+            }
+            if (!__any(more) || expired()) break;
+            __builtin_amdgcn_s_sleep(1);
+            // re-issue every late granule before waiting for any of them
+#pragma unroll
+            for (int r = 0; r < MT; ++r)
+                if (late[r]) mg[r] = gload(Mk + lane + 64 * r);
+        }
+        unsigned bits = 0;
+#pragma unroll
+        for (int r = 0; r < MT; ++r) bits |= (unsigned)mg[r];
+        int hit = -1;
+#pragma unroll
+        for (int q = NI - 1; q >= 0; --q)
+            if (q < m && !__any((bits >> q) & 1u)) hit = q;
+        return hit < 0 ? -1 : kb * NI + hit;
+    };
+
+    // colour levels 1..2m of one block (m = iterations, block-uniform).  The
+    // wave's two rows go through the arithmetic as one packed pair (v_pk_*
+    // f32: the same IEEE operations in the same order per element).  A wave
+    // whose rows are both outside level l's live rows [l, 32 - l) skips the
+    // level (nothing reads them at level l + 1).  Own-row waves note per
+    // iteration whether an own cell changed by >= tol (hot).  Outside a
+    // rollback (k >= 0): wave 0, whose rows die after level 1, publishes the
+    // tile's flags of block k - 1 at the second level and folds every tile's
+    // flags of block k - 3 after the last level (the stop decision, in sh_stop
+    // after the block's last barrier).
+    bool hot[NI];  // per lane: an own cell changed by >= tol (a NaN change never counts, as in v5.py:221)
+    const bool own_rows = kPRW * w + 1 >= L && kPRW * w < kPT0 - L;  // wave-uniform
+    auto levels = [&](int m, int k) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) hot[q] = false;
 #pragma unroll
         for (int j = 0; j < kPRW; ++j) S[0][kPRW * w + j][lane] = A[j];
         lds_barrier_p();
+        if (a.trace && k >= 0 && w == 0 && lane == 0) a.trace[((size_t)k * a.ntiles + bid) * 4 + 2] = wall_clock64();
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const int i0 = kPRW * w;
+        const f2 rh = {RH[0], RH[1]};
+        if (PAIRS) {
+            // one LDS exchange per iteration: each wave reads two rows on
+            // either side, computes the colour-0 level on its rows and the
+            // two around them, then the colour-1 level on its own rows
+            const f2 rhl = {RHh[0], RH[0]}, rhu = {RH[1], RHh[1]};
+#pragma unroll
+            for (int p = 1; p <= NI; ++p) {
+                if (p > m) break;
+                const int l = 2 * p - 1;
+                const int rb = (p - 1) & 1, wb = p & 1;
+                if (p == 1 && check && k >= 1 && w == 0) {
+                    publish_flags(k - 1);
+                    if (k >= kPLag) issue_maxima(k - kPLag);
+                }
+                if (i0 + 1 >= l + 1 && i0 < kPT0 - (l + 1)) {  // wave-uniform: an own row live at l + 1
+                    const float dn2 = i0 >= 2 ? S[rb][i0 - 2][lane] : 0.f;
+                    const float dn1 = i0 >= 1 ? S[rb][i0 - 1][lane] : 0.f;
+                    const float up1 = i0 + 2 < kPT0 ? S[rb][i0 + 2][lane] : 0.f;
+                    const float up2 = i0 + 3 < kPT0 ? S[rb][i0 + 3][lane] : 0.f;
+                    // level l (colour 0): rows i0-1, i0 (pair lo) and i0+1, i0+2 (pair hi)
+                    const f2 cl = {dn1, A[0]}, ch2 = {A[1], up1};
+                    const f2 nl = ((a.cx * (f2{dpp_from_upper(dn1), dpp_from_upper(A[0])} +
+                                            f2{dpp_from_lower(dn1), dpp_from_lower(A[0])}) +
+                                    a.cy * (f2{A[0], A[1]} + f2{dn2, dn1})) - rhl) * a.cd;
+                    const f2 nh = ((a.cx * (f2{dpp_from_upper(A[1]), dpp_from_upper(up1)} +
+                                            f2{dpp_from_lower(A[1]), dpp_from_lower(up1)}) +
+                                    a.cy * (f2{up1, up2} + f2{A[0], A[1]})) - rhu) * a.cd;
+                    const bool ul0 = (i0 - 1 >= l && i0 - 1 < kPT0 - l) && U0h[0];
+                    const bool ul1 = (i0 >= l && i0 < kPT0 - l) && U0[0];
+                    const bool uh0 = (i0 + 1 >= l && i0 + 1 < kPT0 - l) && U0[1];
+                    const bool uh1 = (i0 + 2 >= l && i0 + 2 < kPT0 - l) && U0h[1];
+                    const float q0 = ul0 ? nl[0] : cl[0], q1 = ul1 ? nl[1] : cl[1];
+                    const float q2 = uh0 ? nh[0] : ch2[0], q3 = uh1 ? nh[1] : ch2[1];
+                    if (check && own_rows) {
+                        const f2 dl = nl - cl, dh = nh - ch2;
+                        hot[p - 1] = hot[p - 1] || (own[0] && ul1 && fabsf(dl[1]) >= a.tol) ||
+                                     (own[1] && uh0 && fabsf(dh[0]) >= a.tol);
+                    }
+                    // level l + 1 (colour 1): rows i0, i0 + 1 from q0..q3
+                    const f2 c2 = {q1, q2};
+                    const f2 nv = ((a.cx * (f2{dpp_from_upper(q1), dpp_from_upper(q2)} +
+                                            f2{dpp_from_lower(q1), dpp_from_lower(q2)}) +
+                                    a.cy * (f2{q2, q3} + f2{q0, q1})) - rh) * a.cd;
+                    const bool v0 = (i0 >= l + 1 && i0 < kPT0 - l - 1) && U1[0];
+                    const bool v1 = (i0 + 1 >= l + 1 && i0 + 1 < kPT0 - l - 1) && U1[1];
+                    A[0] = v0 ? nv[0] : c2[0];
+                    A[1] = v1 ? nv[1] : c2[1];
+                    if (check && own_rows) {
+                        const f2 d2 = nv - c2;
+                        hot[p - 1] = hot[p - 1] || (own[0] && v0 && fabsf(d2[0]) >= a.tol) ||
+                                     (own[1] && v1 && fabsf(d2[1]) >= a.tol);
+                    }
+                    S[wb][i0][lane] = A[0];
+                    S[wb][i0 + 1][lane] = A[1];
+                }
+                if (p < m) lds_barrier_p();
+            }
+        } else {
 #pragma unroll
         for (int l = 1; l <= L; ++l) {
             if (l > 2 * m) break;
             const int par = (l - 1) & 1;  // colour of this level
             const int rb = (l - 1) & 1, wb = l & 1;
-            float B[kPRW];
-#pragma unroll
-            for (int j = 0; j < kPRW; ++j) {
-                const int i = kPRW * w + j;
-                const float Nn = j + 1 < kPRW ? A[j + 1] : (i + 1 < kPT0 ? S[rb][i + 1][lane] : 0.f);
-                const float Sv = j > 0 ? A[j - 1] : (i > 0 ? S[rb][i - 1][lane] : 0.f);
-                const float W = dpp_from_lower(A[j]);
-                const float E = dpp_from_upper(A[j]);
-                const bool live = i >= l && i < kPT0 - l;
-                const bool upd = live && (par ? U1[j] : U0[j]);
-                const float nv = ((a.cx * (E + W) + a.cy * (Nn + Sv)) - RH[j]) * a.cd;
-                B[j] = upd ? nv : A[j];
-                const float ch = upd ? fabsf(nv - A[j]) : 0.f;
-                if (own[j]) mx[(l - 1) / 2] = fmaxf(mx[(l - 1) / 2], ch);
+            if (l == 2 && check && k >= 1 && w == 0) {
+                // wave 0 (its rows died after level 1): the tile's flags of
+                // block k - 1, and the loads of every tile's flags of block k - 3
+                publish_flags(k - 1);
+                if (k >= kPLag) issue_maxima(k - kPLag);
             }
+            if (i0 + 1 >= l && i0 < kPT0 - l) {  // wave-uniform: some row live
+                const float up = i0 + 2 < kPT0 ? S[rb][i0 + 2][lane] : 0.f;
+                const float dn = i0 > 0 ? S[rb][i0 - 1][lane] : 0.f;
+                const f2 a2 = {A[0], A[1]};
+                const f2 e2 = {dpp_from_upper(A[0]), dpp_from_upper(A[1])};
+                const f2 w2 = {dpp_from_lower(A[0]), dpp_from_lower(A[1])};
+                const f2 n2 = {A[1], up}, s2 = {dn, A[0]};
+                const f2 nv = ((a.cx * (e2 + w2) + a.cy * (n2 + s2)) - rh) * a.cd;
+                const f2 d2 = nv - a2;
+                float B[kPRW];
 #pragma unroll
-            for (int j = 0; j < kPRW; ++j) {
-                A[j] = B[j];
-                S[wb][kPRW * w + j][lane] = B[j];
-            }
-            lds_barrier_p();
-        }
-    };
-
-    // wave 0: every tile's maxima of block kb (issued early, folded late)
-    unsigned long long mg[NI][MT];
-    auto issue_maxima = [&](int kb) {
-        const unsigned long long *Mk = a.M + (size_t)(kb % kPMSlots) * NI * a.ntiles;
-#pragma unroll
-        for (int q = 0; q < NI; ++q)
-#pragma unroll
-            for (int r = 0; r < MT; ++r) {
-                const int t = lane + 64 * r;
-                mg[q][r] = t < a.ntiles ? gload(Mk + (size_t)q * a.ntiles + t) : 0ull;
-            }
-    };
-    // first iteration of block kb (m iterations) whose global max < tol, else -1
-    auto fold_maxima = [&](int kb, int m) {
-        const unsigned long long *Mk = a.M + (size_t)(kb % kPMSlots) * NI * a.ntiles;
-        const unsigned want = (unsigned)(kb + 1);
-        while (true) {
-            bool more = false;
-#pragma unroll
-            for (int q = 0; q < NI; ++q)
-#pragma unroll
-                for (int r = 0; r < MT; ++r) {
-                    const int t = lane + 64 * r;
-                    if (q < m && t < a.ntiles && gtag(mg[q][r]) != want) {
-                        mg[q][r] = gload(Mk + (size_t)q * a.ntiles + t);
-                        more = more || gtag(mg[q][r]) != want;
-                    }
+                for (int j = 0; j < kPRW; ++j) {
+                    const int i = i0 + j;
+                    const bool live = i >= l && i < kPT0 - l;
+                    const bool upd = live && (par ? U1[j] : U0[j]);
+                    B[j] = upd ? nv[j] : A[j];
+                    if (check && own_rows) hot[(l - 1) / 2] = hot[(l - 1) / 2] || (own[j] && upd && fabsf(d2[j]) >= a.tol);
                 }
-            if (!__any(more) || expired()) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        int hit = -1;
 #pragma unroll
-        for (int q = NI - 1; q >= 0; --q) {
-            float v = 0.f;
-#pragma unroll
-            for (int r = 0; r < MT; ++r) v = fmaxf(v, gval(mg[q][r]));
-            v = wave_max(v);
-            if (q < m && v < a.tol) hit = q;
+                for (int j = 0; j < kPRW; ++j) {
+                    A[j] = B[j];
+                    S[wb][i0 + j][lane] = B[j];
+                }
+            }
+            if (l < 2 * m) lds_barrier_p();
         }
-        return hit < 0 ? -1 : kb * NI + hit;
+        }
+        // the last level's barrier, behind the stop decision
+        if (check && k >= kPLag && w == 0) {
+            const int n = fold_maxima(k - kPLag, NI);
+            if (lane == 0) sh_stop = n;
+        }
+        lds_barrier_p();
+        if (a.trace && k >= 0 && w == 0 && lane == 0) a.trace[((size_t)k * a.ntiles + bid) * 4 + 3] = wall_clock64();
     };
 
     const int nb = (a.niters + NI - 1) / NI;
     int stop = -1;  // first iteration meeting the tolerance (workgroup-uniform)
     if (w == 0) sh_stop = -1;
+    if (w == 0 && lane < NI) busy[lane] = 0;
     for (int k = 0; k < nb; ++k) {
         const int m = min(NI, a.niters - k * NI);
+        if (a.trace && w == 0 && lane == 0) a.trace[((size_t)k * a.ntiles + bid) * 4] = wall_clock64();
         if (k > 0) fetch(k, false);
-        if (check && k >= 2 && w == 0) issue_maxima(k - 2);
-        levels(m);
+        if (a.trace && w == 0 && lane == 0) a.trace[((size_t)k * a.ntiles + bid) * 4 + 1] = wall_clock64();
+        levels(m, k);
         if (check) {
-#pragma unroll
-            for (int q = 0; q < NI; ++q) {
-                const float v = wave_max(mx[q]);
-                if (lane == 0) red[q][w] = v;
-            }
-            if (k >= 2 && w == 0) {
-                const int n = fold_maxima(k - 2, NI);
-                if (lane == 0) sh_stop = n;
-            }
-            lds_barrier_p();  // red and sh_stop visible
             stop = sh_stop;
             if (stop >= 0) break;
-            if (threadIdx.x < NI && (int)threadIdx.x < m) {
-                const int q = threadIdx.x;
-                float b = red[q][0];
+            if (own_rows) {
 #pragma unroll
-                for (int v = 1; v < kPW; ++v) b = fmaxf(b, red[q][v]);
-                gstore(a.M + ((size_t)(k % kPMSlots) * NI + q) * a.ntiles + bid, b, (unsigned)(k + 1));
+                for (int q = 0; q < NI; ++q)
+                    if (__any(hot[q]) && lane == 0) busy[q] = 1;
             }
         }
         if (k + 1 < nb || check) {  // the last block's granules are read only by a rollback
@@ -268,8 +384,10 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         }
     }
     if (check && stop < 0) {
-        // the blocks no in-loop check covered
-        for (int kb = max(0, nb - 2); kb < nb && stop < 0; ++kb) {
+        // the last block's maxima, then the blocks no in-loop check covered
+        lds_barrier_p();
+        if (w == 0) publish_flags(nb - 1);
+        for (int kb = max(0, nb - kPLag); kb < nb && stop < 0; ++kb) {
             if (w == 0) {
                 issue_maxima(kb);
                 const int n = fold_maxima(kb, min(NI, a.niters - kb * NI));
@@ -290,7 +408,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         } else {
             fetch(B, true);
         }
-        levels(need);
+        levels(need, -1);
     }
 #pragma unroll
     for (int j = 0; j < kPRW; ++j)
@@ -319,15 +437,15 @@ int tiles_for(int NI, int ny, int nx, int *nseg) {
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// workgroups of rbgs2d_persist<MASK, NI> the chip holds at once (-1: query failed)
-template <bool MASK, int NI>
+// workgroups of rbgs2d_persist<MASK, NI, PAIRS> the chip holds at once (-1: query failed)
+template <bool MASK, int NI, bool PAIRS>
 int resident_tiles() {
     static int resident = 0;
     if (resident == 0) {
         int dev = 0, per_cu = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rbgs2d_persist<MASK, NI>, 1024, 0) != hipSuccess)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rbgs2d_persist<MASK, NI, PAIRS>, 1024, 0) != hipSuccess)
             return -1;
         resident = per_cu * cus;
     }
@@ -340,7 +458,7 @@ size_t rbgs2d_persist_extra_bytes(int ny, int nx) {
     int nseg;
     const int nt = tiles_for(kPMaxNI, ny, nx, &nseg);  // the most tiles of any NI
     return align256(sizeof(unsigned long long) * kPGSlots * (size_t)ny * nx) +
-           sizeof(unsigned long long) * kPMSlots * kPMaxNI * (size_t)nt + 256;
+           sizeof(unsigned long long) * kPMSlots * (size_t)nt + 256;
 }
 
 int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int ny, int nx, float cx,
@@ -361,6 +479,10 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     a.nx = nx;
     a.ntiles = tiles_for(NI, ny, nx, &a.nseg);
     a.niters = iterations;
+    {
+        const size_t need = 32 * (size_t)a.ntiles * (size_t)((iterations + NI - 1) / NI);
+        a.trace = tuning().gs_trace_bytes >= need ? reinterpret_cast<unsigned long long *>(tuning().gs_trace) : nullptr;
+    }
     a.cx = cx;
     a.cy = cy;
     a.cd = cd;
@@ -370,9 +492,10 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     a.G = reinterpret_cast<unsigned long long *>(p);
     const size_t gbytes = align256(sizeof(unsigned long long) * kPGSlots * (size_t)ny * nx);
     a.M = reinterpret_cast<unsigned long long *>(p + gbytes);
-    const size_t mbytes = sizeof(unsigned long long) * kPMSlots * NI * (size_t)a.ntiles;
+    const size_t mbytes = sizeof(unsigned long long) * kPMSlots * (size_t)a.ntiles;
     // every tile must be resident at once (they wait on each other)
     int resident = 0;
+    const bool pairs = tuning().gs_pairs != 0;
 #define CFD_PERS_N(F)                                         \
     switch (NI) {                                             \
         case 4: F(4); break;                                  \
@@ -380,7 +503,9 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
         case 2: F(2); break;                                  \
         default: F(1); break;                                 \
     }
-#define CFD_RES(N_) resident = mask ? resident_tiles<true, N_>() : resident_tiles<false, N_>()
+#define CFD_RES(N_)                                                                        \
+    resident = pairs ? (mask ? resident_tiles<true, N_, true>() : resident_tiles<false, N_, true>()) \
+                     : (mask ? resident_tiles<true, N_, false>() : resident_tiles<false, N_, false>())
     CFD_PERS_N(CFD_RES)
 #undef CFD_RES
     if (resident < 0) {
@@ -397,8 +522,10 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     }
 #define CFD_LAUNCH(N_)                                                                                     \
     do {                                                                                                   \
-        if (mask) hipLaunchKernelGGL((rbgs2d_persist<true, N_>), dim3(a.ntiles), dim3(1024), 0, s, a);      \
-        else hipLaunchKernelGGL((rbgs2d_persist<false, N_>), dim3(a.ntiles), dim3(1024), 0, s, a);          \
+        if (pairs && mask) hipLaunchKernelGGL((rbgs2d_persist<true, N_, true>), dim3(a.ntiles), dim3(1024), 0, s, a);   \
+        else if (pairs) hipLaunchKernelGGL((rbgs2d_persist<false, N_, true>), dim3(a.ntiles), dim3(1024), 0, s, a);    \
+        else if (mask) hipLaunchKernelGGL((rbgs2d_persist<true, N_, false>), dim3(a.ntiles), dim3(1024), 0, s, a);     \
+        else hipLaunchKernelGGL((rbgs2d_persist<false, N_, false>), dim3(a.ntiles), dim3(1024), 0, s, a);              \
     } while (0)
     CFD_PERS_N(CFD_LAUNCH)
 #undef CFD_LAUNCH

@@ -414,9 +414,15 @@ int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec
 int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows);
 /* Small-grid GS as one persistent launch (cfd_rbgs2d_f32_ws with a workspace
  * of cfd_rbgs2d_workspace_bytes): 0 = default (on), 1 = off (one launch per
- * block of iterations), 2 = on.  Its blocks are the shared-row tile's
- * (iterations per block as cfd_set_small2d_gs_iters). */
+ * block of iterations), 2 = on (one LDS exchange per iteration inside a
+ * tile), 3 = on with one exchange per colour level.  Its blocks are the
+ * shared-row tile's (iterations per block as cfd_set_small2d_gs_iters). */
 int cfd_set_small2d_gs_persistent(int mode);
+/* Diagnostics: the persistent GS writes 4 timestamps (100 MHz device clock)
+ * per tile and block into buf -- block start, halo received, tile ready,
+ * levels done; layout [block][tile][4] u64 -- when bytes covers the solve
+ * (NULL: off, the default). */
+int cfd_set_small2d_gs_trace(void *buf, size_t bytes);
 /* Select the 3-D Jacobi kernel variant (bench / tile sweep):
  * variant 0 = auto, 1 = LDS plane tile, 2 = cache (no LDS); waves = rows per
  * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */

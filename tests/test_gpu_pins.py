@@ -272,7 +272,7 @@ def test_rbgs2d_small_shapes_bitexact(shape, iters, tol):
     assert np.array_equal(host(phi), ref)
 
 
-@pytest.mark.parametrize("persistent", [1, 2])
+@pytest.mark.parametrize("persistent", [1, 2, 3])
 @pytest.mark.parametrize("ni", [2, 3, 4])
 @pytest.mark.parametrize("iters,tol", [(37, 0.0), (400, 3e-5), (401, 1.5e-5)])
 def test_rbgs2d_shared_rows_cylinder_grid(ni, iters, tol, persistent):
@@ -426,9 +426,10 @@ def test_rbgs3d_stop_at_every_iteration(levels):
     assert len(seen) >= 10, seen
 
 
+@pytest.mark.parametrize("mode", [2, 3])
 @pytest.mark.parametrize("ni", [1, 2, 3, 4])
 @pytest.mark.parametrize("masked", [True, False])
-def test_rbgs2d_persistent_stop_at_every_iteration(ni, masked):
+def test_rbgs2d_persistent_stop_at_every_iteration(ni, masked, mode):
     """The persistent small-grid GS (one launch, tiles handing their edge
     cells to each other): a stop at every iteration 1..N of solves of N = 22
     and 23 iterations on a grid of 3 x 4 .. 5 x 7 tiles.  A stop is seen two
@@ -436,7 +437,7 @@ def test_rbgs2d_persistent_stop_at_every_iteration(ni, masked):
     fell in is re-run from its input granules; the count and every value must
     be the oracle's.  Then the same solve with tol = 0 and a stop-free tol."""
     call("cfd_set_small2d_gs_iters", ni, 2)
-    call("cfd_set_small2d_gs_persistent", 2)
+    call("cfd_set_small2d_gs_persistent", mode)
     rng = np.random.default_rng(70 + ni)
     div = rng.standard_normal((75, 170)).astype(np.float32) * np.float32(1e-2)
     mask = (rng.random(div.shape) < 0.05) if masked else None
