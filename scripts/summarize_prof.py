@@ -23,6 +23,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     m = re.match(r"(?:void )?([\w:]+)(<[^()]*>)?", name)
     if not m:
         return name[:80]
