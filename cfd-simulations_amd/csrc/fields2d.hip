@@ -439,6 +439,182 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
         }
     }
 }
+// The same sweep in 16-step chunks whose inner loop runs from registers.
+//  * A lane's old values for a chunk -- 16 consecutive columns of its own row
+//    (E) and of div -- travel memory -> LDS by LDS-DMA (buffer_load_dwordx4
+//    ... lds), R - 1 chunks ahead, into a per-wave ring; at the chunk's start
+//    the lane reads its 16 + 16 values into registers (8 ds_read_b128).  The
+//    windows are skewed per lane by its row, so step k of a chunk is register
+//    k in every lane (compile-time indices).
+//  * In a wave, S is lane t-1's previous output and N lane t+1's E, each ONE
+//    DPP move whose `old` operand supplies the wave-edge lane's value: thread
+//    0's row above and lane 63's row below, read from LDS copies of those rows
+//    (taken at the band's start; the row below is still old then) at uniform
+//    addresses.  A lane past the band's last row loads E from the boundary
+//    row ny-1, which makes the last row's N a DPP too.
+//  * Wave k runs one chunk behind wave k-1 and takes its row above from wave
+//    k-1's lane-63 outputs in a 4-chunk LDS ring; one barrier per chunk.
+//  * Every memory operation of the loop is inline asm (8 DMAs, 4 x4 stores,
+//    and at row ends 16 single-word stores), so the wait for a chunk's DMAs is
+//    an exact vmcnt that leaves the later chunks' DMAs in flight.
+// ~13 VALU per step (the LDS-DMA kernel above: ~40).  Up to 256 rows per band.
+constexpr int kLexC = 16;                     // steps per chunk
+constexpr int kLexR = 4;                      // chunks in the DMA ring
+constexpr int kLexPadL = 16, kLexPadR = 32;   // LDS row copy padding (floats)
+constexpr size_t kLexRegLdsMax = 160 * 1024;  // LDS the register sweep may take
+size_t lex_reg_lds_bytes(int nwaves, int nx) {
+    return (size_t)kLexR * 2 * 4 * 64 * nwaves * sizeof(float4) +
+           (size_t)(nwaves + 1) * (size_t)(nx + kLexPadL + kLexPadR) * sizeof(float);
+}
+__global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ phi,
+                                                         const float *__restrict__ div, int ny, int nx,
+                                                         float cx, float cy, float cd) {
+    __shared__ __attribute__((aligned(16))) float below[4][4 * kLexC];  // wave w's lane-63 outputs by band step
+    // [kLexR][2 fields][4 quads][nt lanes] float4, then (waves + 1) row copies:
+    // [0] the row above the band, [1 + w] the row below wave w's lanes
+    extern __shared__ float4 lex_ring[];
+    const int t = threadIdx.x, nt = blockDim.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int n = ny * nx;
+    const int rs = nx + kLexPadL + kLexPadR;  // LDS row stride
+    float *rows = reinterpret_cast<float *>(lex_ring + (size_t)kLexR * 8 * nt);
+    const v4i32 rp = buf_rsrc4(phi, (uint32_t)(n * 4)), rd = buf_rsrc4(div, (uint32_t)(n * 4));
+    const int imax = ny - 2, jmax = nx - 2;
+    const uint32_t la = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(lex_ring + wv * 64));
+    const uint32_t qstride = (uint32_t)nt * 16u;  // bytes per (slot, field, quad) row
+    for (int b0 = 1; b0 <= imax; b0 += nt) {
+        __threadfence();  // the previous band's rows are final and visible
+        __syncthreads();
+        const int nrows = min(nt, imax - b0 + 1);
+        const int nwaves = (nrows + 63) / 64;
+        for (int r = 0; r <= nwaves; ++r) {
+            const int y = r == 0 ? b0 - 1 : min(b0 + 64 * r, ny - 1);
+            for (int x = t; x < rs; x += nt) {
+                const int col = x - kLexPadL;
+                rows[r * rs + x] = col >= 0 && col < nx ? phi[(size_t)y * nx + col] : 0.f;
+            }
+        }
+        const int i = b0 + t;
+        const bool rowok = t < nrows;
+        const int lag = kLexC * wv;
+        const int jb = 1 - lag - t;  // this lane's column at chunk 0, step 0
+        const int rowc = (i <= ny - 1 ? i : 0) * nx;
+        const uint32_t oE = i <= ny - 1 ? (uint32_t)(rowc + jb + 1) * 4u : kOob;
+        const uint32_t oD = rowok ? (uint32_t)(rowc + jb) * 4u : kOob;
+        const uint32_t oW = (uint32_t)(rowc + jb) * 4u;
+        const float w0 = rowok ? phi[rowc] : 0.f;  // phi(i, 0): W of column 1
+        wait_vmcnt<0>();
+        __syncthreads();  // the row copies are in LDS
+        auto issue = [&](int c, int slot) {  // chunk c's windows into ring slot
+            const uint32_t d = 64u * (uint32_t)c;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                lex_dma_x4(rp, oE + d + 16u * q, la + (uint32_t)((slot * 2 + 0) * 4 + q) * qstride);
+                lex_dma_x4(rd, oD + d + 16u * q, la + (uint32_t)((slot * 2 + 1) * 4 + q) * qstride);
+            }
+        };
+        // chunks: up to the last lane's last step in chunk time (wave w runs
+        // band step s at time s + lag), rounded up to whole rounds of kLexR
+        const int nchunks = ((nrows - 2 + jmax + kLexC * (nwaves - 1)) / kLexC + kLexR) / kLexR * kLexR;
+#pragma unroll
+        for (int r = 0; r < kLexR; ++r) {
+            issue(r, r);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) buf_store_x1(0.f, kOob, rp);  // the loop's x4-store slots
+        }
+        float w = w0, vprev = 0.f;
+        const float *above = rows + kLexPadL;                 // row b0 - 1
+        const float *under = rows + (1 + wv) * rs + kLexPadL;  // the row below lane 63
+        for (int c0 = 0; c0 < nchunks; c0 += kLexR) {
+#pragma unroll
+            for (int r = 0; r < kLexR; ++r) {
+                const int c = c0 + r;
+                // this chunk's DMAs: 12 (kLexR - 1) memory ops were issued after them
+                wait_vmcnt<12 * (kLexR - 1)>();
+                float Er[kLexC], Dr[kLexC];
+                const float4 *slot = lex_ring + (size_t)r * 8 * nt + t;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 e = slot[q * nt], d = slot[(4 + q) * nt];
+                    Er[4 * q] = e.x; Er[4 * q + 1] = e.y; Er[4 * q + 2] = e.z; Er[4 * q + 3] = e.w;
+                    Dr[4 * q] = d.x; Dr[4 * q + 1] = d.y; Dr[4 * q + 2] = d.z; Dr[4 * q + 3] = d.w;
+                }
+                // the wave-edge lanes' neighbours (uniform addresses): thread
+                // 0's S (wave 0: the row above; else wave k-1's lane 63 one band
+                // step earlier) and lane 63's N (the row below)
+                float S0[kLexC], N63[kLexC];
+                if (wv == 0) {
+                    const int j0 = min(max(1 + kLexC * c, -kLexPadL), nx);
+#pragma unroll
+                    for (int k = 0; k < kLexC; ++k) S0[k] = above[j0 + k];
+                } else {
+                    const int base = (kLexC * c - lag) & (4 * kLexC - 1);
+                    const float *ab = below[wv - 1];
+                    S0[0] = ab[(base - 1) & (4 * kLexC - 1)];
+#pragma unroll
+                    for (int q = 0; q < kLexC / 4; ++q) {
+                        const float4 v4 = *reinterpret_cast<const float4 *>(ab + base + 4 * q);
+                        if (4 * q + 1 < kLexC) S0[4 * q + 1] = v4.x;
+                        if (4 * q + 2 < kLexC) S0[4 * q + 2] = v4.y;
+                        if (4 * q + 3 < kLexC) S0[4 * q + 3] = v4.z;
+                        if (4 * q + 4 < kLexC) S0[4 * q + 4] = v4.w;
+                    }
+                }
+                {
+                    const int j0 = min(max(1 - lag - (64 * wv + 63) + kLexC * c, -kLexPadL), nx);  // lane 63's column
+#pragma unroll
+                    for (int k = 0; k < kLexC; ++k) N63[k] = under[j0 + k];
+                }
+                const int jc = jb + kLexC * c;
+                float out[kLexC];
+                bool act[kLexC];
+#pragma unroll
+                for (int k = 0; k < kLexC; ++k) {
+                    const float E = Er[k];
+                    const float N = __int_as_float(__builtin_amdgcn_update_dpp(
+                        __float_as_int(N63[k]), __float_as_int(E), 0x130, 0xf, 0xf, false));  // wave_shl:1
+                    const float S = __int_as_float(__builtin_amdgcn_update_dpp(
+                        __float_as_int(S0[k]), __float_as_int(vprev), 0x138, 0xf, 0xf, false));  // wave_shr:1
+                    const float a = cx * (E + w);
+                    const float bb = cy * (N + S);
+                    const float v = ((a + bb) - Dr[k]) * cd;
+                    act[k] = rowok && (uint32_t)(jc + k - 1) < (uint32_t)jmax;
+                    w = act[k] ? v : w;
+                    vprev = v;
+                    out[k] = v;
+                }
+                if (lane == 63) {
+                    float *mine = below[wv] + ((kLexC * c - lag) & (4 * kLexC - 1));
+#pragma unroll
+                    for (int q = 0; q < kLexC / 4; ++q)
+                        *reinterpret_cast<float4 *>(mine + 4 * q) =
+                            make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+                }
+                // results: one 16-byte store per 4 columns all inside the row,
+                // single words where a group is cut by a row end
+                bool partial = false;
+#pragma unroll
+                for (int q = 0; q < kLexC / 4; ++q) {
+                    const bool full = act[4 * q] && act[4 * q + 3];
+                    partial = partial || (!full && (act[4 * q] || act[4 * q + 1] || act[4 * q + 2] || act[4 * q + 3]));
+                    buf_store_x4(make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]),
+                                 full ? oW + 64u * c + 16u * q : kOob, rp);
+                }
+                if (__any(partial)) {
+#pragma unroll
+                    for (int k = 0; k < kLexC; ++k) {
+                        const bool full = act[k & ~3] && act[(k & ~3) + 3];
+                        buf_store_x1(out[k], act[k] && !full ? oW + 64u * c + 4u * k : kOob, rp);
+                    }
+                }
+                issue(c + kLexR, r);
+                lex_lds_barrier();
+            }
+        }
+    }
+}
+
 size_t lex_dma_lds_bytes(int nt, int lx) {
     return (size_t)lx * 4 * nt * sizeof(float4) + (size_t)(nt / 64) * kLexRing * sizeof(float);
 }
@@ -737,6 +913,22 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
             // one thread per row of a band: as many waves as rows (idle
             // waves would only add barrier traffic to every step)
             if (n * 4 < ((size_t)1 << 31)) {
+                // bands of at most 256 rows, one wave per 64 rows, with LDS
+                // copies of (waves + 1) rows
+                const int ntr = ny - 2 >= 256 ? 256 : 64 * ceil_div(ny - 2, 64);
+                const size_t rows_lds = lex_reg_lds_bytes(ntr / 64, nx);
+                if (rows_lds + 1024 <= kLexRegLdsMax && !getenv("CFD_LEX_DMA")) {
+                    static bool attr_reg = false;
+                    if (!attr_reg) {
+                        CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lex_gs_sweep_reg),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                          (int)(kLexRegLdsMax - 1024)));
+                        attr_reg = true;
+                    }
+                    hipLaunchKernelGGL(k_lex_gs_sweep_reg, dim3(1), dim3(ntr), rows_lds, s, phi, div, ny, nx,
+                                       (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
+                    goto swept;
+                }
                 // bands of at most 512 rows (the ring's LDS), one wave per 64 rows
                 static const int band = [] {
                     const char *e = getenv("CFD_LEX_BAND");  // rows per band (A/B knob)
@@ -759,6 +951,7 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
                                    (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
             }
         }
+    swept:
         hipLaunchKernelGGL(k_sub_gradient, grid2d(ny, nx), dim3(256), 0, s, phi, u, v, ny, nx, cx,
                            cy);
         CFD_LAUNCH_CHECK();
@@ -824,6 +1017,11 @@ int cfd_absmax2_f32(const float *a, const float *b, size_t n, float *out, void *
 int cfd_energy_mean2d_f32(const float *u, const float *v, size_t n, double *out, void *stream) {
     CFD_REQUIRE(u && v && out && n > 0, "energy_mean2d: bad arguments");
     hipStream_t s = as_stream(stream);
+    if (n <= kEnergyOneBlock) {
+        hipLaunchKernelGGL(k_energy_mean_1blk<float>, dim3(1), dim3(1024), 0, s, u, v, n, out);
+        CFD_LAUNCH_CHECK();
+        return CFD_OK;
+    }
     CFD_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(double), s));
     hipLaunchKernelGGL(k_energy_sum, dim3(grid1d(n)), dim3(256), 0, s, u, v, n, out);
     hipLaunchKernelGGL(k_scale_double, dim3(1), dim3(1), 0, s, out, 1.0 / (double)n);

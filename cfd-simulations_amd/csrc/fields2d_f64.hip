@@ -612,6 +612,11 @@ int cfd_absmax2_f64(const double *a, const double *b, size_t n, double *out, voi
 int cfd_energy_mean2d_f64(const double *u, const double *v, size_t n, double *out, void *stream) {
     CFD_REQUIRE(u && v && out && n > 0, "energy_mean2d_f64: bad arguments");
     hipStream_t s = as_stream(stream);
+    if (n <= kEnergyOneBlock) {
+        hipLaunchKernelGGL(k_energy_mean_1blk<double>, dim3(1), dim3(1024), 0, s, u, v, n, out);
+        CFD_LAUNCH_CHECK();
+        return CFD_OK;
+    }
     CFD_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(double), s));
     hipLaunchKernelGGL(k_energy_sum64, dim3(grid1d64(n)), dim3(256), 0, s, u, v, n, out);
     hipLaunchKernelGGL(k_scale64, dim3(1), dim3(1), 0, s, out, 1.0 / (double)n);
