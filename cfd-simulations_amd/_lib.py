@@ -77,6 +77,7 @@ PROTOTYPES = {
     "cfd_apply_lid_bc2d_f64": (c_int, [P, P, c_int, c_int, c_double, P]),
     "cfd_apply_ibm2d_f64": (c_int, [P, P, P, c_int, c_double, P]),
     "cfd_clip_f64": (c_int, [P, c_size_t, c_double, c_double, P]),
+    "cfd_numpy_pow_f64": (c_int, [P, c_double, P, c_size_t, P]),
     "cfd_absmax2_f64": (c_int, [P, P, c_size_t, P, P]),
     "cfd_energy_mean2d_f64": (c_int, [P, P, c_size_t, P, P]),
     "cfd_vorticity2d_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_double, P]),

@@ -260,6 +260,9 @@ int cfd_apply_lid_bc2d_f64(double *u, double *v, int ny, int nx, double u_lid, v
 int cfd_apply_ibm2d_f64(double *u, double *v, const double *ibm_mask, int n, double force_strength,
                         void *stream);
 int cfd_clip_f64(double *a, size_t n, double lo, double hi, void *stream);
+/* glibc's double pow elementwise, as NumPy's float64 scalar `**` runs it
+ * (the device restatement the float64 SUPG tau uses): out[i] = x[i] ** y. */
+int cfd_numpy_pow_f64(const double *x, double y, double *out, size_t n, void *stream);
 /* max(|a|, |b|) (b may be NULL) into a zeroed device double */
 int cfd_absmax2_f64(const double *a, const double *b, size_t n, double *out, void *stream);
 int cfd_energy_mean2d_f64(const double *u, const double *v, size_t n, double *out, void *stream);

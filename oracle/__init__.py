@@ -71,6 +71,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_divergence2d_f32.argtypes = [_f32p, _f32p, _f32p, _i, _i, _d, _d]
         L.oracle_gradient2d_f32.argtypes = [_f32p, _f32p, _f32p, _i, _i, _d, _d]
         L.oracle_powf_f32.argtypes = [_f32p, _f, _f32p, ctypes.c_size_t]
+        L.oracle_pow_f64.argtypes = [_f64p, _d, _f64p, ctypes.c_size_t]
         L.oracle_clean_divergence2d_f32.argtypes = [_f32p, _f32p, _i, _i, _d, _d, _i]
         _LIB = L
     return _LIB
@@ -193,6 +194,14 @@ def predictor2d(u, v, nu_eff, *, dx, dy, dt, use_supg=True):
     lib().oracle_predictor2d_f32(u, v, nu, u.shape[0], u.shape[1], float(dx), float(dy), np.float32(dt),
                                  int(bool(use_supg)), out["tau"], out["conv_u"], out["conv_v"],
                                  out["lap_u"], out["lap_v"], out["u_star"], out["v_star"])
+    return out
+
+
+def numpy_pow(x, y):
+    """libm pow elementwise: NumPy's float64 scalar ``x ** y``."""
+    x = np.ascontiguousarray(x, np.float64)
+    out = np.empty_like(x)
+    lib().oracle_pow_f64(x, float(y), out, x.size)
     return out
 
 

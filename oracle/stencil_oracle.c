@@ -354,6 +354,12 @@ void oracle_powf_f32(const float *x, float y, float *out, size_t n) {
     for (size_t k = 0; k < n; ++k) out[k] = powf(x[k], y);
 }
 
+/* libm pow elementwise (NumPy float64 scalar `**`): the checker for the
+ * library's device restatement of glibc pow (cfd_numpy_pow_f64). */
+void oracle_pow_f64(const double *x, double y, double *out, size_t n) {
+    for (size_t k = 0; k < n; ++k) out[k] = pow(x[k], y);
+}
+
 /* ---- a7/a8/a9/a10: predictor, v5.py:112-176 and :388-403 ---------------
  * nu_eff is an (ny,nx) float32 array (nu + nu_t + art_visc, v5.py:388).
  * Writes tau (SUPG only), conv_u/conv_v, lap_u/lap_v and u_star/v_star.

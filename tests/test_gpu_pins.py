@@ -210,6 +210,31 @@ def test_device_powf_is_libm(y):
         assert (ref[-2 * vel.size:-vel.size] != vel * vel).any()  # the case a plain u*u misses
 
 
+@pytest.mark.parametrize("y", [2.0, 0.5])
+def test_device_pow_f64_is_libm(y):
+    """cfd_numpy_pow_f64 (the device glibc pow of the float64 SUPG tau)
+    equals libm pow -- NumPy's float64 scalar `**` -- on random bit patterns,
+    velocity-like values and their squares (where pow(x, 2) != x*x and
+    pow(x, 0.5) != sqrt(x) now and then), subnormals, zeros, infinities, NaN."""
+    rng = np.random.default_rng(int(y * 10) + 7)
+    x = rng.integers(0, 2 ** 63, 1 << 21, dtype=np.uint64).view(np.float64)
+    extra = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 5e-324, 1e-310, 2.2e-308, 1.7e308, 5.0, 0.1])
+    vel = rng.uniform(-5, 5, 1 << 20)
+    x = np.concatenate([x, -x[: x.size // 2], extra, vel, vel * vel])
+    if y == 0.5:
+        x = np.abs(x)
+    ref = oracle.numpy_pow(x, y)
+    out = torch.empty(x.size, dtype=torch.float64, device=DEV)
+    xd = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+    call("cfd_numpy_pow_f64", ptr(xd), float(y), ptr(out), x.size, stream_handle())
+    got = host(out)
+    same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+    assert same.all(), x[~same][:8]
+    naive = vel * vel if y == 2.0 else np.sqrt(np.abs(vel))
+    tail = ref[-2 * vel.size:-vel.size] if y == 2.0 else ref[-2 * vel.size:-vel.size]
+    assert (tail != naive).any()  # the cases a correctly rounded form misses
+
+
 # ------------------------------------------------- 2-D RB-GS, odd tail + stop
 def _stop_at_first_of_last_pair():
     """A small grid and tolerance whose oracle stop falls on iteration s (0-based,

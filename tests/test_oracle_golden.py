@@ -274,3 +274,24 @@ def test_host_setup_f64_matches_reference(golden, branch):
     assert u.dtype == np.float64
     assert np.array_equal(cyl, d["cylinder_mask"]) and np.array_equal(ibm, d["ibm_mask"])
     assert np.array_equal(u, d["u0"]) and np.array_equal(v, d["v0"])
+
+
+def test_libm_pow_restatement(tmp_path):
+    """The device restatement of glibc's double pow (csrc/libm_pow.hpp, the
+    SUPG tau's |V| in float64), compiled for this host, equals libm's pow bit
+    for bit at y = 2 and y = 0.5 on 2M random and edge-case inputs
+    (oracle/pow_check.cpp).  The reference's golden steps were made on an
+    FMA/AVX2 host, whose libm runs glibc's FMA variant of pow: the one restated."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    cpu = Path("/proc/cpuinfo").read_text() if Path("/proc/cpuinfo").exists() else ""
+    if " fma " not in cpu or shutil.which("g++") is None:
+        pytest.skip("needs an FMA host and g++")
+    root = Path(__file__).resolve().parents[1]
+    exe = tmp_path / "pow_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-mfma", "-DCFD_LIBM_HOST",
+                    str(root / "oracle" / "pow_check.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "1000000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout
