@@ -585,8 +585,9 @@ def _gather_uneven(dist, parts, mine, rank):
 
 def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):
     """Config 3: time every tile on this grid: the single-sweep kernel's
-    (variant, waves, zchunk), the 2-level kernel's rows, and the tall-tile
-    kernels' (levels, output rows, zchunk)."""
+    (variant, waves, zchunk) and the tall-tile kernels' (levels, output rows,
+    zchunk); 2 levels is the tall-tile kernel too (the older 2-level kernels
+    are gone from the library)."""
     import torch
     res = []
     call("cfd_set_jacobi3d_blocking", 1, 0, 0)
