@@ -109,6 +109,7 @@ PROTOTYPES = {
     "cfd_set_small2d_gs_iters": (c_int, [c_int, c_int]),
     "cfd_set_small2d_gs_persistent": (c_int, [c_int]),
     "cfd_set_small2d_gs_trace": (c_int, [P, c_size_t]),
+    "cfd_set_tbr_trace": (c_int, [P, c_size_t]),
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_jacobi3d_blocking": (c_int, [c_int, c_int, c_int]),
     "cfd_get_jacobi3d_levels": (c_int, []),

@@ -131,6 +131,12 @@ int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows) {
     return CFD_OK;
 }
 
+int cfd_set_tbr_trace(void *buf, size_t bytes) {
+    CFD_REQUIRE(!buf || bytes >= (size_t)16 * 64 * 5 * 8, "tbr trace buffer: 40 KiB");
+    tuning().tbr_trace = buf;
+    return CFD_OK;
+}
+
 int cfd_set_small2d_gs_trace(void *buf, size_t bytes) {
     tuning().gs_trace = buf;
     tuning().gs_trace_bytes = buf ? bytes : 0;

@@ -43,6 +43,9 @@ struct Tuning {
     // block, the 100 MHz clock) into this device buffer when it is big enough
     void *gs_trace = nullptr;
     size_t gs_trace_bytes = 0;
+    // diagnostics: the tall-tile kernels' per-wave step timestamps (workgroup
+    // 0, 64 steps, 5 marks each, 16 waves' worth: 40 KiB) into this buffer
+    void *tbr_trace = nullptr;
 };
 Tuning &tuning();
 

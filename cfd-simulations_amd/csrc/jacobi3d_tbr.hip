@@ -29,8 +29,22 @@ namespace cfd {
 
 namespace {
 
-__device__ inline float4 ldg4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-__device__ inline void stg4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+// Global (not flat) loads and stores: the halo wave's pointers reach it as
+// generic pointers (TbrArgs by value), and a flat load counts in lgkmcnt as
+// well as vmcnt, so the LDS barrier's lgkmcnt(0) waited for the halo wave's
+// just-issued prefetch -- a full memory latency at the first barrier of every
+// step (r03 per-wave trace, cfd_set_tbr_trace: the halo wave arrived last at
+// it, ~2200 cycles into a 5500-cycle step).
+// (The HIP float4 struct would still load through a generic `this`: native
+// ext vectors in the global address space.)
+typedef float gv4g __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) gv4g *gcv4p;
+typedef __attribute__((address_space(1))) gv4g *gv4p;
+__device__ inline float4 ldg4(const float *p) {
+    const gv4g v = *(gcv4p)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ inline void stg4(float *p, float4 v) { *(gv4p)p = gv4g{v.x, v.y, v.z, v.w}; }
 __device__ inline float4 lds4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
@@ -83,7 +97,29 @@ struct TbrArgs {
     int lag;         // GS: the stop test reads maxc[it-1-lag], maxc[it-2-lag] (see rbgs3d_tbr_pass)
     float *rhs_out;  // first pass (F & kFirstRhs): the rhs of the owned cells goes here
     int xbw;         // XCD block width in x-segments (0: each XCD takes whole tile rows), see tbr_launch
+    unsigned long long *trace;  // diagnostics (cfd_set_tbr_trace): per-wave step timestamps, or NULL
 };
+// Diagnostics (builds with -DCFD_TBR_TRACE only: the marks cost the 4-level
+// kernels registers, 9-33 VGPRs of spill): workgroup 0's waves record the
+// shader clock at 5 points of kTraceSteps z-steps from kTraceStep0 on (step
+// entry, before / after the first barrier, before / after the second) into
+// trace[wave][step][5].  r03 finding, 1024^3, cycles per step: K = 3 Jacobi
+// 5430-5500 = phase W ~2000 (the third wave of each SIMD and the halo wave
+// arrive last at the first barrier) + phase R ~3300 (VALU-bound per SIMD);
+// 4-level GS 6900-7300.
+constexpr int kTraceStep0 = 200, kTraceSteps = 64;
+__device__ inline void trace_mark(unsigned long long *tr, int wave, int step, int e) {
+#ifdef CFD_TBR_TRACE
+    const int k = step - kTraceStep0;
+    if (tr && blockIdx.x == 0 && (threadIdx.x & 63) == 0 && k >= 0 && k < kTraceSteps)
+        tr[((size_t)wave * kTraceSteps + k) * 5 + e] = __builtin_readcyclecounter();
+#else
+    (void)tr;
+    (void)wave;
+    (void)step;
+    (void)e;
+#endif
+}
 // First-pass flags (template F of jacobi3d_tbr, Jacobi on the LDS-DMA path):
 // kFirstRhs: `div` is raw; the row waves form f32(h*h)*div/dt once per cell
 // (the bits k_rhs_f32 and the in-register form give) and store it to rhs_out
@@ -270,7 +306,9 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
         Hq[i] = ldhp(zs + 2 + i);
         Rn[i] = ldh(a.div, zs + 1 + i);
     }
+    const int hw = threadIdx.x >> 6;
     for (int z = zs; z <= zl; ++z) {
+        trace_mark(a.trace, hw, z - zs, 0);
         Lq[PD - 1] = ldlo(z + PD);
         Uq[PD - 1] = ldhi(z + PD);
         Hq[PD - 1] = ldhp(z + 1 + PD);
@@ -296,7 +334,9 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
                     }
                 }
         }
+        trace_mark(a.trace, hw, z - zs, 1);
         __syncthreads();
+        trace_mark(a.trace, hw, z - zs, 2);
         // phase R: levels 1..K-1 of the halo chunks
 #pragma unroll
         for (int l = 1; l < K; ++l) {
@@ -330,7 +370,9 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
                 H[l][2] = v;
             }
         }
+        trace_mark(a.trace, hw, z - zs, 3);
         __syncthreads();
+        trace_mark(a.trace, hw, z - zs, 4);
         lo = Lq[0];
         hi = Uq[0];
         H[0][0] = H[0][1];
@@ -576,6 +618,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 // (zoff + p + y + 1 + h0 + l - 1) with p = z - l + 1 and z = zs + E
                 // is BP ^ E ^ (j * NWR) mod 2 (BP: see march)
                 constexpr int BPv = decltype(bpc)::value;
+                trace_mark(a.trace, wv, z - zs, 0);
                 float *const pw = E ? st_p1 : st_p0;
                 float *const rw = E ? st_r1 : st_r0;
                 const float *const pr = E ? st_p0 : st_p1;
@@ -638,7 +681,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 // the previous step's DMAs have landed once at most this step's
                 // 2 * RPW remain in flight (they are issued in order)
                 wait_vmcnt<((ZERO ? 0 : 1) + 1) * RPW>();
+                trace_mark(a.trace, wv, z - zs, 1);
                 lds_barrier();
+                trace_mark(a.trace, wv, z - zs, 2);
 #pragma unroll
                 for (int j = 0; j < RPW; ++j) {
                     V[j][vs(1)] = ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
@@ -777,7 +822,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                         }
                     }
                 }
+                trace_mark(a.trace, wv, z - zs, 3);
                 lds_barrier();
+                trace_mark(a.trace, wv, z - zs, 4);
                 if constexpr (!ROT) {
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
@@ -1037,6 +1084,7 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
     }
     a.nseg = nseg;
     a.ntile_y = ceil_div(a.ny - 2, best->rows());
+    a.trace = reinterpret_cast<unsigned long long *>(tuning().tbr_trace);
     a.zchunk = best_zlen;
     // CFD_TBR_XBW = w (A/B knob): each XCD takes a block of w x-segments x
     // (its share / w) tile rows instead of whole tile rows, which changes how

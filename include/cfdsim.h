@@ -426,6 +426,12 @@ int cfd_set_small2d_gs_persistent(int mode);
  * levels done; layout [block][tile][4] u64 -- when bytes covers the solve
  * (NULL: off, the default). */
 int cfd_set_small2d_gs_trace(void *buf, size_t bytes);
+/* Diagnostics, in a library built with -DCFD_TBR_TRACE (scripts/build_variant.sh;
+ * a no-op otherwise): the 3-D tall-tile kernels' workgroup 0 records, per wave,
+ * the shader clock at 5 points (step entry, before / after each of the step's
+ * two barriers) of z-steps 200..263 into buf, layout [wave][64][5] u64 (40 KiB,
+ * 16 waves; NULL: off, the default). */
+int cfd_set_tbr_trace(void *buf, size_t bytes);
 /* Select the 3-D Jacobi kernel variant (bench / tile sweep):
  * variant 0 = auto, 1 = LDS plane tile, 2 = cache (no LDS); waves = rows per
  * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */
