@@ -32,6 +32,19 @@ constexpr int gcd_c(int a, int b) { return b ? gcd_c(b, a % b) : a; }
 template <int K>
 constexpr int kTbkUnroll = 3 * K / gcd_c(3, K);
 
+// the pass's output rows with the streaming (nt) store policy: 8192^2 f64,
+// r03: 0.3354 -> 0.3305 ms per pass
+template <typename T, int VEC>
+__device__ inline void st_out(T *p, const T (&r)[VEC]) {
+    if constexpr (VEC > 1) {
+        typename VecOf<T, VEC>::type v;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) v[k] = r[k];
+        __builtin_nontemporal_store(v, reinterpret_cast<typename VecOf<T, VEC>::type *>(p));
+    } else {
+        __builtin_nontemporal_store(r[0], p);
+    }
+}
 template <typename T, int VEC, int K, bool PRE, bool MASK>
 __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T *__restrict__ out,
                                                     const T *__restrict__ div,
@@ -130,7 +143,7 @@ __global__ __launch_bounds__(256) void jacobi2d_tbk(const T *__restrict__ in, T 
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) Q[l][sc][k] = v[k];  // over row p - 3 of level l, dead
             } else if (writer && p >= y0 && p < y1) {
-                st<T, VEC>(out + row(p), v);
+                st_out<T, VEC>(out + row(p), v);
             }
         }
 #pragma unroll
@@ -237,7 +250,7 @@ __global__ __launch_bounds__(256) void jacobi2d_tbd(const T *__restrict__ in, T 
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) Q[l][sc][k] = v[k];
             } else if (writer && p >= y0 && p < y1) {
-                st<T, VEC>(out + row(p), v);
+                st_out<T, VEC>(out + row(p), v);
             }
         }
 #pragma unroll

@@ -58,6 +58,15 @@ __device__ inline __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, int p, in
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(in ? base + (size_t)p * plane : base),
                                              (short)0, in ? (int)(plane * sizeof(float)) : 0, 0x00020000);
 }
+// Cache policy of the passes' HBM stores (buffer-store aux bits): nt, the
+// streaming policy -- 1024^3, r03: K = 3 Jacobi 2.204 -> 2.174 ms per pass,
+// K = 4 2.954 -> 2.894, the 4-level GS 2.752 -> 2.675.  (sc1 and sc0 sc1,
+// which drop the line from L2: K = 4 3.07; nt on the LDS-DMA / buffer loads
+// as well: 2.97 ms at K = 3 -- the neighbouring tiles' halo re-reads then
+// miss L2.)
+constexpr int kStoreNt = 2;
+
+
 __device__ inline float4 ldb4(__amdgpu_buffer_rsrc_t r, uint32_t byte_ofs) {
     const gv4f v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_ofs, 0, 0);
     return make_float4(v.x, v.y, v.z, v.w);
@@ -132,7 +141,7 @@ enum { kFirstRhs = 1, kFirstZero = 2 };
 // Red-black GS: the cells of colour `par` parity (v5.py:213-219 generalised:
 // (((cx(E+W) + cy(N+S)) + cz(U+D)) - rhs) * cd with rhs = -div * dt_inv, the
 // in-place kernel's operation order); `chg` folds max|change| of own cells.
-template <int MODE, bool PRE>
+template <int MODE, bool PRE, bool PK = false>
 __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S, float4 U,
                                 float4 D, float4 d, int x, int nx, bool upd, const TbrArgs &a,
                                 int par, bool own, float &chg) {
@@ -167,28 +176,60 @@ __device__ inline float4 level4(float4 c, float wl, float er, float4 N, float4 S
         }
         return hi ? make_float4(c.x, o.x, c.z, o.y) : make_float4(o.x, c.y, o.y, c.w);
     }
-    const float h2 = a.h2, dt = a.dt;
-    const float cv[4] = {c.x, c.y, c.z, c.w};
-    const float nv[4] = {N.x, N.y, N.z, N.w};
-    const float sv[4] = {S.x, S.y, S.z, S.w};
-    const float uv[4] = {U.x, U.y, U.z, U.w};
-    const float dv[4] = {D.x, D.y, D.z, D.w};
-    const float rv[4] = {d.x, d.y, d.z, d.w};
-    float o[4];
+    // PK: the packed form below; else this one, left to the compiler's
+    // vectoriser (1024^3, r03: the K = 4 pass 3.67 ms this way against 2.81
+    // packed -- 36 VGPRs of spill -- the K = 3 pass 2.17 against 2.24)
+    if constexpr (!PK) {
+        float o[4];
+        const float cv[4] = {c.x, c.y, c.z, c.w};
+        const float nv[4] = {N.x, N.y, N.z, N.w};
+        const float sv[4] = {S.x, S.y, S.z, S.w};
+        const float uv[4] = {U.x, U.y, U.z, U.w};
+        const float dv[4] = {D.x, D.y, D.z, D.w};
+        const float rv[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float E = k < 3 ? cv[k + 1] : er;
-        const float Wv = k > 0 ? cv[k - 1] : wl;
-        float s = E + Wv;
-        s = s + nv[k];
-        s = s + sv[k];
-        s = s + uv[k];
-        s = s + dv[k];
-        const float rhs = PRE ? rv[k] : (h2 * rv[k]) / dt;
-        const int xk = x + k;
-        o[k] = (xk != 0 && xk != nx - 1) ? (1.0f / 6.0f) * (s - rhs) : cv[k];
+        for (int k = 0; k < 4; ++k) {
+            const float E = k < 3 ? cv[k + 1] : er;
+            const float Wv = k > 0 ? cv[k - 1] : wl;
+            float s = E + Wv;
+            s = s + nv[k];
+            s = s + sv[k];
+            s = s + uv[k];
+            s = s + dv[k];
+            const float rhs = PRE ? rv[k] : (a.h2 * rv[k]) / a.dt;
+            const int xk = x + k;
+            o[k] = (xk != 0 && xk != nx - 1) ? (1.0f / 6.0f) * (s - rhs) : cv[k];
     }
     return make_float4(o[0], o[1], o[2], o[3]);
+    }
+    // cells (0, 1) and (2, 3) as packed pairs (v_pk_add / v_pk_mul: each
+    // element the scalar operation, in the single sweep's order), written
+    // out so that the pairs are the aligned register pairs of the float4s
+    typedef float v2 __attribute__((ext_vector_type(2)));
+    const v2 mid = {c.y, c.z};  // E of cells 0, 1 and W of cells 2, 3
+    v2 s01 = mid + v2{wl, c.x};
+    v2 s23 = v2{c.w, er} + mid;
+    s01 = s01 + v2{N.x, N.y};
+    s23 = s23 + v2{N.z, N.w};
+    s01 = s01 + v2{S.x, S.y};
+    s23 = s23 + v2{S.z, S.w};
+    s01 = s01 + v2{U.x, U.y};
+    s23 = s23 + v2{U.z, U.w};
+    s01 = s01 + v2{D.x, D.y};
+    s23 = s23 + v2{D.z, D.w};
+    v2 r01 = {d.x, d.y}, r23 = {d.z, d.w};
+    if constexpr (!PRE) {
+        r01 = (a.h2 * r01) / a.dt;
+        r23 = (a.h2 * r23) / a.dt;
+    }
+    v2 o01 = (1.0f / 6.0f) * (s01 - r01);
+    v2 o23 = (1.0f / 6.0f) * (s23 - r23);
+    // edge columns 0 and nx - 1 keep their values: with x % 4 == 0 and
+    // nx % 4 == 0 (the launcher's requirement) only cell 0 can be column 0
+    // and only cell 3 column nx - 1
+    o01.x = x != 0 ? o01.x : c.x;
+    o23.y = x + 3 != nx - 1 ? o23.y : c.w;
+    return make_float4(o01.x, o01.y, o23.x, o23.y);
 }
 
 // Red-black GS pairs: in a float4 at x % 4 == 0 a colour owns the cells
@@ -232,8 +273,10 @@ __device__ inline v2f_t level2(v2f_t C, v2f_t O, float wl, float er, v2f_t N, v2
     const v2f_t r = a.cz * (U + D);
     v2f_t o = (((p + q) + r) - rhs) * a.cd;
     const int x0 = x + h;  // the pair's cells x0, x0 + 2
-    o.x = (x0 != 0 && x0 != nx - 1) ? o.x : C.x;
-    o.y = (x0 + 2 != nx - 1) ? o.y : C.y;
+    // (x % 4 == 0, nx % 4 == 0: only x0 = 0 can be column 0 and only
+    // x0 + 2 = x + 3 column nx - 1)
+    if (h == 0) o.x = x0 != 0 ? o.x : C.x;
+    if (h == 1) o.y = x0 + 2 != nx - 1 ? o.y : C.y;
     if (own) {
         chg = fmaxf(chg, fabsf(o.x - C.x));
         chg = fmaxf(chg, fabsf(o.y - C.y));
@@ -704,10 +747,49 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             a.rhs_out + (size_t)(own ? z : 0) * plane, (short)0,
                             own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
                         const gv4f rv = {Rq[j][RS0].x, Rq[j][RS0].y, Rq[j][RS0].z, Rq[j][RS0].w};
-                        __builtin_amdgcn_raw_buffer_store_b128(rv, ro, (int)so[j], 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(rv, ro, (int)so[j], 0, kStoreNt);
                     }
                 }
-                // phase R: level l of plane p = z - l + 1
+                // phase R: level l of plane p = z - l + 1, one (level, row)
+                // at a time.  (Reading the next update's LDS operands before
+                // this one computes -- they all come from tiles phase W wrote
+                // -- ran at 3.40 against 2.24 ms per K = 3 pass: 17 VGPRs of
+                // spill.)
+                struct LdsIn {
+                    QT N, S;       // rows r + 1, r - 1 of level l - 1 (GS: the pair)
+                    float wl, er;  // the x-halo cells xs - 1, xs + 256
+                };
+                auto fetch = [&](int l, int j) {
+                    const int r = rr[j];
+                    LdsIn o;
+                    const float *row = T(l - 1, r);
+                    if constexpr (MODE == kRbgs) {
+                        const int h = (BPv ^ E ^ (j * NWR)) & 1;
+                        // cell xs - 1 (the left chunk's cell 3) and xs + 256 (the
+                        // right chunk's cell 0), level l - 1; in a pair tile the
+                        // left pair holds cells 1, 3 when h = 0 and the right one
+                        // cells 0, 2 when h = 1, the cases that read them
+                        const bool pt = PT && l > 1;
+                        o.wl = pt ? row[1] : row[3];
+                        o.er = pt ? row[130] : row[260];
+                        if (pt) {
+                            o.N = *reinterpret_cast<const v2f_t *>(T(l - 1, r + 1) + 2 + 2 * lane);
+                            o.S = *reinterpret_cast<const v2f_t *>(T(l - 1, r - 1) + 2 + 2 * lane);
+                        } else if (SPLIT) {
+                            o.N = lds2s(T(l - 1, r + 1), lane, h);
+                            o.S = lds2s(T(l - 1, r - 1), lane, h);
+                        } else {
+                            o.N = pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
+                            o.S = pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
+                        }
+                    } else {
+                        o.wl = row[3];
+                        o.er = row[260];
+                        o.N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
+                        o.S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
+                    }
+                    return o;
+                };
 #pragma unroll
                 for (int l = 1; l <= K; ++l) {
                     const int p = z - l + 1;
@@ -728,32 +810,15 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             const v2f_t Op = l == 1 ? pick2(V[j][vs(0)], 1 - h) : Q[j][l - 1][qs(l - 1, 1)];
                             const v2f_t Up = l == 1 ? pick2(V[j][vs(1)], h) : Q[j][l - 1][qs(l - 1, 2)];
                             const v2f_t Dp = l == 1 ? pick2(V[j][vs(-1)], h) : Q[j][l - 1][qs(l - 1, 0)];
-                            const float *row = T(l - 1, r);
+                            const LdsIn in = fetch(l, j);
                             float wl = dpp_from_lower(Op.y), er = dpp_from_upper(Op.x);
-                            // cell xs - 1 (the left chunk's cell 3) and xs + 256 (the
-                            // right chunk's cell 0), level l - 1; in a pair tile the
-                            // left pair holds cells 1, 3 when h = 0 and the right one
-                            // cells 0, 2 when h = 1, the cases that read them
-                            const bool pt = PT && l > 1;
-                            const float wl_l = pt ? row[1] : row[3], er_l = pt ? row[130] : row[260];
-                            if (lane == 0) wl = wl_l;
-                            if (lane == 63) er = er_l;
-                            v2f_t v = Cp;
-                            if (xin) {
-                                v2f_t N, Sv;
-                                if (pt) {
-                                    N = *reinterpret_cast<const v2f_t *>(T(l - 1, r + 1) + 2 + 2 * lane);
-                                    Sv = *reinterpret_cast<const v2f_t *>(T(l - 1, r - 1) + 2 + 2 * lane);
-                                } else if (SPLIT) {
-                                    N = lds2s(T(l - 1, r + 1), lane, h);
-                                    Sv = lds2s(T(l - 1, r - 1), lane, h);
-                                } else {
-                                    N = pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
-                                    Sv = pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
-                                }
-                                v = level2(Cp, Op, wl, er, N, Sv, Up, Dp, pick2(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], h), h, x, nx,
-                                           irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, chgl[slot(l)]);
-                            }
+                            if (lane == 0) wl = in.wl;
+                            if (lane == 63) er = in.er;
+                            // every lane computes (one beyond nx reads zeros and is
+                            // never stored: its LDS writes and HBM store are masked)
+                            const v2f_t v = level2(Cp, Op, wl, er, in.N, in.S, Up, Dp,
+                                                   pick2(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], h), h, x, nx,
+                                                   irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, chgl[slot(l)]);
                             if (l < K) {
                                 if constexpr (ROT) {
                                     Q[j][l][sl3(R - l + 1)] = v;
@@ -770,34 +835,26 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                     a.out + (size_t)(own ? p : 0) * plane, (short)0,
                                     own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
                                 const gv4f vv = {f.x, f.y, f.z, f.w};
-                                __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, 0);
+                                __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, kStoreNt);
                             }
-                            __builtin_amdgcn_sched_barrier(0);
                           }
                         } else if (r >= l && r < NR - l) {
                             // level l-1 at planes p (c), p + 1 (U), p - 1 (D)
                             const float4 c = l == 1 ? V[j][vs(0)] : Q[j][l - 1][qs(l - 1, 1)];
                             const float4 U = l == 1 ? V[j][vs(1)] : Q[j][l - 1][qs(l - 1, 2)];
                             const float4 D = l == 1 ? V[j][vs(-1)] : Q[j][l - 1][qs(l - 1, 0)];
+                            const LdsIn in = fetch(l, j);
                             float wl = dpp_from_lower(c.w);
                             float er = dpp_from_upper(c.x);
-                            const float *row = T(l - 1, r);
-                            const float wl_l = row[3], er_l = row[260];
-                            if (lane == 0) wl = wl_l;
-                            if (lane == 63) er = er_l;
-                            float4 v = c;
-                            if (xin) {
-                                const float4 N = lds4(T(l - 1, r + 1) + 4 + 4 * lane);
-                                const float4 S = lds4(T(l - 1, r - 1) + 4 + 4 * lane);
-                                const int y = y0 - K + r;
-                                float lm = 0.f;
-                                (void)y;
-                                v = level4<MODE, PREL>(c, wl, er, N, S, U, D,
-                                                      Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], x, nx,
-                                                      irow[j] && !fx, a, (BPv ^ E ^ (j * NWR)) & 1,
-                                                      orow[j] && p >= z0 && p < z1, lm);
-                                fold(l, lm);
-                            }
+                            if (lane == 0) wl = in.wl;
+                            if (lane == 63) er = in.er;
+                            float lm = 0.f;
+                            // every lane (see the GS branch)
+                            const float4 v = level4<MODE, PREL, K == 4>(c, wl, er, in.N, in.S, U, D,
+                                                                Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], x, nx,
+                                                                irow[j] && !fx, a, (BPv ^ E ^ (j * NWR)) & 1,
+                                                                orow[j] && p >= z0 && p < z1, lm);
+                            fold(l, lm);
                             if (l < K) {
                                 if constexpr (ROT) {
                                     Q[j][l][sl3(R - l + 1)] = v;  // over plane p - 3, dead
@@ -814,12 +871,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                     a.out + (size_t)(own ? p : 0) * plane, (short)0,
                                     own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
                                 const gv4f vv = {v.x, v.y, v.z, v.w};
-                                __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, 0);
+                                __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, kStoreNt);
                             }
-                            // one (level, row) at a time: measured 0.4 % faster than
-                            // letting the scheduler interleave them
-                            __builtin_amdgcn_sched_barrier(0);
                         }
+                        __builtin_amdgcn_sched_barrier(0);
                     }
                 }
                 trace_mark(a.trace, wv, z - zs, 3);
@@ -1052,6 +1107,10 @@ static int tbr_launch(TbrArgs a, int K, int rows, int zchunk, bool pre, hipStrea
     const int pd = jacobi3d_tb_prefetch();
     if (first && (MODE != kJacobi || pre || pd != 1 || rows != 0 || K < 2)) {
         set_error("jacobi3d_tbr: a first pass needs Jacobi, raw div, prefetch 1, auto tiles, 2..4 levels");
+        return CFD_E_INVALID;
+    }
+    if (a.nx % 4 != 0) {  // float4 rows; the levels' edge rule assumes it (level4)
+        set_error("jacobi3d_tbr: nx must be a multiple of 4");
         return CFD_E_INVALID;
     }
     const int L = a.ze - a.zb;
