@@ -65,6 +65,12 @@ __device__ inline __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, int p, in
 // as well: 2.97 ms at K = 3 -- the neighbouring tiles' halo re-reads then
 // miss L2.)
 constexpr int kStoreNt = 2;
+#ifndef CFD_TBR_EARLY
+#define CFD_TBR_EARLY 1
+#endif
+#ifndef CFD_GS_ROT4
+#define CFD_GS_ROT4 0
+#endif
 
 
 __device__ inline float4 ldb4(__amdgpu_buffer_rsrc_t r, uint32_t byte_ofs) {
@@ -488,6 +494,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // GS level-0 tile by colour pair (sts4s; at 3 levels every tile): +1.2 %
     // at K = 3
     constexpr bool SPLIT = MODE == kRbgs && DMA;
+    // EARLY (DMA path): each step's staging rows are fetched two steps ahead,
+    // in phase R right after the wave read its rows of the same buffer,
+    // instead of one step ahead at the start of phase W
+    constexpr bool EARLY = DMA && MODE == kRbgs && CFD_TBR_EARLY;
     constexpr int SST = DMA ? SR_ * 256 : 4;
     constexpr int SSR = RDMA ? SR_ * 256 : 4;
     __shared__ __attribute__((aligned(16))) float st_p0[SST], st_p1[SST], st_r0[SSR], st_r1[SSR];
@@ -578,7 +588,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // to 3 levels: -2.3 % per pass for the Jacobi at K = 3, -2.9 % for the
     // red-black GS (whose level queues hold pairs, so its two march copies fit
     // with them at 2 rows per wave); K = 4 spills with them
-    constexpr bool ROT = DMA && K <= 3 && (MODE == kJacobi || RPW <= 2) && !SHIFTQ;
+    constexpr bool ROT = DMA && (K <= 3 || (CFD_GS_ROT4 && MODE == kRbgs)) && (MODE == kJacobi || RPW <= 2) && !SHIFTQ;
     const int zl = ROT ? zs + 6 * ((zl0 - zs + 6) / 6) - 1 : zl0;
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
@@ -644,12 +654,28 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 else
                     Rn[j] = ldb4(plane_rsrc(a.div, zs, nz, plane), bo[j]);
             }
+            if constexpr (EARLY) {
+                // and step zs + 1's (plane zs + 2, rhs zs + 1) in the even ones;
+                // from then on step z fetches step z + 2's (see the step)
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) {
+                    if (!ZERO) dma_row(plane_rsrc4(a.in, zs + 2, nz, plane), bo[j], st_p0 + (rr[j] - 1) * 256);
+                    if constexpr (RDMA) dma_row(plane_rsrc4(a.div, zs + 1, nz, plane), bo[j], st_r0 + (rr[j] - 1) * 256);
+                }
+                wait_vmcnt<0>();
+            }
             // Register queues without moves: plane q of level 0 / level l lives
             // in slot (q - zs) mod 3 of V / Q[.][l], and (when the unroll
             // period 6 is a multiple of K) the rhs of plane q in slot
             // (q - zs) mod K of Rq; the march is unrolled by 6 so that every
             // slot index is a compile-time constant.  (K = 4 shifts Rq.)
             constexpr bool ROTR = ROT && 6 % K == 0;
+            // memory operations per step and wave, for EARLY's vmcnt wait:
+            // staging DMAs, !RDMA rhs loads, level-K stores (one per row, issued
+            // for every row: see phase R), first-pass rhs stores
+            constexpr int kND = ((ZERO ? 0 : 1) + (RDMA ? 1 : 0)) * RPW, kNR = RDMA ? 0 : RPW, kNSK = RPW,
+                          kNSR = RHSW ? RPW : 0;
+            static_assert(2 * kNSK + 2 * kNR + kNSR + kND < 64, "vmcnt range");
             auto step = [&](int z, auto parc, auto rotc, auto bpc) {
                 constexpr int E = decltype(parc)::value;  // (z - zs) & 1
                 constexpr int R = decltype(rotc)::value;  // (z - zs) mod 6 (ROT), else 0
@@ -666,7 +692,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 float *const rw = E ? st_r1 : st_r0;
                 const float *const pr = E ? st_p0 : st_p1;
                 const float *const rdr = E ? st_r0 : st_r1;
-                {
+                if constexpr (!EARLY) {
                     const v4i32 rp = plane_rsrc4(a.in, z + 2, nz, plane);
                     const v4i32 rd = plane_rsrc4(a.div, z + 1, nz, plane);
 #pragma unroll
@@ -674,6 +700,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                         if (!ZERO) dma_row(rp, bo[j], pw + (rr[j] - 1) * 256);
                         if constexpr (RDMA) dma_row(rd, bo[j], rw + (rr[j] - 1) * 256);
                     }
+                } else {
+                    (void)pw;
+                    (void)rw;
                 }
                 // !RDMA: this step's rhs row (loaded last step) and the next one's load
                 float4 Rc[RPW];
@@ -721,9 +750,17 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             }
                         }
                 }
-                // the previous step's DMAs have landed once at most this step's
-                // 2 * RPW remain in flight (they are issued in order)
-                wait_vmcnt<((ZERO ? 0 : 1) + 1) * RPW>();
+                // this step's DMAs have landed once at most the memory
+                // operations issued after them remain in flight (vmcnt counts
+                // in issue order): without EARLY, this step's 2 * RPW
+                // fetches (the next step's rows); with EARLY (issued in step
+                // z - 2's phase R), step z - 2's level-K stores, the !RDMA rhs
+                // loads of steps z - 1 and z, step z - 1's rhs stores (first
+                // pass) and DMAs, and step z - 1's level-K stores
+                if constexpr (EARLY)
+                    wait_vmcnt<2 * kNSK + 2 * kNR + kNSR + kND>();
+                else
+                    wait_vmcnt<((ZERO ? 0 : 1) + 1) * RPW>();
                 trace_mark(a.trace, wv, z - zs, 1);
                 lds_barrier();
                 trace_mark(a.trace, wv, z - zs, 2);
@@ -748,6 +785,19 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
                         const gv4f rv = {Rq[j][RS0].x, Rq[j][RS0].y, Rq[j][RS0].z, Rq[j][RS0].w};
                         __builtin_amdgcn_raw_buffer_store_b128(rv, ro, (int)so[j], 0, kStoreNt);
+                    }
+                }
+                if constexpr (EARLY) {
+                    // the staging rows just read are this wave's own: once the
+                    // reads are done, fetch step z + 2's rows into them (plane
+                    // z + 3, rhs z + 2), two steps ahead and off phase W
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    const v4i32 rp = plane_rsrc4(a.in, z + 3, nz, plane);
+                    const v4i32 rd = plane_rsrc4(a.div, z + 2, nz, plane);
+#pragma unroll
+                    for (int j = 0; j < RPW; ++j) {
+                        if (!ZERO) dma_row(rp, bo[j], const_cast<float *>(pr) + (rr[j] - 1) * 256);
+                        if constexpr (RDMA) dma_row(rd, bo[j], const_cast<float *>(rdr) + (rr[j] - 1) * 256);
                     }
                 }
                 // phase R: level l of plane p = z - l + 1, one (level, row)
@@ -873,6 +923,14 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 const gv4f vv = {v.x, v.y, v.z, v.w};
                                 __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, kStoreNt);
                             }
+                        }
+                        if (EARLY && l == K && !(r >= l && r < NR - l)) {
+                            // a row outside level K's range still issues its store
+                            // (to an empty resource: dropped), so that every step
+                            // has kNSK of them for EARLY's vmcnt count
+                            const __amdgpu_buffer_rsrc_t ro =
+                                __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, 0, 0x00020000);
+                            __builtin_amdgcn_raw_buffer_store_b128(gv4f{0.f, 0.f, 0.f, 0.f}, ro, (int)kOob, 0, kStoreNt);
                         }
                         __builtin_amdgcn_sched_barrier(0);
                     }

@@ -92,8 +92,10 @@ int launch_zero_faces3d(float *a, float *b, int nz, int ny, int nx, hipStream_t 
 }
 
 // Jacobi sweeps per pass when tb_steps == 0 (r01 sweep at 1024^3: K=2 855,
-// K=3 1010-1030, K=4 1000 Gcell/s)
-constexpr int kDefaultLevels = 3;
+// K=3 1010-1030, K=4 1000 Gcell/s; r03, nt stores and the packed K = 4
+// level, three runs each on one box: 1024^3 K=3 1462-1466 / K=4 1490-1494,
+// 512^3 1380-1385 / 1435-1443, channel 1450-1465 / 1490-1492)
+constexpr int kDefaultLevels = 4;
 
 // planes per tile of the blocked kernels (0 = the launcher's cost model)
 int jacobi3d_tb_zchunk() { return tuning().tb_zchunk; }

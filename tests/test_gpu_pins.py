@@ -2,10 +2,10 @@
 found unpinned.  All bit-exact against the oracle (BIT-EXACT bar: the Jacobi and
 red-black GS paths reassociate nothing).
 
-* The headline kernel: 1024^3 Jacobi with 3, 4 and 5 sweeps on the default
-  blocking (3 sweeps per pass, the tall-tile jacobi3d_tbr<3, 10 row waves x 2
-  rows> the bench runs), with and without the RHS workspace; the test asserts
-  that this shape ran.
+* The headline kernel: 1024^3 Jacobi with 4, 5 and 6 sweeps on the default
+  blocking (4 sweeps per pass, the tall-tile jacobi3d_tbr<4, 11 row waves x 2
+  rows> the bench runs) and 3, 4, 5 on the 3-sweep one (tbr<3, 10 x 2>), with
+  and without the RHS workspace; the test asserts that these shapes ran.
 * Config 5's kernel: 1024^3 red-black GS, 2 and 3 iterations on the default
   16-row tile (4 levels, 11 x 2) and on the 3-level one (10 x 2), and every
   explicit GS tile (2, 3, 4 levels) on a ragged grid, with an early stop.
@@ -65,27 +65,30 @@ def div1024():
 
 # ------------------------------------------------------------- north star
 def test_jacobi3d_1024_headline_kernel_bitexact(div1024):
-    """1024^3, h = 1/1023, dt = 5e-5 (the bench's grid and constants): 3, 4
-    and 5 sweeps -- one tbr<3> pass; a tbr<3> pass plus a single sweep; a
-    tbr<3> pass plus the 2-sweep remainder pass -- with and without the RHS
-    workspace (the bench uses it)."""
+    """1024^3, h = 1/1023, dt = 5e-5 (the bench's grid and constants), with and
+    without the RHS workspace (the bench uses it).  Default blocking (4 sweeps
+    per pass, tbr<4, 11 row waves x 2 rows>): 4, 5 and 6 sweeps -- one pass;
+    a 3-sweep first pass and a 2-sweep remainder; a 2-sweep first pass and a
+    tbr<4> pass.  Three sweeps per pass (tbr<3, 10 x 2>): 3, 4 and 5."""
     n = 1024
     h, dt = 1.0 / (n - 1), np.float32(5e-5)
-    assert int(lib().cfd_get_jacobi3d_levels()) == 3
+    assert int(lib().cfd_get_jacobi3d_levels()) == 4
     ref = {3: oracle.jacobi3d(div1024, h=h, dt=dt, iters=3, mt=True)}
-    ref[4] = oracle.jacobi3d(div1024, ref[3], h=h, dt=dt, iters=1, mt=True)
-    ref[5] = oracle.jacobi3d(div1024, ref[4], h=h, dt=dt, iters=1, mt=True)
+    for it in (4, 5, 6):
+        ref[it] = oracle.jacobi3d(div1024, ref[it - 1], h=h, dt=dt, iters=1, mt=True)
     d = dev(div1024)
     phi = torch.zeros_like(d)
     tmp = torch.empty_like(d)
-    for rhs in (torch.empty_like(d), None):
-        for iters in (3, 4, 5):
-            phi.zero_()
-            K.solve_pressure_jacobi3d(phi, d, h, dt, None, iters, phi_tmp=tmp, rhs_ws=rhs)
-            if iters == 3:
-                # the bench's kernel: 3 levels, 10 row waves x 2 rows (16 output rows), one z-chunk
-                assert last_shape() == (3, 10, 2, n - 2), last_shape()
-            assert np.array_equal(host(phi), ref[iters]), (iters, rhs is None)
+    for levels, shape in ((0, (4, 11, 2, n - 2)), (3, (3, 10, 2, n - 2))):
+        call("cfd_set_jacobi3d_blocking", levels, 0, 0)
+        k = levels or 4
+        for rhs in (torch.empty_like(d), None):
+            for iters in (k, k + 1, k + 2):
+                phi.zero_()
+                K.solve_pressure_jacobi3d(phi, d, h, dt, None, iters, phi_tmp=tmp, rhs_ws=rhs)
+                if iters == k:  # the bench's kernel for this depth, one z-chunk
+                    assert last_shape() == shape, last_shape()
+                assert np.array_equal(host(phi), ref[iters]), (levels, iters, rhs is None)
 
 
 def test_rbgs3d_1024_default_tile_bitexact(div1024):
@@ -166,8 +169,8 @@ def test_channel_1024x1024x512_slab_rccl_bitexact(iters):
 
 def test_jacobi3d_512_bench_step_200_sweeps_bitexact():
     """Config 3's whole bench step at full size: phi = 0 and 200 sweeps
-    (cfd_jacobi3d_zero_f32: the fused first pass of 2 sweeps, then 66 passes
-    of jacobi3d_tbr<3> on the cost model's 512^3 shape -- 16-row tiles, four
+    (cfd_jacobi3d_zero_f32: the fused first pass of 4 sweeps, then 49 passes
+    of jacobi3d_tbr<4> on the cost model's 512^3 shape -- 16-row tiles, four
     z-chunks of 128 planes, 256 workgroups) against the oracle's 200 sweeps
     (OpenMP form, bit-identical to the serial one)."""
     n, iters = 512, 200
@@ -180,7 +183,7 @@ def test_jacobi3d_512_bench_step_200_sweeps_bitexact():
     phi = torch.empty_like(d)
     tmp, rhs = torch.empty_like(d), torch.empty_like(d)
     K.solve_pressure_jacobi3d_zero(phi, d, h, dt, iters, phi_tmp=tmp, rhs_ws=rhs)
-    assert last_shape() == (3, 10, 2, 128), last_shape()
+    assert last_shape() == (4, 11, 2, 128), last_shape()
     assert np.array_equal(host(phi), ref)
 
 
