@@ -322,7 +322,11 @@ def main():
     elif len(shape) == 3:
         nz, ny, nx = shape
         h = 1.0 / (nx - 1)
-        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else int(lib().cfd_get_jacobi3d_levels()))
+        # slab ghosts: as deep as the sweeps per pass, at most 3 -- at R = 8 the
+        # 3-sweep slab pass beats the 4-sweep one (per-rank rehearsal, r03:
+        # 22.5 vs 23.5 ms per 200-sweep solve; equal at R = 2)
+        levels = int(lib().cfd_get_jacobi3d_levels())
+        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else (min(levels, 3) if world > 1 else levels))
         if not use_slab:
             div = torch.randn(shape, generator=g, device=dev, dtype=torch.float32)
             phi = torch.zeros_like(div)
@@ -412,7 +416,8 @@ def main():
     # sweeps per launch: K Jacobi sweeps per blocked pass; the GS timing
     # counts iterations, and a fused GS pass is one (two with --tb 4)
     if not gs:
-        spl = levels if blocked else 1
+        # (a slab pass fuses min(levels, ghost) sweeps)
+        spl = (min(levels, plan.ghost) if use_slab and len(shape) == 3 else levels) if blocked else 1
     elif use_slab:  # slab passes: two iterations with 4-deep ghosts, else one
         spl = 2 if blocked and plan.ghost == 4 else 1
     else:  # single GPU: half-sweeps per pass (--tb, or the library's auto: 4 = two iterations)

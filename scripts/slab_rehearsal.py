@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--transport", default="ce", choices=["ce", "rccl"])
     ap.add_argument("--comm-priority", type=int, default=1, help="1: high-priority comm stream")
     ap.add_argument("--prefetch", type=int, default=0, help="cfd_set_jacobi3d_prefetch (0 auto, 1 DMA, 2 regs)")
+    ap.add_argument("--ghost", type=int, default=0, help="Jacobi ghost planes (0: the sweeps per pass)")
     ap.add_argument("--tb", type=int, default=0,
                     help="--self red-black GS: 0 or 4 = two iterations per pass (4-deep ghosts), 2 = one")
     a = ap.parse_args()
@@ -120,9 +121,11 @@ def rccl_self(a):
     n, R = a.n, a.ranks
     nz = a.nz or n
     gs = a.workload == "rbgs"
-    G = (4 if a.tb in (0, 4) else 2) if gs else 3
-    if gs and a.tb:
-        call("cfd_set_jacobi3d_blocking", a.tb, 0, 0)  # rbgs3d_iters_per_pass(): 2 at 4, else 1
+    if a.tb:
+        call("cfd_set_jacobi3d_blocking", a.tb, 0, 0)  # GS: rbgs3d_iters_per_pass(): 2 at 4, else 1
+    # Jacobi: ghosts as deep as the sweeps per pass (bench.py's plan at N > 1;
+    # --ghost overrides, and a pass then fuses min(levels, ghost) sweeps)
+    G = (4 if a.tb in (0, 4) else 2) if gs else (a.ghost or int(lib().cfd_get_jacobi3d_levels()))
     nzl = nz // R
     shape = (nzl + 2 * G, n, n)
     h = 1.0 / (n - 1)
