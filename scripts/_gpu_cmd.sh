@@ -1,4 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "f64 or pow or time_step or solver" > gpurun_out/t_f64.log 2>&1; rc=$?; tail -5 gpurun_out/t_f64.log; echo "tests rc=$rc"
+for R in 8 2; do for g in 0 3; do timeout -k 10 200 python scripts/slab_rehearsal.py --self --ranks $R --ghost $g --steps 3 2>/dev/null | tail -1; done; done
+for R in 8 2; do timeout -k 10 200 python scripts/slab_rehearsal.py --self --ranks $R --workload rbgs --steps 3 2>/dev/null | tail -1; done
