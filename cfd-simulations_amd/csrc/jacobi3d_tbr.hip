@@ -68,9 +68,6 @@ constexpr int kStoreNt = 2;
 #ifndef CFD_TBR_EARLY
 #define CFD_TBR_EARLY 1
 #endif
-#ifndef CFD_GS_ROT4
-#define CFD_GS_ROT4 0
-#endif
 
 
 __device__ inline float4 ldb4(__amdgpu_buffer_rsrc_t r, uint32_t byte_ofs) {
@@ -587,8 +584,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // register queues rotated by compile-time slots (see the DMA row wave) up
     // to 3 levels: -2.3 % per pass for the Jacobi at K = 3, -2.9 % for the
     // red-black GS (whose level queues hold pairs, so its two march copies fit
-    // with them at 2 rows per wave); K = 4 spills with them
-    constexpr bool ROT = DMA && (K <= 3 || (CFD_GS_ROT4 && MODE == kRbgs)) && (MODE == kJacobi || RPW <= 2) && !SHIFTQ;
+    // with them at 2 rows per wave); K = 4 spills with them (r03: 111 VGPRs
+    // for the Jacobi, 34 for the GS -- although the shifting queues' moves are
+    // about half of the K = 4 passes' VALU instructions)
+    constexpr bool ROT = DMA && K <= 3 && (MODE == kJacobi || RPW <= 2) && !SHIFTQ;
     const int zl = ROT ? zs + 6 * ((zl0 - zs + 6) / 6) - 1 : zl0;
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
