@@ -244,6 +244,16 @@ __device__ inline v2f_t pick2(float4 f, int h) { return h ? v2f_t{f.y, f.w} : v2
 __device__ inline float4 join2(v2f_t a, v2f_t b, int h) {
     return h ? make_float4(b.x, a.x, b.y, a.y) : make_float4(a.x, b.x, a.y, b.y);
 }
+// A float4 of the GS row waves' level-0 and rhs queues, held as its two
+// colour pairs (cells 0, 2 and 1, 3): a level takes its pair without the
+// moves that picking one out of a float4 costs (2 per pick, ~10 per update)
+struct P4 {
+    v2f_t e, o;
+};
+__device__ inline v2f_t pick2(const P4 &f, int h) { return h ? f.o : f.e; }
+__device__ inline P4 split4(float4 f) { return P4{v2f_t{f.x, f.z}, v2f_t{f.y, f.w}}; }
+// from LDS: two ds_read2_b32 (words 0, 2 and 1, 3) straight into the pairs
+__device__ inline P4 ldsp(const float *p) { return P4{v2f_t{p[0], p[2]}, v2f_t{p[1], p[3]}}; }
 // GS tiles (SPLIT): the 256 cells of a tile row are stored by colour pair,
 // cells 4 i + {0, 2} at 4 + 2 i and cells 4 i + {1, 3} at 132 + 2 i, so a
 // lane reads its pair as one conflict-free ds_read_b64 (the float4 layout
@@ -253,6 +263,10 @@ __device__ inline float4 join2(v2f_t a, v2f_t b, int h) {
 __device__ inline void sts4s(float *row, int lane, float4 v) {
     *reinterpret_cast<v2f_t *>(row + 4 + 2 * lane) = v2f_t{v.x, v.z};
     *reinterpret_cast<v2f_t *>(row + 132 + 2 * lane) = v2f_t{v.y, v.w};
+}
+__device__ inline void sts4s(float *row, int lane, const P4 &v) {
+    *reinterpret_cast<v2f_t *>(row + 4 + 2 * lane) = v.e;
+    *reinterpret_cast<v2f_t *>(row + 132 + 2 * lane) = v.o;
 }
 // pair-tile row (PT): left chunk pair | 64 lanes x pair | right chunk pair
 constexpr int kPairRow = 132;
@@ -630,7 +644,15 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             // cells keep the previous level's values, which the level below
             // holds): half the registers of the level queues
             using QT = std::conditional_t<MODE == kRbgs, v2f_t, float4>;
-            float4 V[RPW][3], Rq[RPW][K];
+            // GS: V and Rq hold colour pairs (P4)
+            using VT = std::conditional_t<MODE == kRbgs, P4, float4>;
+            auto toV = [](float4 f) -> VT {
+                if constexpr (MODE == kRbgs)
+                    return split4(f);
+                else
+                    return f;
+            };
+            VT V[RPW][3], Rq[RPW][K];
             QT Q[RPW][K][3];
             float4 Rn[RPW];  // !RDMA: the rhs row of the next step's plane, in flight
 #pragma unroll
@@ -639,13 +661,13 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = QT{};
                 // planes zs - 1 and zs in slots 2 and 0 (slot (q - zs) mod 3), or 0
                 // and 1 (shifted queues)
-                V[j][ROT ? 2 : 0] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]);
-                V[j][ROT ? 0 : 1] = ZERO ? z4 : ldb4(plane_rsrc(a.in, zs, nz, plane), bo[j]);
-                V[j][ROT ? 1 : 2] = z4;
+                V[j][ROT ? 2 : 0] = toV(ZERO ? z4 : ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]));
+                V[j][ROT ? 0 : 1] = toV(ZERO ? z4 : ldb4(plane_rsrc(a.in, zs, nz, plane), bo[j]));
+                V[j][ROT ? 1 : 2] = toV(z4);
                 // rhs rows of planes before zs only feed levels of planes below the
                 // ones the outputs need (the pipeline fill), so they start at 0
 #pragma unroll
-                for (int i = 0; i < K; ++i) Rq[j][i] = z4;
+                for (int i = 0; i < K; ++i) Rq[j][i] = toV(z4);
                 // read at step zs (even): plane zs + 1 and rhs zs in the odd buffers
                 if (!ZERO) dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], st_p1 + (rr[j] - 1) * 256);
                 if constexpr (RDMA)
@@ -765,16 +787,26 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 trace_mark(a.trace, wv, z - zs, 2);
 #pragma unroll
                 for (int j = 0; j < RPW; ++j) {
-                    V[j][vs(1)] = ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
+                    if constexpr (MODE == kRbgs)
+                        V[j][vs(1)] = ldsp(pr + (rr[j] - 1) * 256 + 4 * lane);
+                    else
+                        V[j][vs(1)] = ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
                     constexpr int RS0 = ROTR ? slk(R, K) : 0;  // slot of this step's rhs
                     if constexpr (!ROTR) {
 #pragma unroll
                         for (int i = K - 1; i > 0; --i) Rq[j][i] = Rq[j][i - 1];
                     }
-                    if constexpr (RDMA)
-                        Rq[j][RS0] = torhs(lds4(rdr + (rr[j] - 1) * 256 + 4 * lane));
-                    else
-                        Rq[j][RS0] = torhs(Rc[j]);
+                    if constexpr (RDMA && MODE == kRbgs) {
+                        // -div * dt_inv on the pairs (each element the scalar form)
+                        P4 d = ldsp(rdr + (rr[j] - 1) * 256 + 4 * lane);
+                        d.e = -d.e * a.dt_inv;
+                        d.o = -d.o * a.dt_inv;
+                        Rq[j][RS0] = d;
+                    } else if constexpr (RDMA) {
+                        Rq[j][RS0] = toV(torhs(lds4(rdr + (rr[j] - 1) * 256 + 4 * lane)));
+                    } else {
+                        Rq[j][RS0] = toV(torhs(Rc[j]));
+                    }
                     if constexpr (RHSW) {
                         // the rhs of plane z for the later passes: owned planes and
                         // rows only (so[j] = kOob elsewhere), every x of the row
