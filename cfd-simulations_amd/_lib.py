@@ -108,6 +108,7 @@ PROTOTYPES = {
     "cfd_rbgs_finish": (c_int, [P, P, P, c_size_t, P, P]),
     "cfd_set_small2d_gs_iters": (c_int, [c_int, c_int]),
     "cfd_set_small2d_gs_persistent": (c_int, [c_int]),
+    "cfd_set_small2d_jacobi_persistent": (c_int, [c_int, c_int]),
     "cfd_set_small2d_gs_trace": (c_int, [P, c_size_t]),
     "cfd_set_tbr_trace": (c_int, [P, c_size_t]),
     "cfd_set_jacobi3d_config": (c_int, [c_int, c_int, c_int]),

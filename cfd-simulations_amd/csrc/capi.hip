@@ -53,6 +53,9 @@ static Tuning process_defaults() {
         t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;
         t.gs_wg = env_int("CFD_GS_SMALL_WG", t.gs_wg) != 0;
         t.gs_persist = env_int("CFD_GS_PERSIST", t.gs_persist) != 0;
+        t.j2_persist = env_int("CFD_J2_PERSIST", t.j2_persist) != 0;
+        const int jn = env_int("CFD_J2P_NI", t.j2p_ni);
+        t.j2p_ni = jn == 4 || jn == 6 || jn == 8 ? jn : t.j2p_ni;
         t.gs_pairs = env_int("CFD_GS_PAIRS", t.gs_pairs) != 0;
         const int ni = env_int("CFD_GS_SMALL_NI", t.gs_ni);
         t.gs_ni = ni >= 1 && ni <= 4 ? ni : t.gs_ni;
@@ -149,6 +152,16 @@ int cfd_set_small2d_gs_persistent(int mode) {
     const Tuning d = process_defaults();
     tuning().gs_persist = mode ? mode >= 2 : d.gs_persist;
     tuning().gs_pairs = mode >= 2 ? mode == 2 : d.gs_pairs;
+    return CFD_OK;
+}
+
+int cfd_set_small2d_jacobi_persistent(int on, int sweeps_per_block) {
+    CFD_REQUIRE(on >= 0 && on <= 2, "small-grid Jacobi persistent: on must be 0 (default), 1 (off) or 2 (on)");
+    CFD_REQUIRE(sweeps_per_block == 0 || sweeps_per_block == 4 || sweeps_per_block == 6 || sweeps_per_block == 8,
+                "small-grid Jacobi persistent: sweeps per block must be 0 (default), 4, 6 or 8");
+    const Tuning d = process_defaults();
+    tuning().j2_persist = on ? on == 2 : d.j2_persist;
+    tuning().j2p_ni = sweeps_per_block ? sweeps_per_block : d.j2p_ni;
     return CFD_OK;
 }
 

@@ -23,6 +23,10 @@ struct Tuning {
     int j2_dma = 0;
     // small-grid 2-D Jacobi: sweeps per launch (1..8), rows per wave, cells per lane
     int j2s_k = 4, j2s_rw = 1, j2s_vec = 1;
+    // small-grid 2-D Jacobi (f32) as one persistent launch (jacobi2d_persist)
+    // when every tile fits on the chip at once, j2p_ni (4, 6, 8) sweeps per
+    // block; 0 = one launch per j2s_k sweeps
+    int j2_persist = 1, j2p_ni = 8;
     // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per
     // workgroup, iterations per launch (1..4)
     int gs_rw = 2, gs_vec = 1, gs_wpb = 4, gs_ni = 4;
@@ -48,6 +52,11 @@ struct Tuning {
     void *tbr_trace = nullptr;
 };
 Tuning &tuning();
+
+// jacobi2d_persist.hip: 1 if it ran the solve (phi <- the result; *rc set on
+// a HIP error), 0 if the persistent path does not apply
+int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t *mask, int ny, int nx,
+                           float dx2, float dtv, int iterations, hipStream_t s, int *rc);
 
 // poisson3d.hip
 int launch_fix_faces3d(const float *src, float *dst, const uint8_t *mask, int ny, int nx, int za,

@@ -1,0 +1,308 @@
+// jacobi2d_persist.hip -- the small-grid 2-D Jacobi solve (v5.py:336-346, the
+// NumPy branch of solve_pressure_fast on the 600 x 180 cylinder: 1500 sweeps,
+// masked cells forced to 0 after each) as ONE persistent launch.
+//
+// The launch-per-pass path (jacobi2d_small, poisson2d.hip) pays ~4 us of
+// kernel boundary and load latency per 4 sweeps at 600 x 180.  Here, as in
+// rbgs2d_persist.hip (whose hand-off this is), the tiles stay resident for
+// the whole solve: a workgroup is one 32-row x 64-column tile (16 waves x 2
+// rows, one cell per lane) that advances NI sweeps per block, the
+// intermediate levels eroding into an NI-row / NI-lane halo, and owns its
+// inner (32 - 2 NI) x (64 - 2 NI) cells.  Own cells stay in registers from
+// block to block; after a block the tile publishes them as 8-byte {value,
+// tag} granules (sc1 stores, tag = block + 1) into a ring of granule planes,
+// and before the next block it polls its halo cells (owned by its 8
+// neighbour tiles) until their tags match.  A level is one LDS exchange of the
+// waves' rows (double-buffered: one barrier per level); x-neighbours by DPP.
+// There is no stop rule in this branch of the reference (a fixed count).
+//
+// Arithmetic: jac5's order, ((E + W) + N + S - rhs) * 0.25 with rhs =
+// f32(dx^2) * div / dt formed as k_rhs2d forms it, two rows per wave as one
+// packed pair (v_pk_add / v_pk_mul: the same IEEE operation per element); a
+// masked cell becomes 0 at every sweep (v5.py:345), rows 0 and ny - 1 and
+// columns 0 and nx - 1 keep their values.  Bit-identical to the single
+// sweep, sweep for sweep.
+//
+// Ring ordering (kJGSlots planes): a tile publishes block k over block
+// k - kJGSlots's granules after it consumed all its neighbours' block k - 1
+// output, which each published after reading its own block k - 1 input
+// (block k - 2 granules): nobody reads a granule plane older than k - 2 then.
+// The result: every tile writes its own cells into phi after its last block;
+// a neighbour read phi only at its start, which preceded its block 0 output
+// that this tile consumed (hence nb >= 2 blocks, iterations > NI).  Every poll
+// is bounded (20 s of the 100 MHz clock), and the launcher checks that every
+// tile is resident at once.
+#include <mutex>
+
+#include "internal.hpp"
+
+namespace cfd {
+namespace {
+
+constexpr int kJW = 16, kJRW = 2, kJT0 = kJW * kJRW;  // waves, rows per wave, tile rows
+constexpr int kJGSlots = 3;
+constexpr int kJMaxTiles = 256;
+constexpr unsigned long long kJSpinLimit = 2000000000ull;  // 20 s at 100 MHz
+
+struct JPersistArgs {
+    float *phi;         // in: the initial guess; out: the own cells of the result
+    const float *src;   // div, or the precomputed rhs (pre)
+    const uint8_t *mask;
+    unsigned long long *G;  // kJGSlots planes of ny * nx granules
+    int *status;            // bit 0: a poll expired
+    int ny, nx, nseg, niters, pre;
+    float dx2, dtv;
+};
+
+__device__ inline unsigned long long jgload(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load sc1
+}
+__device__ inline void jgstore(unsigned long long *p, float v, unsigned tag) {
+    __hip_atomic_store(p, ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store sc1
+}
+__device__ inline void lds_barrier_j() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool MASK, int NI>
+__global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
+    constexpr int HL = NI, SOUT = 64 - 2 * HL, OUT = kJT0 - 2 * NI;
+    static_assert(OUT >= 2, "too many sweeps per block for the tile");
+    __shared__ float S[2][kJT0][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int seg = bid % a.nseg, ty = bid / a.nseg;
+    const int ytop = 1 + ty * OUT - NI;  // global row of tile row 0
+    const int x = seg * SOUT - HL + lane;
+    const bool valid = x >= 0 && x < a.nx;
+    const bool writer = lane >= HL && lane < 64 - HL && valid;
+    const unsigned long long t0 = wall_clock64();
+    bool broken = false;
+
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    float A[kJRW];
+    f2 rh;
+    bool upd[kJRW], zero[kJRW], own[kJRW], inner[kJRW], edgez[kJRW];
+    size_t off[kJRW];
+#pragma unroll
+    for (int j = 0; j < kJRW; ++j) {
+        const int i = kJRW * w + j, y = ytop + i;
+        const bool in_ = valid && y >= 0 && y <= a.ny - 1;
+        off[j] = (size_t)min(max(y, 0), a.ny - 1) * a.nx + (valid ? x : 0);
+        const float v = a.phi[off[j]], d = a.src[off[j]];
+        const bool mk = MASK ? a.mask[off[j]] != 0 : false;
+        A[j] = in_ ? v : 0.f;
+        const float dd = in_ ? d : 0.f;
+        rh[j] = a.pre ? dd : (a.dx2 * dd) / a.dtv;
+        upd[j] = in_ && y >= 1 && y <= a.ny - 2 && x >= 1 && x <= a.nx - 2;
+        zero[j] = in_ && mk;  // v5.py:345: after the interior, masked cells <- 0
+        own[j] = writer && i >= NI && i < kJT0 - NI && y <= a.ny - 2;
+        inner[j] = in_ && y >= 1 && y <= a.ny - 2;  // the cells some tile owns
+        // a masked cell of row 0 or ny - 1 (no tile owns it) becomes 0 too
+        edgez[j] = writer && in_ && !inner[j] && mk;
+    }
+    const size_t plane = (size_t)a.ny * a.nx;
+    const int i0 = kJRW * w;
+
+    // block k's halo cells (block k - 1's granules)
+    auto fetch = [&](int k) {
+        const unsigned long long *Gk = a.G + (size_t)((k - 1) % kJGSlots) * plane;
+        bool need[kJRW];
+#pragma unroll
+        for (int j = 0; j < kJRW; ++j) need[j] = inner[j] && !own[j];
+        while (true) {
+            unsigned long long g[kJRW];
+#pragma unroll
+            for (int j = 0; j < kJRW; ++j) g[j] = need[j] ? jgload(Gk + off[j]) : 0ull;
+            bool more = false;
+#pragma unroll
+            for (int j = 0; j < kJRW; ++j) {
+                if (need[j] && (unsigned)(g[j] >> 32) == (unsigned)k) {
+                    A[j] = __uint_as_float((unsigned)g[j]);
+                    need[j] = false;
+                }
+                more = more || need[j];
+            }
+            broken = broken || wall_clock64() - t0 > kJSpinLimit;
+            if (!__any(more) || broken) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+
+    // sweeps 1..m of one block: level l keeps the tile rows [l, 32 - l); a
+    // wave whose two rows are both dead at level l skips it
+    auto levels = [&](int m) {
+#pragma unroll
+        for (int j = 0; j < kJRW; ++j) S[0][i0 + j][lane] = A[j];
+        lds_barrier_j();
+#pragma unroll
+        for (int l = 1; l <= NI; ++l) {
+            if (l > m) break;
+            const int rb = (l - 1) & 1, wb = l & 1;
+            if (i0 + 1 >= l && i0 < kJT0 - l) {
+                const float up = i0 + 2 < kJT0 ? S[rb][i0 + 2][lane] : 0.f;
+                const float dn = i0 > 0 ? S[rb][i0 - 1][lane] : 0.f;
+                const f2 e2 = {dpp_from_upper(A[0]), dpp_from_upper(A[1])};
+                const f2 w2 = {dpp_from_lower(A[0]), dpp_from_lower(A[1])};
+                f2 s2 = e2 + w2;
+                s2 = s2 + f2{A[1], up};  // N
+                s2 = s2 + f2{dn, A[0]};  // S
+                const f2 nv = 0.25f * (s2 - rh);
+#pragma unroll
+                for (int j = 0; j < kJRW; ++j) {
+                    float b = upd[j] ? nv[j] : A[j];
+                    if (MASK && zero[j]) b = 0.f;
+                    A[j] = b;
+                    S[wb][i0 + j][lane] = b;
+                }
+            }
+            if (l < m) lds_barrier_j();
+        }
+    };
+
+    const int nb = (a.niters + NI - 1) / NI;
+    for (int k = 0; k < nb; ++k) {
+        const int m = min(NI, a.niters - k * NI);
+        if (k > 0) fetch(k);
+        levels(m);
+        if (k + 1 < nb) {
+#pragma unroll
+            for (int j = 0; j < kJRW; ++j)
+                if (own[j]) jgstore(a.G + (size_t)(k % kJGSlots) * plane + off[j], A[j], (unsigned)(k + 1));
+        }
+        lds_barrier_j();  // the next block's LDS writes follow every wave's last reads
+    }
+#pragma unroll
+    for (int j = 0; j < kJRW; ++j) {
+        if (own[j]) a.phi[off[j]] = A[j];
+        if (MASK && edgez[j]) a.phi[off[j]] = 0.f;
+    }
+    if (broken && lane == 0) atomicOr(a.status, 1);
+}
+
+// an expired poll leaves garbage: mark the result (phi[0] <- NaN) so that it
+// cannot pass for a solution
+__global__ void k_jp_status(const int *status, float *phi) {
+    if (*status) phi[0] = __int_as_float(0x7fc00000);
+}
+
+int jtiles_for(int NI, int ny, int nx, int *nseg) {
+    const int OUT = kJT0 - 2 * NI, SOUT = 64 - 2 * NI;
+    *nseg = ceil_div(nx, SOUT);
+    return *nseg * ceil_div(ny - 2, OUT);
+}
+
+template <bool MASK, int NI>
+int jresident_tiles() {
+    static int resident = 0;
+    if (resident == 0) {
+        int dev = 0, per_cu = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jacobi2d_persist<MASK, NI>, 1024, 0) != hipSuccess)
+            return -1;
+        resident = per_cu * cus;
+    }
+    return resident;
+}
+
+// The granule ring and the status word live in a library-owned device buffer
+// (per device, grown on demand, never shrunk): the Jacobi entry points take
+// no exchange workspace.  Growing it frees the old one (hipFree waits for the
+// device), so a process solving ever larger small grids pays that a few times.
+struct JRing {
+    std::mutex mu;
+    void *p[64] = {};
+    size_t bytes[64] = {};
+};
+JRing &jring() {
+    static JRing r;
+    return r;
+}
+void *ring_for(size_t bytes, int *rc) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        *rc = CFD_E_HIP;
+        set_error("jacobi2d persistent: no device");
+        return nullptr;
+    }
+    JRing &r = jring();
+    std::lock_guard<std::mutex> g(r.mu);
+    if (r.bytes[dev] < bytes) {
+        if (r.p[dev]) (void)hipFree(r.p[dev]);
+        r.p[dev] = nullptr;
+        r.bytes[dev] = 0;
+        if (hipMalloc(&r.p[dev], bytes) != hipSuccess) {
+            *rc = CFD_E_HIP;
+            set_error("jacobi2d persistent: ring allocation of %zu bytes failed", bytes);
+            return nullptr;
+        }
+        r.bytes[dev] = bytes;
+    }
+    return r.p[dev];
+}
+
+}  // namespace
+
+int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t *mask, int ny, int nx,
+                           float dx2, float dtv, int iterations, hipStream_t s, int *rc) {
+    *rc = CFD_OK;
+    const int NI = tuning().j2p_ni;
+    if (!tuning().j2_persist || iterations <= NI || ny < 3 || nx < 3) return 0;
+    JPersistArgs a;
+    a.phi = phi;
+    a.src = src;
+    a.mask = mask;
+    a.ny = ny;
+    a.nx = nx;
+    a.niters = iterations;
+    a.pre = pre ? 1 : 0;
+    a.dx2 = dx2;
+    a.dtv = dtv;
+    const int ntiles = jtiles_for(NI, ny, nx, &a.nseg);
+    int resident = 0;
+#define CFD_JN(F)              \
+    switch (NI) {              \
+        case 8: F(8); break;   \
+        case 6: F(6); break;   \
+        default: F(4); break;  \
+    }
+#define CFD_RES(N_) resident = mask ? jresident_tiles<true, N_>() : jresident_tiles<false, N_>()
+    CFD_JN(CFD_RES)
+#undef CFD_RES
+    if (resident < 0) {
+        *rc = CFD_E_HIP;
+        set_error("jacobi2d persistent: occupancy query failed");
+        return 1;
+    }
+    if (ntiles > resident || ntiles > kJMaxTiles) return 0;  // the launch-per-pass path
+    const size_t plane = (size_t)ny * nx;
+    const size_t gbytes = sizeof(unsigned long long) * kJGSlots * plane;
+    char *p = static_cast<char *>(ring_for(gbytes + 256, rc));
+    if (!p) return 1;
+    a.G = reinterpret_cast<unsigned long long *>(p);
+    a.status = reinterpret_cast<int *>(p + gbytes);
+    // a stale granule of an earlier solve carries a valid-looking tag: reset the ring
+    if (hipMemsetAsync(p, 0, gbytes + 256, s) != hipSuccess) {
+        *rc = CFD_E_HIP;
+        set_error("jacobi2d persistent: ring reset failed");
+        return 1;
+    }
+#define CFD_LAUNCH(N_)                                                                                      \
+    do {                                                                                                    \
+        if (mask) hipLaunchKernelGGL((jacobi2d_persist<true, N_>), dim3(ntiles), dim3(1024), 0, s, a);      \
+        else hipLaunchKernelGGL((jacobi2d_persist<false, N_>), dim3(ntiles), dim3(1024), 0, s, a);          \
+    } while (0)
+    CFD_JN(CFD_LAUNCH)
+#undef CFD_LAUNCH
+#undef CFD_JN
+    hipLaunchKernelGGL(k_jp_status, dim3(1), dim3(1), 0, s, a.status, phi);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *rc = CFD_E_HIP;
+        set_error("jacobi2d persistent launch failed: %s", hipGetErrorString(e));
+    }
+    return 1;
+}
+
+}  // namespace cfd

@@ -354,6 +354,19 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
     const bool vec_ok = (nx % V == 0) && aligned16(src) && aligned16(phi) && aligned16(tmp);
     T *a = phi, *b = tmp;
     const int tk = timing_begin(s);
+    if constexpr (std::is_same_v<T, float>) {
+        // small f32 grids (those the launch-per-pass kernel would take): the
+        // whole solve as one persistent launch, any row length
+        if (tuning().j2_blocking == 0 && resid_every <= 0 && ny >= 3 &&
+            auto_levels2d<T>(ny, nx) != kDefaultLevels2d) {
+            int prc = CFD_OK;
+            if (jacobi2d_persist_solve(phi, src, pre, mask, ny, nx, dx2, dtv, iters, s, &prc)) {
+                if (prc) return prc;
+                timing_end(tk, s, iters);
+                return CFD_OK;
+            }
+        }
+    }
     if (tuning().j2_blocking != 1 && vec_ok && resid_every <= 0 && iters >= 2 && ny >= 3) {
         // temporally blocked: passes of K sweeps, the remainder last
         // small grids (auto depth 2) take the preloaded kernel, 4 sweeps a pass

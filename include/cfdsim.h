@@ -421,6 +421,11 @@ int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows);
  * tile), 3 = on with one exchange per colour level.  Its blocks are the
  * shared-row tile's (iterations per block as cfd_set_small2d_gs_iters). */
 int cfd_set_small2d_gs_persistent(int mode);
+/* Small-grid float32 Jacobi (cfd_jacobi2d_f32 on a grid the launch-per-pass
+ * kernel would take, more sweeps than one block) as one persistent launch:
+ * on = 0 default (on), 1 off, 2 on; sweeps_per_block 0 = default (8), or
+ * 4, 6, 8.  Its exchange ring lives in a library-owned device buffer. */
+int cfd_set_small2d_jacobi_persistent(int on, int sweeps_per_block);
 /* Diagnostics: the persistent GS writes 4 timestamps (100 MHz device clock)
  * per tile and block into buf -- block start, halo received, tile ready,
  * levels done; layout [block][tile][4] u64 -- when bytes covers the solve

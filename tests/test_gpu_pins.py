@@ -326,14 +326,44 @@ def test_rbgs2d_shared_rows_cylinder_grid(ni, iters, tol, persistent):
 @pytest.mark.parametrize("k,rw,vec", [(1, 1, 1), (3, 2, 1), (5, 1, 4), (8, 2, 4), (4, 2, 1)])
 def test_jacobi2d_small_shapes_bitexact(k, rw, vec):
     """The small-grid Jacobi kernel's non-default shapes (sweeps per launch
-    1..8, rows per wave, cells per lane) on the cylinder case's kind of grid."""
+    1..8, rows per wave, cells per lane) on the cylinder case's kind of grid
+    (the launch-per-pass path: the persistent solve off)."""
     call("cfd_set_small2d_shape", k, rw, vec, 0, 0, 0)
+    call("cfd_set_small2d_jacobi_persistent", 1, 0)
     rng = np.random.default_rng(k)
     div = rng.standard_normal((180, 600)).astype(np.float32)
     mask = rng.random(div.shape) < 0.03
     ref = oracle.jacobi2d(div, dx=20 / 599, dt=np.float32(5e-5), iters=37, mask=mask)
     phi = torch.zeros_like(dev(div))
     K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), dev(mask), 37)
+    assert np.array_equal(host(phi), ref)
+
+
+@pytest.mark.parametrize("ni", [4, 6, 8])
+@pytest.mark.parametrize("shape,iters,pre", [((180, 600), 1500, True), ((180, 600), 37, False),
+                                             ((36, 120), 9, True), ((53, 131), 17, False), ((3, 70), 12, True),
+                                             ((97, 64), 25, False)])
+def test_jacobi2d_persistent_bitexact(ni, shape, iters, pre):
+    """The small-grid Jacobi as one persistent launch (jacobi2d_persist): the
+    cylinder's grid at the reference's 1500 sweeps, ragged grids (tiles cut
+    by the edges, one tile row, a one-row interior), sweep counts that are no
+    multiple of the block, with and without the RHS workspace; the mask
+    covers interior and edge cells (edge ones become 0 too), phi starts
+    non-zero."""
+    call("cfd_set_small2d_jacobi_persistent", 2, ni)
+    rng = np.random.default_rng(ni * 1000 + iters)
+    div = rng.standard_normal(shape).astype(np.float32)
+    phi0 = rng.standard_normal(shape).astype(np.float32)
+    mask = rng.random(shape) < 0.03
+    mask[0, 5] = mask[-1, 7] = mask[shape[0] // 2, 0] = True
+    ref = oracle.jacobi2d(div, phi0, dx=20 / 599, dt=np.float32(5e-5), iters=iters, mask=mask)
+    phi = dev(phi0)
+    K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), dev(mask), iters,
+                            rhs_ws=torch.empty_like(phi) if pre else None)
+    assert np.array_equal(host(phi), ref)
+    # and again on the same ring (a stale granule must not pass for a new one)
+    phi = dev(phi0)
+    K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), dev(mask), iters)
     assert np.array_equal(host(phi), ref)
 
 
