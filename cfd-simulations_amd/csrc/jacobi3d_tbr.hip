@@ -65,6 +65,9 @@ __device__ inline __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, int p, in
 // as well: 2.97 ms at K = 3 -- the neighbouring tiles' halo re-reads then
 // miss L2.)
 constexpr int kStoreNt = 2;
+#ifndef CFD_TBR_SB
+#define CFD_TBR_SB 1
+#endif
 #ifndef CFD_TBR_EARLY
 #define CFD_TBR_EARLY 1
 #endif
@@ -963,7 +966,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, 0, 0x00020000);
                             __builtin_amdgcn_raw_buffer_store_b128(gv4f{0.f, 0.f, 0.f, 0.f}, ro, (int)kOob, 0, kStoreNt);
                         }
-                        __builtin_amdgcn_sched_barrier(0);
+                        if constexpr (CFD_TBR_SB) __builtin_amdgcn_sched_barrier(0);
                     }
                 }
                 trace_mark(a.trace, wv, z - zs, 3);
