@@ -32,8 +32,6 @@
 // that this tile consumed (hence nb >= 2 blocks, iterations > NI).  Every poll
 // is bounded (20 s of the 100 MHz clock), and the launcher checks that every
 // tile is resident at once.
-#include <mutex>
-
 #include "internal.hpp"
 
 namespace cfd {
@@ -43,6 +41,7 @@ constexpr int kJW = 16, kJRW = 2, kJT0 = kJW * kJRW;  // waves, rows per wave, t
 constexpr int kJGSlots = 3;
 constexpr int kJMaxTiles = 256;
 constexpr unsigned long long kJSpinLimit = 2000000000ull;  // 20 s at 100 MHz
+constexpr int kMaxDevices = 64;
 
 struct JPersistArgs {
     float *phi;         // in: the initial guess; out: the own cells of the result
@@ -206,30 +205,35 @@ int jresident_tiles() {
     return resident;
 }
 
-// The granule ring and the status word live in a library-owned device buffer
-// (per device, grown on demand, never shrunk): the Jacobi entry points take
-// no exchange workspace.  Growing it frees the old one (hipFree waits for the
-// device), so a process solving ever larger small grids pays that a few times.
+// The granule ring and the status word live in a library-owned device buffer,
+// one per host thread and device (the Jacobi entry points take no exchange
+// workspace), grown on demand and freed when the thread exits.  Solves that
+// share a ring are ordered: a solve on another stream than the ring's last
+// user first waits for that solve (an event), so two streams of one thread
+// never run on the same granules at once.
 struct JRing {
-    std::mutex mu;
-    void *p[64] = {};
-    size_t bytes[64] = {};
-};
-JRing &jring() {
-    static JRing r;
-    return r;
-}
-void *ring_for(size_t bytes, int *rc) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
-        *rc = CFD_E_HIP;
-        set_error("jacobi2d persistent: no device");
-        return nullptr;
+    void *p[kMaxDevices] = {};
+    size_t bytes[kMaxDevices] = {};
+    hipEvent_t done[kMaxDevices] = {};
+    hipStream_t last[kMaxDevices] = {};
+    ~JRing() {
+        for (int d = 0; d < kMaxDevices; ++d) {
+            if (done[d]) (void)hipEventDestroy(done[d]);
+            if (p[d]) (void)hipFree(p[d]);
+        }
     }
-    JRing &r = jring();
-    std::lock_guard<std::mutex> g(r.mu);
+};
+thread_local JRing t_ring;
+
+// the ring for device dev, at least `bytes`, ordered after its last user
+void *ring_acquire(int dev, size_t bytes, hipStream_t s, int *rc) {
+    JRing &r = t_ring;
     if (r.bytes[dev] < bytes) {
-        if (r.p[dev]) (void)hipFree(r.p[dev]);
+        if (r.p[dev]) {
+            // the old ring may still be in use by queued work
+            if (r.done[dev]) (void)hipEventSynchronize(r.done[dev]);
+            (void)hipFree(r.p[dev]);
+        }
         r.p[dev] = nullptr;
         r.bytes[dev] = 0;
         if (hipMalloc(&r.p[dev], bytes) != hipSuccess) {
@@ -239,7 +243,21 @@ void *ring_for(size_t bytes, int *rc) {
         }
         r.bytes[dev] = bytes;
     }
+    if (!r.done[dev] && hipEventCreateWithFlags(&r.done[dev], hipEventDisableTiming) != hipSuccess) {
+        *rc = CFD_E_HIP;
+        set_error("jacobi2d persistent: event creation failed");
+        return nullptr;
+    }
+    if (r.last[dev] != s && hipStreamWaitEvent(s, r.done[dev], 0) != hipSuccess) {
+        *rc = CFD_E_HIP;
+        set_error("jacobi2d persistent: stream ordering failed");
+        return nullptr;
+    }
     return r.p[dev];
+}
+void ring_release(int dev, hipStream_t s) {
+    JRing &r = t_ring;
+    if (hipEventRecord(r.done[dev], s) == hipSuccess) r.last[dev] = s;
 }
 
 }  // namespace
@@ -278,7 +296,13 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
     if (ntiles > resident || ntiles > kJMaxTiles) return 0;  // the launch-per-pass path
     const size_t plane = (size_t)ny * nx;
     const size_t gbytes = sizeof(unsigned long long) * kJGSlots * plane;
-    char *p = static_cast<char *>(ring_for(gbytes + 256, rc));
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+        *rc = CFD_E_HIP;
+        set_error("jacobi2d persistent: no device");
+        return 1;
+    }
+    char *p = static_cast<char *>(ring_acquire(dev, gbytes + 256, s, rc));
     if (!p) return 1;
     a.G = reinterpret_cast<unsigned long long *>(p);
     a.status = reinterpret_cast<int *>(p + gbytes);
@@ -297,6 +321,7 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
 #undef CFD_LAUNCH
 #undef CFD_JN
     hipLaunchKernelGGL(k_jp_status, dim3(1), dim3(1), 0, s, a.status, phi);
+    ring_release(dev, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *rc = CFD_E_HIP;
