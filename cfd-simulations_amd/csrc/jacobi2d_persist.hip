@@ -207,7 +207,9 @@ int jresident_tiles() {
 
 // The granule ring and the status word live in a library-owned device buffer,
 // one per host thread and device (the Jacobi entry points take no exchange
-// workspace), grown on demand and freed when the thread exits.  Solves that
+// workspace: 24 B per cell, 2.6 MB at 600 x 180), grown on demand and kept
+// for the life of the process (a destructor at thread exit could run after
+// the HIP runtime's teardown; a thread that exits leaves its ring).  Solves that
 // share a ring are ordered: a solve on another stream than the ring's last
 // user first waits for that solve (an event), so two streams of one thread
 // never run on the same granules at once.
@@ -216,12 +218,6 @@ struct JRing {
     size_t bytes[kMaxDevices] = {};
     hipEvent_t done[kMaxDevices] = {};
     hipStream_t last[kMaxDevices] = {};
-    ~JRing() {
-        for (int d = 0; d < kMaxDevices; ++d) {
-            if (done[d]) (void)hipEventDestroy(done[d]);
-            if (p[d]) (void)hipFree(p[d]);
-        }
-    }
 };
 thread_local JRing t_ring;
 
