@@ -367,6 +367,49 @@ def test_jacobi2d_persistent_bitexact(ni, shape, iters, pre):
     assert np.array_equal(host(phi), ref)
 
 
+def test_jacobi2d_persistent_streams_and_threads():
+    """The persistent Jacobi's library-owned ring: solves queued on two streams
+    of one thread (the second waits for the first), and two host threads with
+    a ring each, all equal to the oracle."""
+    import threading
+    shape, iters = (180, 600), 300
+    rng = np.random.default_rng(7)
+    cases = []
+    for _ in range(4):
+        div = rng.standard_normal(shape).astype(np.float32)
+        mask = rng.random(shape) < 0.03
+        cases.append((div, mask, oracle.jacobi2d(div, dx=20 / 599, dt=np.float32(5e-5), iters=iters, mask=mask)))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    out = []
+    for i, (div, mask, _) in enumerate(cases):
+        with torch.cuda.stream(streams[i % 2]):
+            phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+            K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), dev(mask), iters)
+            out.append(phi)
+    torch.cuda.synchronize()
+    for phi, (_, _, ref) in zip(out, cases):
+        assert np.array_equal(host(phi), ref)
+
+    res = [None] * len(cases)
+
+    def work(i):
+        div, mask, _ = cases[i]
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+            K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), dev(mask), iters)
+            s.synchronize()
+            res[i] = phi.cpu().numpy()
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(cases))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    for r, (_, _, ref) in zip(res, cases):
+        assert r is not None and np.array_equal(r, ref)
+
+
 # ------------------------------------------- zero-start solve, fused first pass
 def test_jacobi3d_1024_zero_start_bitexact(div1024):
     """cfd_jacobi3d_zero_f32 at the bench geometry: phi = zeros then 2..6 and
