@@ -442,8 +442,9 @@ int cfd_set_tbr_trace(void *buf, size_t bytes);
  * workgroup (1..16); zchunk = planes per workgroup (0 = auto). */
 int cfd_set_jacobi3d_config(int variant, int waves, int zchunk);
 /* Temporal blocking of the 3-D Jacobi solve (cfd_jacobi3d_f32 without mask
- * or residual): steps = sweeps fused per HBM pass (0 = auto, 1 = off, 2..4;
- * a remainder of iters % steps runs as a shorter pass); rows = output rows
+ * or residual): steps = sweeps fused per HBM pass (0 = auto: 4 since r03,
+ * 1 = off, 2..4; a remainder of iters % steps runs as a shorter pass, or,
+ * from zeros, as the fused first pass); rows = output rows
  * per tile of the 2-sweep kernel (0 auto, 5, 13); zchunk = planes per tile.
  * Fused or not, results are bit-identical.  The red-black GS solves run
  * fused out-of-place passes whenever blocking is not off: steps = their
