@@ -412,22 +412,24 @@ def test_jacobi2d_persistent_streams_and_threads():
 
 # ------------------------------------------- zero-start solve, fused first pass
 def test_jacobi3d_1024_zero_start_bitexact(div1024):
-    """cfd_jacobi3d_zero_f32 at the bench geometry: phi = zeros then 2..6 and
-    200 sweeps (the bench's step: a fused 2-sweep first pass that starts from
-    the zeros and forms the RHS workspace, then 66 passes of 3).  phi and the
-    workspace start as NaN garbage: the first pass must read neither."""
+    """cfd_jacobi3d_zero_f32 at the bench geometry: phi = zeros then 2..9 and
+    200 sweeps (the bench's step at the default 4 sweeps per pass: a fused
+    4-sweep first pass that starts from the zeros and forms the RHS
+    workspace, then 49 passes of 4; 7 and 9 sweeps open with a 3-sweep first
+    pass, 9 ends with a 2-sweep remainder).  phi and the workspace start as
+    NaN garbage: the first pass must read neither."""
     n = 1024
     h, dt = 1.0 / (n - 1), np.float32(5e-5)
     refs = {}
     ref = np.zeros_like(div1024)
-    for it in range(1, 7):
+    for it in range(1, 10):
         ref = oracle.jacobi3d(div1024, ref, h=h, dt=dt, iters=1, mt=True)
         refs[it] = ref
     d = dev(div1024)
     phi = torch.empty_like(d)
     tmp = torch.empty_like(d)
     rhs = torch.empty_like(d)
-    for iters in (2, 3, 4, 5, 6):
+    for iters in (2, 3, 4, 5, 6, 7, 8, 9):
         phi.fill_(float("nan"))
         tmp.fill_(float("nan"))
         rhs.fill_(float("nan"))
