@@ -420,6 +420,8 @@ def main():
         spl = (min(levels, plan.ghost) if use_slab and len(shape) == 3 else levels) if blocked else 1
     elif use_slab:  # slab passes: two iterations with 4-deep ghosts, else one
         spl = 2 if blocked and plan.ghost == 4 else 1
+    elif ARGS.tb_rows in (5, 13):  # the tuned 2-level GS kernel: one iteration per pass
+        spl = 1
     else:  # single GPU: half-sweeps per pass (--tb, or the library's auto: 4 = two iterations)
         spl = int(lib().cfd_get_rbgs3d_levels()) / 2 if blocked else 1
     launch_ms = sweep_ms * spl

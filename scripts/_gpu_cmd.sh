@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for w in jacobi3d_512 jacobi3d_channel; do timeout -k 10 300 python bench.py --workload $w > gpurun_out/b_$w.json 2>gpurun_out/b_$w.err; echo "$w rc=$?"; cut -c1-200 gpurun_out/b_$w.json; done
-timeout -k 10 300 python bench.py --workload rbgs3d_1024 > gpurun_out/b_rbgs3d_1024.json 2>gpurun_out/b_rbgs.err; echo "gs rc=$?"; cut -c1-200 gpurun_out/b_rbgs3d_1024.json
-timeout -k 10 300 python bench.py --workload jacobi2d_8192_f64 > gpurun_out/b_f64.json 2>gpurun_out/b_f64.err; echo "f64 rc=$?"; cut -c1-200 gpurun_out/b_f64.json
+timeout -k 10 1000 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/tall.log 2>&1; echo "tests rc=$?"; tail -3 gpurun_out/tall.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | tail -2
+timeout -k 10 300 python bench.py > gpurun_out/bench_final2.json 2>gpurun_out/bench_final2.err; echo "bench rc=$?"; cut -c1-400 gpurun_out/bench_final2.json
