@@ -60,6 +60,12 @@ WORKLOADS = {
     # config 1: lid-driven cavity 128^2, Re = 100, 500 Jacobi sweeps per pressure
     # solve; one step = one LidDrivenCavitySolver.time_step() (v5.py:375-441)
     "cavity2d_128": ((128, 128), "f32", 500, 12),
+    # the second north-star kernel: the fused advection-diffusion predictor
+    # (v5.py:388-403, kernels :127-176) over an 8192^2 SUPG field, scalar
+    # nu_eff (LES off), tau written: one step = one cfd_predictor2d call;
+    # 20 B per cell (u, v read; u*, v*, tau written), 40 B in float64
+    "predictor2d_8192": ((8192, 8192), "f32", 1, 20),
+    "predictor2d_8192_f64": ((8192, 8192), "f64", 1, 40),
 }
 GS_TOL = 1e-8  # OptimizedTurbulentConfig.pressure_tolerance (v5.py)
 
@@ -249,11 +255,91 @@ def cavity_bench():
     print(json.dumps(out), flush=True)
 
 
+def predictor_bench():
+    """The fused predictor (v5.py:388-403) on the 8192^2 grid of
+    OptimizedTurbulentConfig's domain: u, v ~ U(-1, 1) (seeded), SUPG, nu_eff =
+    nu + art_visc as a scalar (nu_t == 0 with LES off, v5.py:386-388), tau
+    written.  value = cells / s; roofline = algorithmic bytes (20 B per f32
+    cell, 40 B per f64) / the launch's HIP-event duration."""
+    import torch
+    import _pkgpath
+    _pkgpath.load()
+    from cfd_simulations_amd import kernels as K
+    from cfd_simulations_amd._lib import call
+    from cfd_simulations_amd.solver import OptimizedTurbulentConfig
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("the predictor workload is single-GPU")
+    shape, dt_name, _, bpc = WORKLOADS[ARGS.workload]
+    ny, nx = shape
+    f64 = dt_name == "f64"
+    tdt = torch.float64 if f64 else torch.float32
+    cfg = OptimizedTurbulentConfig(nx=nx, ny=ny)
+    nu_eff = (np.float64 if f64 else np.float32)(cfg.nu) + (np.float64 if f64 else np.float32)(cfg.artificial_viscosity)
+    dt = np.float32(2e-5)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    u = torch.rand(shape, generator=g, device="cuda", dtype=tdt) * 2 - 1
+    v = torch.rand(shape, generator=g, device="cuda", dtype=tdt) * 2 - 1
+    us, vs, tau = torch.empty_like(u), torch.empty_like(u), torch.empty_like(u)
+
+    def step():
+        K.predictor_fused(u, v, cfg.dx, cfg.dy, dt, float(nu_eff), True, us, vs, tau)
+    for _ in range(max(ARGS.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    call("cfd_timing_enable", 1)
+    t0 = time.perf_counter()
+    for _ in range(ARGS.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = ctypes.c_double()
+    nl = ctypes.c_longlong()
+    call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(nl), 1)
+    call("cfd_timing_enable", 0)
+    launch_ms = ms.value / max(nl.value, 1)
+    cells = ny * nx
+    alg = cells * bpc
+    achieved = alg / (launch_ms * 1e-3) / 1e9
+    kern = "k_predictor64<SUPG> (one thread per cell)" if f64 else "k_predictor_rows<SUPG, scalar nu> (row march)"
+    out = {
+        "metric": "Gcell-updates/s of the fused advection-diffusion predictor; achieved HBM GB/s vs peak",
+        "value": round(cells * ARGS.steps / elapsed / 1e9, 3), "unit": "Gcell-updates/s", "n_gpus": 1,
+        "steps": ARGS.steps, "warmup": ARGS.warmup, "ms_per_step": round(elapsed / ARGS.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": dt_name,
+        "data": "synthetic: u, v ~ U(-1, 1) seeded, on OptimizedTurbulentConfig's 20 x 4 domain (no dataset)",
+        "config": {"workload": f"predictor2d_supg_{ny}x{nx}_{dt_name}", "grid": [ny, nx], "use_supg": True,
+                   "nu_eff": "scalar (LES off)", "tau_written": True},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(ARGS.workload, 1),
+                     "kernel": kern, "bytes_per_cell": bpc, "cells_per_launch": cells,
+                     "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(launch_ms, 5)},
+        "cpu_baseline": None,
+    }
+    if not ARGS.no_cpu_baseline and not f64:
+        import oracle
+        rows = 1024
+        hu, hv = u[:rows].cpu().numpy(), v[:rows].cpu().numpy()
+        n = 0
+        t0 = time.perf_counter()
+        while n < 1 or (time.perf_counter() - t0 < 10.0 and n < 20):
+            oracle.predictor2d(hu, hv, nu_eff, dx=cfg.dx, dy=cfg.dy, dt=dt, use_supg=True)
+            n += 1
+        t = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": rows * nx * n / t / 1e9, "unit": "Gcell-updates/s", "cores": 1,
+                               "kind": "port",
+                               "sample": f"{rows}x{nx} rows of the grid, {n} calls of oracle.predictor2d (C "
+                                         f"restatement of v5.py:127-176, :388-403 with libm powf, serial); "
+                                         f"{t:.2f} s; host has {os.cpu_count()} logical CPUs, 1 used"}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     global ARGS
     ARGS = parse()
     if ARGS.workload == "cavity2d_128":
         return cavity_bench()
+    if ARGS.workload.startswith("predictor2d"):
+        return predictor_bench()
     import torch
     import torch.distributed as dist
     import _pkgpath

@@ -57,6 +57,8 @@ static Tuning process_defaults() {
         const int jn = env_int("CFD_J2P_NI", t.j2p_ni);
         t.j2p_ni = jn == 4 || jn == 6 || jn == 8 ? jn : t.j2p_ni;
         t.gs_pairs = env_int("CFD_GS_PAIRS", t.gs_pairs) != 0;
+        const int pv = env_int("CFD_PRED_VARIANT", t.pred_variant);
+        t.pred_variant = pv >= 0 && pv <= 2 ? pv : t.pred_variant;
         const int ni = env_int("CFD_GS_SMALL_NI", t.gs_ni);
         t.gs_ni = ni >= 1 && ni <= 4 ? ni : t.gs_ni;
         return t;

@@ -12,6 +12,7 @@
 // These kernels are one-pass per cell and HBM-bound; the fused predictor
 // reads u, v once (5-point neighbourhoods from L1/L2) and writes u*, v*, tau.
 #include "common.hpp"
+#include "internal.hpp"
 #include "libm_powf.hpp"
 
 namespace cfd {
@@ -43,12 +44,25 @@ static PredConst make_pred_const(double dx, double dy) {
 
 // compute_supg_stabilization_fast body, v5.py:155-161: vel_mag =
 // (u**2 + v**2) ** 0.5 on float32 scalars, i.e. libm powf three times
+// (powf_sq / powf_sqrt: glibc powf at y = 2 / 0.5 bit for bit, with a cheap
+// exact path away from rounding midpoints -- libm_powf.hpp)
 __device__ inline float supg_tau(float u, float v, float nu, float dt, const PredConst &k) {
-    const float vm = libm::powf(libm::powf(u, 2.0f) + libm::powf(v, 2.0f), 0.5f);
+    const float vm = libm::powf_sqrt(libm::powf_sq(u) + libm::powf_sq(v));
     if (vm > k.eps) {
         const float pe = (vm * k.h) / (nu + k.eps);
         const float half = pe / 2.0f;
         const float lim = half < 1.0f ? half : 1.0f;  // Python min(1.0, Pe/2.0)
+        return (k.h / (2.0f * vm)) * lim;
+    }
+    return dt / 2.0f;
+}
+// the same from |V|^2 = u**2 + v**2 already formed (the row-march predictor
+// forms the squares and roots of a lane's four cells in batches)
+__device__ inline float supg_tau_vm(float vm, float nu, float dt, const PredConst &k) {
+    if (vm > k.eps) {
+        const float pe = (vm * k.h) / (nu + k.eps);
+        const float half = pe / 2.0f;
+        const float lim = half < 1.0f ? half : 1.0f;
         return (k.h / (2.0f * vm)) * lim;
     }
     return dt / 2.0f;
@@ -161,6 +175,210 @@ __global__ __launch_bounds__(256) void k_predictor(const float *__restrict__ u,
     us[c] = uc + dt * (-cu + lu);
     vs[c] = vc + dt * (-cv + lv);
     if (SUPG && tau_out) tau_out[c] = t;
+}
+
+// ---- row-march predictor (r04): the fused predictor as a tiled stencil ------
+// One wave owns a 256-column segment of the grid (64 lanes x one float4 of 4
+// cells) and marches down a chunk of rows.  Rows i-1, i, i+1 of u and v sit in
+// a 4-slot register queue (row i+2 is in flight: each row is loaded once, as
+// one 1 KiB coalesced dwordx4 load per field, two steps ahead), rotated
+// through compile-time slots by a 4-fold unrolled march.  y-neighbours are
+// the queue's other slots, x-neighbours are the lane's own float4 plus DPP
+// wave shifts (wave_shr / wave_shl) for cells 0 and 3; the two columns just
+// outside the segment arrive as one dword load per row and field (lane 0:
+// column xs - 1, lane 63: column xs + 256) and enter the shifts as their
+// `old` operand.  The four waves of a workgroup take four adjacent segments;
+// workgroups are dealt chunk by chunk, XCD-swizzled, so the two halo rows a
+// chunk shares with its neighbours are read from the same L2.  u*, v* and tau
+// leave as streaming float4 stores.  HBM: u, v read once (+2 halo rows per
+// chunk), u*, v*, tau written once: 20 B per cell (16 without tau).
+//
+// |V| = (u**2 + v**2)**0.5 through powf_sq / powf_sqrt (libm_powf.hpp): a
+// lane's 8 squares, then its 4 roots, are formed exactly in double; the rare
+// ones near a float rounding midpoint (~0.36 % per call) are re-done by the
+// full glibc powf in a per-lane loop over a bit mask, so the wave runs ONE
+// powf body per batch at most instead of one per call.  Arithmetic per cell is
+// k_predictor's, operation for operation (bit-identical).
+typedef float pv4f __attribute__((ext_vector_type(4)));
+
+struct PredRowArgs {
+    const float *u, *v, *nu;  // nu: the nu_eff array, or null (nu_s)
+    float *us, *vs, *tau;     // tau: null = not written
+    float nu_s, dt;
+    int ny, nx, rows, nseg, groups;
+    PredConst k;
+};
+
+__device__ inline pv4f pld4(__amdgpu_buffer_rsrc_t r, uint32_t ofs) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)ofs, 0, 0);
+}
+__device__ inline float pld1(__amdgpu_buffer_rsrc_t r, uint32_t ofs) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)ofs, 0, 0));
+}
+// DPP wave shifts whose out-of-wave lane keeps `old` (bound_ctrl off)
+__device__ inline float shr_old(float old, float src) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x138, 0xf, 0xf, false));
+}
+__device__ inline float shl_old(float old, float src) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x130, 0xf, 0xf, false));
+}
+template <int N>
+__device__ inline float pick(const float (&a)[N], int q) {
+    float x = a[0];
+#pragma unroll
+    for (int c = 1; c < N; ++c) x = q == c ? a[c] : x;
+    return x;
+}
+template <int N>
+__device__ inline void place(float (&a)[N], int q, float r) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) a[c] = q == c ? r : a[c];
+}
+
+// |V| of a lane's four cells, v5.py:155, bit for bit
+__device__ inline void vel_mag4(const pv4f &u, const pv4f &v, float (&vm)[4]) {
+    float sq[8];
+    uint32_t slow = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const double a = (double)u[c] * (double)u[c], b = (double)v[c] * (double)v[c];
+        sq[c] = (float)a;
+        sq[4 + c] = (float)b;
+        slow |= (libm::powf_window_ok(a, libm::kPowfSqWin) ? 0u : 1u) << c;
+        slow |= (libm::powf_window_ok(b, libm::kPowfSqWin) ? 0u : 1u) << (4 + c);
+    }
+    if (slow) {
+        const float in[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+        do {
+            const int q = __builtin_ctz(slow);
+            place(sq, q, libm::powf(pick(in, q), 2.0f));
+            slow &= slow - 1;
+        } while (slow);
+    }
+    float s[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        s[c] = sq[c] + sq[4 + c];
+        const double d = __builtin_sqrt((double)s[c]);
+        vm[c] = (float)d;
+        slow |= (s[c] > 0.0f && libm::powf_window_ok(d, libm::kPowfSqrtWin) ? 0u : 1u) << c;
+    }
+    if (slow) {
+        do {
+            const int q = __builtin_ctz(slow);
+            place(vm, q, libm::powf(pick(s, q), 0.5f));
+            slow &= slow - 1;
+        } while (slow);
+    }
+}
+
+template <bool SUPG, bool NUA>
+__global__ __launch_bounds__(256) void k_predictor_rows(PredRowArgs a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int b = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+    const int chunk = b / a.groups;
+    const int seg = (b - chunk * a.groups) * 4 + wv;
+    if (seg >= a.nseg) return;
+    const int ny = a.ny, nx = a.nx;
+    const int r0 = chunk * a.rows;
+    const int r1 = min(r0 + a.rows, ny);
+    const int xs = seg * 256;
+    const int x0 = xs + lane * 4;
+    const bool lane_in = x0 < nx;  // nx % 4 == 0: a lane's float4 is all in or all out
+    const int bytes = (int)((size_t)ny * nx * sizeof(float));
+    const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.u), 0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.v), 0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rn =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(NUA ? a.nu : a.u), 0, NUA ? bytes : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rus = __builtin_amdgcn_make_buffer_rsrc(a.us, 0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rvs = __builtin_amdgcn_make_buffer_rsrc(a.vs, 0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(a.tau ? a.tau : a.us, 0, a.tau ? bytes : 0, 0x00020000);
+    // byte offset of this lane's float4 in row i (kOob outside the grid: reads 0, stores dropped)
+    auto rofs = [&](int i) -> uint32_t {
+        return (i >= 0 && i < ny && lane_in) ? (uint32_t)(((size_t)i * nx + x0) * sizeof(float)) : kOob;
+    };
+    // the segment's x-halo cells of row i: lane 0 column xs - 1, lane 63 column xs + 256
+    const int hx = lane == 0 ? xs - 1 : (lane == kWave - 1 ? xs + 256 : -1);
+    const bool h_in = hx >= 0 && hx < nx;
+    auto hofs = [&](int i) -> uint32_t {
+        return (i >= 0 && i < ny && h_in) ? (uint32_t)(((size_t)i * nx + hx) * sizeof(float)) : kOob;
+    };
+    const bool c0_in = x0 >= 1;           // cell 0 off the x = 0 face
+    const bool c3_in = x0 + 3 <= nx - 2;  // cell 3 off the x = nx-1 face (cells 1, 2 never touch one)
+    const float dt = a.dt;
+
+    pv4f U[4], V[4], NU[4];
+    float HU[4], HV[4];
+    U[3] = pld4(ru, rofs(r0 - 1));
+    V[3] = pld4(rv, rofs(r0 - 1));
+    U[0] = pld4(ru, rofs(r0));
+    V[0] = pld4(rv, rofs(r0));
+    HU[0] = pld1(ru, hofs(r0));
+    HV[0] = pld1(rv, hofs(r0));
+    U[1] = pld4(ru, rofs(r0 + 1));
+    V[1] = pld4(rv, rofs(r0 + 1));
+    HU[1] = pld1(ru, hofs(r0 + 1));
+    HV[1] = pld1(rv, hofs(r0 + 1));
+    if (NUA) {
+        NU[0] = pld4(rn, rofs(r0));
+        NU[1] = pld4(rn, rofs(r0 + 1));
+    }
+    for (int i0 = r0; i0 < r1; i0 += 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = i0 + q;
+            if (i >= r1) break;
+            // two rows ahead: row i+2 (and its halo cells / nu row)
+            U[(q + 2) & 3] = pld4(ru, rofs(i + 2));
+            V[(q + 2) & 3] = pld4(rv, rofs(i + 2));
+            HU[(q + 2) & 3] = pld1(ru, hofs(i + 2));
+            HV[(q + 2) & 3] = pld1(rv, hofs(i + 2));
+            if (NUA) NU[(q + 2) & 3] = pld4(rn, rofs(i + 2));
+            const pv4f uc = U[q], vc = V[q];
+            pv4f uo = uc, vo = vc, to = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (i >= 1 && i <= ny - 2) {  // wave-uniform: boundary rows keep u* = u + dt*(-0 + 0)
+                const pv4f uS = U[(q + 3) & 3], uN = U[(q + 1) & 3];
+                const pv4f vS = V[(q + 3) & 3], vN = V[(q + 1) & 3];
+                const float uE[4] = {uc[1], uc[2], uc[3], shl_old(HU[q], uc[0])};
+                const float uW[4] = {shr_old(HU[q], uc[3]), uc[0], uc[1], uc[2]};
+                const float vE[4] = {vc[1], vc[2], vc[3], shl_old(HV[q], vc[0])};
+                const float vW[4] = {shr_old(HV[q], vc[3]), vc[0], vc[1], vc[2]};
+                float vm[4];
+                if (SUPG) vel_mag4(uc, vc, vm);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float nu = NUA ? NU[q][c] : a.nu_s;
+                    float cu, cv, t = 0.0f;
+                    if (SUPG) {
+                        t = supg_tau_vm(vm[c], nu, dt, a.k);
+                        cu = conv_supg(uc[c], vc[c], uc[c], uE[c], uW[c], uN[c], uS[c], t, a.k);
+                        cv = conv_supg(uc[c], vc[c], vc[c], vE[c], vW[c], vN[c], vS[c], t, a.k);
+                    } else {
+                        cu = conv_upwind(uc[c], vc[c], uc[c], uE[c], uW[c], uN[c], uS[c], a.k);
+                        cv = conv_upwind(uc[c], vc[c], vc[c], vE[c], vW[c], vN[c], vS[c], a.k);
+                    }
+                    const float lu = laplacian(nu, uc[c], uE[c], uW[c], uN[c], uS[c], a.k);
+                    const float lv = laplacian(nu, vc[c], vE[c], vW[c], vN[c], vS[c], a.k);
+                    const bool in = c == 0 ? c0_in : (c == 3 ? c3_in : true);
+                    // a face cell: conv = lap = tau = 0 (np.zeros_like rings)
+                    uo[c] = uc[c] + dt * (-(in ? cu : 0.0f) + (in ? lu : 0.0f));
+                    vo[c] = vc[c] + dt * (-(in ? cv : 0.0f) + (in ? lv : 0.0f));
+                    to[c] = in ? t : 0.0f;
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    uo[c] = uc[c] + dt * (-0.0f + 0.0f);
+                    vo[c] = vc[c] + dt * (-0.0f + 0.0f);
+                }
+            }
+            const uint32_t o = rofs(i);
+            __builtin_amdgcn_raw_buffer_store_b128(uo, rus, (int)o, 0, 2 /* nt */);
+            __builtin_amdgcn_raw_buffer_store_b128(vo, rvs, (int)o, 0, 2);
+            if (SUPG && a.tau) __builtin_amdgcn_raw_buffer_store_b128(to, rt, (int)o, 0, 2);
+        }
+    }
 }
 
 // compute_divergence_fast, v5.py:178-187 (+ max|div| diagnostic, v5.py:410)
@@ -777,14 +995,25 @@ __global__ void k_nonfinite(const float *__restrict__ a, const float *__restrict
 }
 
 // NumPy float32 scalar power (glibc powf, libm_powf.hpp) elementwise: the
-// parity hook for the device powf the SUPG tau uses.
+// parity hook for the device powf the SUPG tau uses -- at y = 2 and 0.5 the
+// exact-path forms it calls (powf_sq / powf_sqrt), else the restatement.
 __global__ void k_numpy_powf(const float *__restrict__ x, float y, float *__restrict__ out, size_t n) {
     for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < n;
          c += (size_t)gridDim.x * blockDim.x)
-        out[c] = libm::powf(x[c], y);
+        out[c] = y == 2.0f ? libm::powf_sq(x[c]) : (y == 0.5f ? libm::powf_sqrt(x[c]) : libm::powf(x[c], y));
 }
 
 static dim3 grid2d(int ny, int nx) { return dim3(ceil_div(nx, 256), ny); }
+
+// workgroups of the row-march predictor resident on the device at once
+static int pred_rows_resident(bool supg, bool nua) {
+    int dev = 0, cus = 256, per = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const void *f = supg ? (nua ? (const void *)k_predictor_rows<true, true> : (const void *)k_predictor_rows<true, false>)
+                         : (nua ? (const void *)k_predictor_rows<false, true> : (const void *)k_predictor_rows<false, false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per < 1) per = 1;
+    return per * cus;
+}
 static int grid1d(size_t n) {
     long b = (long)((n + 255) / 256);
     if (b > 2048) b = 2048;
@@ -848,13 +1077,61 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
                 "predictor2d: outputs must not alias inputs");
     CFD_SHAPE2D(ny, nx);
     const PredConst k = make_pred_const(dx, dy);
-    if (use_supg)
-        hipLaunchKernelGGL(k_predictor<true>, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u, v,
-                           nu_eff, nu_eff_scalar, u_star, v_star, tau, ny, nx, dt, k);
-    else
-        hipLaunchKernelGGL(k_predictor<false>, grid2d(ny, nx), dim3(256), 0, as_stream(stream), u,
-                           v, nu_eff, nu_eff_scalar, u_star, v_star, tau, ny, nx, dt, k);
+    hipStream_t s = as_stream(stream);
+    const bool rows_ok = nx % 4 == 0 && (size_t)ny * nx * sizeof(float) < ((size_t)1 << 31) && aligned16(u) &&
+                         aligned16(v) && aligned16(u_star) && aligned16(v_star) && (!tau || aligned16(tau)) &&
+                         (!nu_eff || aligned16(nu_eff));
+    const int tk = timing_begin(s);
+    if (tuning().pred_variant != 1 && rows_ok) {
+        PredRowArgs a;
+        a.u = u;
+        a.v = v;
+        a.nu = nu_eff;
+        a.us = u_star;
+        a.vs = v_star;
+        a.tau = use_supg ? tau : nullptr;
+        a.nu_s = nu_eff_scalar;
+        a.dt = dt;
+        a.ny = ny;
+        a.nx = nx;
+        a.nseg = ceil_div(nx, 256);
+        a.groups = ceil_div(a.nseg, 4);
+        a.k = k;
+        // rows per chunk: every workgroup resident at once (one round at the
+        // kernel's occupancy), chunks of at least 8 rows (2 halo rows each)
+        a.rows = tuning().pred_rows;
+        if (a.rows <= 0) {
+            const int resident = pred_rows_resident(use_supg != 0, nu_eff != nullptr);
+            const int chunks = resident / a.groups > 0 ? resident / a.groups : 1;
+            a.rows = ceil_div(ny, chunks);
+            if (a.rows < 8) a.rows = 8;
+        }
+        const int nblk = a.groups * ceil_div(ny, a.rows);
+        if (use_supg) {
+            if (nu_eff) hipLaunchKernelGGL((k_predictor_rows<true, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_predictor_rows<true, false>), dim3(nblk), dim3(256), 0, s, a);
+        } else {
+            if (nu_eff) hipLaunchKernelGGL((k_predictor_rows<false, true>), dim3(nblk), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_predictor_rows<false, false>), dim3(nblk), dim3(256), 0, s, a);
+        }
+    } else if (use_supg) {
+        hipLaunchKernelGGL(k_predictor<true>, grid2d(ny, nx), dim3(256), 0, s, u, v, nu_eff, nu_eff_scalar, u_star,
+                           v_star, tau, ny, nx, dt, k);
+    } else {
+        hipLaunchKernelGGL(k_predictor<false>, grid2d(ny, nx), dim3(256), 0, s, u, v, nu_eff, nu_eff_scalar, u_star,
+                           v_star, tau, ny, nx, dt, k);
+    }
+    timing_end(tk, s, 1);
     CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+// 0: auto (row march when the shape allows it), 1: one thread per cell
+// (k_predictor), 2: row march; rows per chunk (0: auto)
+int cfd_set_predictor2d_config(int variant, int rows) {
+    CFD_REQUIRE(variant >= 0 && variant <= 2 && rows >= 0, "predictor2d config: variant 0..2, rows >= 0");
+    tuning().pred_variant = variant;
+    tuning().pred_rows = rows;
     return CFD_OK;
 }
 

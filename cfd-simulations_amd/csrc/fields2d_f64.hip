@@ -504,12 +504,14 @@ int cfd_predictor2d_f64(const double *u, const double *v, const double *nu_eff, 
                 "predictor2d_f64: outputs must not alias inputs");
     CFD_SHAPE2D64(ny, nx);
     const Pred64 k = make_pred64(dx, dy);
+    const int tk = timing_begin(as_stream(stream));
     if (use_supg)
         hipLaunchKernelGGL(k_predictor64<true>, grid2d64(ny, nx), dim3(256), 0, as_stream(stream), u, v, nu_eff,
                            nu_eff_scalar, u_star, v_star, tau, ny, nx, dt, k);
     else
         hipLaunchKernelGGL(k_predictor64<false>, grid2d64(ny, nx), dim3(256), 0, as_stream(stream), u, v, nu_eff,
                            nu_eff_scalar, u_star, v_star, tau, ny, nx, dt, k);
+    timing_end(tk, as_stream(stream), 1);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }

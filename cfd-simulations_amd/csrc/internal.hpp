@@ -50,6 +50,10 @@ struct Tuning {
     // diagnostics: the tall-tile kernels' per-wave step timestamps (workgroup
     // 0, 64 steps, 5 marks each, 16 waves' worth: 40 KiB) into this buffer
     void *tbr_trace = nullptr;
+    // fused 2-D predictor (cfd_predictor2d_f32): 0 auto (the row march when
+    // nx % 4 == 0 and the arrays are 16-byte aligned), 1 one thread per cell,
+    // 2 row march; rows per chunk of the row march (0: one resident round)
+    int pred_variant = 0, pred_rows = 0;
 };
 Tuning &tuning();
 

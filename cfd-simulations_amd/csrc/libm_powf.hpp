@@ -20,23 +20,63 @@
 // them too.  tests/test_gpu_parity.py checks this device copy against the
 // oracle's libm calls.  No multiply-add is fused here (-ffp-contract=off).
 #pragma once
+#ifdef CFD_LIBM_HOST
+#include <cstdint>
+#include <cstring>
+#include <cmath>
+#define CFD_HDF inline
+#define CFD_LIBMF_TABLE static
+#define CFD_SQRT_D(x) std::sqrt(x)
+#else
 #include "common.hpp"
+#define CFD_HDF __device__ inline
+#define CFD_LIBMF_TABLE __device__ __constant__
+#define CFD_SQRT_D(x) __builtin_sqrt(x)
+#endif
+// fast-path windows: oracle/powf_window.cpp measure (1.05x the largest error + 4)
+#ifndef CFD_POWF_SQ_WIN
+#define CFD_POWF_SQ_WIN 952545u
+#endif
+#ifndef CFD_POWF_SQRT_WIN
+#define CFD_POWF_SQRT_WIN 931768u
+#endif
 
 namespace cfd {
 namespace libm {
 
-__device__ __constant__ const double kLog2InvC[16] = {
+CFD_HDF uint32_t asu32f(float x) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    return u;
+}
+CFD_HDF float asf32u(uint32_t u) {
+    float x;
+    memcpy(&x, &u, 4);
+    return x;
+}
+CFD_HDF uint64_t asu64d(double x) {
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    return u;
+}
+CFD_HDF double asf64d(uint64_t u) {
+    double x;
+    memcpy(&x, &u, 8);
+    return x;
+}
+
+CFD_LIBMF_TABLE const double kLog2InvC[16] = {
     0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
     0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
     0x1.0953f419900a7p+0, 0x1p+0,               0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
     0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
-__device__ __constant__ const double kLog2C[16] = {
+CFD_LIBMF_TABLE const double kLog2C[16] = {
     -0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2,
     -0x1.01d9bf3f2b631p-2, -0x1.97c1d1b3b7afp-3,  -0x1.2f9e393af3c9fp-3, -0x1.960cbbf788d5cp-4,
     -0x1.a6f9db6475fcep-5, 0x0p+0,                0x1.338ca9f24f53dp-4,  0x1.476a9543891bap-3,
     0x1.e840b4ac4e4d2p-3,  0x1.40645f0c6651cp-2,  0x1.88e9c2c1b9ff8p-2,  0x1.ce0a44eb17bccp-2};
 // tab[i] = bits(2^(i/32)) - (i << 47)
-__device__ __constant__ const unsigned long long kExp2Tab[32] = {
+CFD_LIBMF_TABLE const unsigned long long kExp2Tab[32] = {
     0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
     0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
     0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
@@ -46,9 +86,9 @@ __device__ __constant__ const unsigned long long kExp2Tab[32] = {
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
 
-__device__ inline bool zeroinfnan(uint32_t i) { return 2u * i - 1u >= 2u * 0x7f800000u - 1u; }
+CFD_HDF bool zeroinfnan(uint32_t i) { return 2u * i - 1u >= 2u * 0x7f800000u - 1u; }
 // 0: not an integer, 1: odd integer, 2: even integer
-__device__ inline int checkint(uint32_t iy) {
+CFD_HDF int checkint(uint32_t iy) {
     const int e = iy >> 23 & 0xff;
     if (e < 0x7f) return 0;
     if (e > 0x7f + 23) return 2;
@@ -57,10 +97,49 @@ __device__ inline int checkint(uint32_t iy) {
     return 2;
 }
 
-__device__ inline float powf(float x, float y) {
+// log2(x) for a positive normal(ised) float's bits (POWF_SCALE_BITS = 0 on x86_64)
+CFD_HDF double powf_log2(uint32_t ix) {
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (tmp >> 19) % 16;
+    const uint32_t top = tmp & 0xff800000u;
+    const uint32_t iz = ix - top;
+    const int k = (int32_t)top >> 23;
+    const double invc = kLog2InvC[i], logc = kLog2C[i];
+    const double z = (double)asf32u(iz);
+    const double r = z * invc - 1.0;
+    const double y0 = logc + (double)k;
+    const double r2 = r * r;
+    double yy = 0x1.27616c9496e0bp-2 * r + -0x1.71969a075c67ap-2;
+    const double p = 0x1.ec70a6ca7baddp-2 * r + -0x1.7154748bef6c8p-1;
+    const double r4 = r2 * r2;
+    double q = 0x1.71547652ab82bp+0 * r + y0;
+    q = p * r2 + q;
+    yy = yy * r4 + q;
+    return yy;
+}
+
+// 2^ylogx in double, before the final rounding to float (EXP2F_TABLE_BITS = 5,
+// shift 0x1.8p+52 / 32)
+CFD_HDF double powf_exp2(double ylogx, uint32_t sign_bias) {
+    double kd = ylogx + 0x1.8p+47;
+    const unsigned long long ki = asu64d(kd);
+    kd -= 0x1.8p+47;
+    const double rr = ylogx - kd;
+    unsigned long long t = kExp2Tab[ki % 32];
+    t += (ki + sign_bias) << 47;
+    const double s = asf64d(t);
+    const double zz = 0x1.c6af84b912394p-5 * rr + 0x1.ebfce50fac4f3p-3;
+    const double rr2 = rr * rr;
+    double e = 0x1.62e42ff0c52d6p-1 * rr + 1.0;
+    e = zz * rr2 + e;
+    e = e * s;
+    return e;
+}
+
+CFD_HDF float powf(float x, float y) {
     uint32_t sign_bias = 0;
-    uint32_t ix = __float_as_uint(x);
-    const uint32_t iy = __float_as_uint(y);
+    uint32_t ix = asu32f(x);
+    const uint32_t iy = asu32f(y);
     if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u || zeroinfnan(iy)) {
         // x < 0x1p-126, inf or nan; or y is 0, inf or nan
         if (zeroinfnan(iy)) {
@@ -78,53 +157,64 @@ __device__ inline float powf(float x, float y) {
         }
         if (ix & 0x80000000u) {  // finite x < 0
             const int yint = checkint(iy);
-            if (yint == 0) return __builtin_nanf("");
+            if (yint == 0) return asf32u(0x7fc00000u);
             if (yint == 1) sign_bias = 1u << 16;  // SIGN_BIAS = 1 << (EXP2F_TABLE_BITS + 11)
             ix &= 0x7fffffffu;
         }
         if (ix < 0x00800000u) {  // subnormal x: normalise
-            ix = __float_as_uint(x * 0x1p23f);
+            ix = asu32f(x * 0x1p23f);
             ix &= 0x7fffffffu;
             ix -= 23u << 23;
         }
     }
-    // log2 of x (POWF_SCALE_BITS = 0 on x86_64)
-    const uint32_t tmp = ix - 0x3f330000u;
-    const int i = (tmp >> 19) % 16;
-    const uint32_t top = tmp & 0xff800000u;
-    const uint32_t iz = ix - top;
-    const int k = (int32_t)top >> 23;
-    const double invc = kLog2InvC[i], logc = kLog2C[i];
-    const double z = (double)__uint_as_float(iz);
-    const double r = z * invc - 1.0;
-    const double y0 = logc + (double)k;
-    const double r2 = r * r;
-    double yy = 0x1.27616c9496e0bp-2 * r + -0x1.71969a075c67ap-2;
-    const double p = 0x1.ec70a6ca7baddp-2 * r + -0x1.7154748bef6c8p-1;
-    const double r4 = r2 * r2;
-    double q = 0x1.71547652ab82bp+0 * r + y0;
-    q = p * r2 + q;
-    yy = yy * r4 + q;
-    const double ylogx = (double)y * yy;
-    if (((unsigned long long)__double_as_longlong(ylogx) >> 47 & 0xffff) >=
-        ((unsigned long long)__double_as_longlong(126.0) >> 47)) {
-        if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -__builtin_inff() : __builtin_inff();
+    const double ylogx = (double)y * powf_log2(ix);
+    if ((asu64d(ylogx) >> 47 & 0xffff) >=
+        (asu64d(126.0) >> 47)) {
+        if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -asf32u(0x7f800000u) : asf32u(0x7f800000u);
         if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
     }
-    // exp2 (EXP2F_TABLE_BITS = 5, shift 0x1.8p+52 / 32)
-    double kd = ylogx + 0x1.8p+47;
-    const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
-    kd -= 0x1.8p+47;
-    const double rr = ylogx - kd;
-    unsigned long long t = kExp2Tab[ki % 32];
-    t += (ki + sign_bias) << 47;
-    const double s = __longlong_as_double((long long)t);
-    const double zz = 0x1.c6af84b912394p-5 * rr + 0x1.ebfce50fac4f3p-3;
-    const double rr2 = rr * rr;
-    double e = 0x1.62e42ff0c52d6p-1 * rr + 1.0;
-    e = zz * rr2 + e;
-    e = e * s;
-    return (float)e;
+    return (float)powf_exp2(ylogx, sign_bias);
+}
+
+// ---- fast exact paths for the two exponents the reference uses ------------
+// powf(x, 2) and powf(x, 0.5) are x*x and sqrt(x) computed in double and
+// rounded once to float, except that glibc's double result carries a small
+// error before that rounding.  It can only change the rounded float when the
+// exact value lies within that error of a rounding midpoint.  So: form the
+// exact square (48 significant bits: exact in double) or the double sqrt, and
+// look at the 29 bits below the float's last place; if they are at least
+// kPowfWin units (of 2^-29 float ulp) away from the midpoint 2^28, return the
+// rounded exact value; otherwise (and for zero, subnormal, huge, inf or nan
+// inputs) run the full powf.  kPowfWin is 1.05x (+4) the largest |e - exact| glibc's
+// algorithm shows over EVERY float input (oracle/powf_window.cpp measures it:
+// y = 2 over all 2^32 floats, y = 0.5 over all 2^31 non-negative ones), and the
+// same program checks powf_sq / powf_sqrt against libm's powf for every
+// input, bit for bit.  A lane leaves the fast path with probability ~2 *
+// kPowfWin / 2^29 per call.
+constexpr uint32_t kPowfSqWin = CFD_POWF_SQ_WIN;
+constexpr uint32_t kPowfSqrtWin = CFD_POWF_SQRT_WIN;
+
+CFD_HDF bool powf_window_ok(double d, uint32_t win) {
+    const uint64_t b = asu64d(d);
+    const uint32_t ex = (uint32_t)(b >> 52) & 0x7ffu;
+    const int32_t frac = (int32_t)(uint32_t)(b & 0x1fffffffull) - (1 << 28);
+    const uint32_t dist = (uint32_t)(frac < 0 ? -frac : frac);
+    // d a positive float-normal value below 2^127 (so (float)d cannot overflow)
+    return (ex - (1023u - 126u)) < 253u && dist >= win;
+}
+
+// NumPy float32 scalar x**2, bit for bit (glibc powf(x, 2.0f))
+CFD_HDF float powf_sq(float x) {
+    const double d = (double)x * (double)x;
+    if (powf_window_ok(d, kPowfSqWin)) return (float)d;
+    return powf(x, 2.0f);
+}
+
+// NumPy float32 scalar x**0.5, bit for bit (glibc powf(x, 0.5f))
+CFD_HDF float powf_sqrt(float x) {
+    const double d = CFD_SQRT_D((double)x);
+    if (x > 0.0f && powf_window_ok(d, kPowfSqrtWin)) return (float)d;
+    return powf(x, 0.5f);
 }
 
 }  // namespace libm

@@ -165,6 +165,12 @@ int cfd_laplacian2d_f32(const float *phi, const float *nu_eff, float nu_eff_scal
 int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, float nu_eff_scalar,
                         float *u_star, float *v_star, float *tau, int ny, int nx,
                         double dx, double dy, float dt, int use_supg, void *stream);
+/* Kernel of cfd_predictor2d_f32 (tuning, per host thread; same bits either
+ * way): variant 0 = auto (the row-march tile kernel when nx % 4 == 0, every
+ * array 16-byte aligned and ny*nx < 2^29; else one thread per cell), 1 = one
+ * thread per cell, 2 = row march where it applies; rows = rows per row-march
+ * chunk (0 = auto: every workgroup resident in one round). */
+int cfd_set_predictor2d_config(int variant, int rows);
 
 /* compute_divergence_fast, v5.py:178-187.  absmax (device float*, optional):
  * receives max|div| (the v5.py:410 diagnostic); must be zeroed by the caller. */

@@ -40,6 +40,15 @@ for s in "$@"; do
     benchch) step benchch 600 python bench.py --workload jacobi3d_channel --no-cpu-baseline ;;
     testsk) step pytest_k 900 python -m pytest tests -m gpu -q -k "k_levels or variants_agree or temporal or full_size" ;;
     ksweep) step ksweep 900 bash -c 'for cfg in ${KSWEEP:-"3 0 1 0" "3 16 2 0" "3 16 1 256" "4 0 1 0" "2 0 1 0"}; do set -- $cfg; echo "K=$1 rows=$2 PD=$3 zchunk=$4"; python bench.py --no-cpu-baseline --steps 5 --tb $1 --tb-rows $2 --tb-prefetch $3 --tb-zchunk $4 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
+    testspred) step pytest_pred 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "predictor or powf or time_step or golden" ;;
+    benchpred) step benchpred 600 python bench.py --workload predictor2d_8192 --steps 20 --warmup 3 ;;
+    benchpred64) step benchpred64 600 python bench.py --workload predictor2d_8192_f64 --steps 20 --warmup 3 ;;
+    benchpredv1) step benchpredv1 600 env CFD_PRED_VARIANT=1 python bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    profpred) step profpred 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profpred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    profpred64) step profpred64 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profpred64 -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    pmc_fetch_pred) step pmc_fetch_pred 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_pred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline ;;
+    pmc_write_pred) step pmc_write_pred 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_pred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline ;;
+    sq_pred) step sq_pred 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES -d gpurun_out/sq_pred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline ;;
     tests2d) step pytest_2d 900 python -m pytest tests -m gpu -q -k "jacobi2d or rbgs2d or time_step or golden" ;;
     sweep2d) step sweep2d 900 bash -c 'for K in ${K2D:-8 10 12}; do echo "K=$K"; python bench.py --workload jacobi2d_8192_f64 --no-cpu-baseline --steps 3 --tb $K | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
     testslocal) step pytest_local 900 python -m pytest tests -m gpu -q -x -k "local_group" ;;

@@ -199,7 +199,14 @@ def test_device_powf_is_libm(y):
     extra = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-45, 1e-38, 3.4e38, 5.0, 0.1],
                      np.float32)
     vel = rng.uniform(-5, 5, 1 << 20).astype(np.float32)
-    x = np.concatenate([x, extra, vel, vel * vel])
+    # values whose exact square / root lies near a float rounding midpoint:
+    # the exact-path forms (powf_sq / powf_sqrt) hand these to the full powf
+    cand = rng.uniform(0.01, 8.0, 1 << 22).astype(np.float32)
+    d = cand.astype(np.float64) ** 2 if y == 2.0 else np.sqrt(cand.astype(np.float64))
+    lo = (d.view(np.uint64) & np.uint64((1 << 29) - 1)).astype(np.int64) - (1 << 28)
+    near = cand[np.abs(lo) < 2_000_000]
+    assert near.size > 1000
+    x = np.concatenate([x, extra, vel, vel * vel, near])
     if y == 0.5:
         x = np.abs(x)
     ref = oracle.numpy_powf(x, y)
@@ -210,7 +217,8 @@ def test_device_powf_is_libm(y):
     same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
     assert same.all(), x[~same][:8]
     if y == 2.0:
-        assert (ref[-2 * vel.size:-vel.size] != vel * vel).any()  # the case a plain u*u misses
+        sq = ref[-2 * vel.size - near.size:-vel.size - near.size]
+        assert (sq != vel * vel).any()  # the case a plain u*u misses
 
 
 @pytest.mark.parametrize("y", [2.0, 0.5])
