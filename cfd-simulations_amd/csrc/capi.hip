@@ -1,3 +1,4 @@
+#include <mutex>
 // capi.hip -- error reporting, identification and sweep timing of libcfdsim.
 #include <cstring>
 #include <vector>
@@ -93,6 +94,44 @@ void timing_end(int k, hipStream_t s, long long sweeps) {
     g_timing.sweeps[k] = sweeps;
     (void)hipEventRecord(g_timing.stop[k], s);
 }
+
+int *persist_fail_word() {
+    static std::mutex mu;
+    static int *word[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!word[dev]) {
+        int *p = nullptr;
+        if (hipMalloc(&p, 256) != hipSuccess) return nullptr;
+        if (hipMemset(p, 0, 256) != hipSuccess) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        word[dev] = p;
+    }
+    return word[dev];
+}
+
+int launch_persistent(const void *f, int nblocks, int threads, void *args, hipStream_t s) {
+    void *kargs[] = {args};
+    hipError_t e;
+    if (tuning().persist_coop) {
+        e = hipLaunchCooperativeKernel(f, dim3(nblocks), dim3(threads), kargs, 0, s);
+        if (e == hipErrorCooperativeLaunchTooLarge) {
+            (void)hipGetLastError();  // clear it: the caller runs the launch-per-pass path
+            return 0;
+        }
+    } else {
+        e = hipLaunchKernel(f, dim3(nblocks), dim3(threads), kargs, 0, s);
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("persistent launch failed: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 1;
+}
 }  // namespace cfd
 
 using namespace cfd;
@@ -104,6 +143,32 @@ const char *cfd_device_arch(void) { return "gfx950"; }
 
 int cfd_reset_tuning(void) {
     tuning() = process_defaults();
+    return CFD_OK;
+}
+
+int cfd_set_persistent_launch(int cooperative, long long poll_ticks) {
+    CFD_REQUIRE(cooperative == 0 || cooperative == 1, "persistent launch: cooperative must be 0 or 1");
+    CFD_REQUIRE(poll_ticks >= 0, "persistent launch: poll_ticks must be >= 0 (0 = the 20 s default)");
+    tuning().persist_coop = cooperative;
+    tuning().persist_poll = (unsigned long long)poll_ticks;
+    return CFD_OK;
+}
+
+int cfd_persistent_status(int *expired) {
+    CFD_REQUIRE(expired, "persistent_status: null pointer");
+    *expired = 0;
+    int *w = persist_fail_word();
+    CFD_REQUIRE(w, "persistent_status: no status word on this device");
+    CFD_CHECK_HIP(hipDeviceSynchronize());
+    int h = 0;
+    CFD_CHECK_HIP(hipMemcpy(&h, w, sizeof(int), hipMemcpyDeviceToHost));
+    if (h) CFD_CHECK_HIP(hipMemset(w, 0, sizeof(int)));
+    *expired = h;
+    return CFD_OK;
+}
+
+int cfd_release_thread_resources(void) {
+    release_thread_rings();
     return CFD_OK;
 }
 

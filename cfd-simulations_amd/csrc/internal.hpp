@@ -54,8 +54,29 @@ struct Tuning {
     // nx % 4 == 0 and the arrays are 16-byte aligned), 1 one thread per cell,
     // 2 row march; rows per chunk of the row march (0: one resident round)
     int pred_variant = 0, pred_rows = 0;
+    // persistent small-grid solves (jacobi2d_persist, rbgs2d_persist): launch
+    // cooperatively (the runtime guarantees every tile co-resident or refuses
+    // the launch, which then takes the launch-per-pass path); the bound of a
+    // neighbour poll in ticks of the 100 MHz clock (0: 20 s)
+    int persist_coop = 1;
+    unsigned long long persist_poll = 0;
 };
+// The current device's failure counter of persistent solves (a device int,
+// process-wide, allocated on first use): a solve whose poll expired adds 1;
+// cfd_persistent_status reads and clears it.  nullptr if allocation failed.
+int *persist_fail_word();
+// Launch a persistent kernel: cooperatively when tuning().persist_coop (0 if
+// the runtime refuses the size: every tile could not be co-resident -- the
+// error is cleared and the caller takes its launch-per-pass path), else a
+// plain launch.  1 = launched; -1 = another launch error (set_error done).
+int launch_persistent(const void *f, int nblocks, int threads, void *args, hipStream_t s);
+// free the calling thread's persistent Jacobi rings (jacobi2d_persist.hip)
+void release_thread_rings();
 Tuning &tuning();
+// the persistent solves' poll bound in effect (tuning().persist_poll, or 20 s)
+inline unsigned long long persist_poll_ticks() {
+    return tuning().persist_poll ? tuning().persist_poll : 2000000000ull;
+}
 
 // jacobi2d_persist.hip: 1 if it ran the solve (phi <- the result; *rc set on
 // a HIP error), 0 if the persistent path does not apply

@@ -30,9 +30,13 @@
 // The result: every tile writes its own cells into phi after its last block;
 // a neighbour read phi only at its start, which preceded its block 0 output
 // that this tile consumed (hence nb >= 2 blocks, iterations > NI).  Every poll
-// is bounded (20 s of the 100 MHz clock), and the launcher checks that every
-// tile is resident at once.
+// is bounded (20 s of the 100 MHz clock by default, cfd_set_persistent_launch);
+// an expired one leaves phi all NaN and counts a failure (cfd_persistent_status).
+// The launch is cooperative (launch_persistent): the runtime guarantees that
+// every tile is resident at once, or refuses and the launch-per-pass path runs.
 #include "internal.hpp"
+
+#include <atomic>
 
 namespace cfd {
 namespace {
@@ -40,7 +44,6 @@ namespace {
 constexpr int kJW = 16, kJRW = 2, kJT0 = kJW * kJRW;  // waves, rows per wave, tile rows
 constexpr int kJGSlots = 3;
 constexpr int kJMaxTiles = 256;
-constexpr unsigned long long kJSpinLimit = 2000000000ull;  // 20 s at 100 MHz
 constexpr int kMaxDevices = 64;
 
 struct JPersistArgs {
@@ -49,6 +52,8 @@ struct JPersistArgs {
     const uint8_t *mask;
     unsigned long long *G;  // kJGSlots planes of ny * nx granules
     int *status;            // bit 0: a poll expired
+    int *fail;              // the device's persistent-failure counter (cfd_persistent_status)
+    unsigned long long spin;  // poll bound, 100 MHz ticks
     int ny, nx, nseg, niters, pre;
     float dx2, dtv;
 };
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
                 }
                 more = more || need[j];
             }
-            broken = broken || wall_clock64() - t0 > kJSpinLimit;
+            broken = broken || (unsigned long long)(wall_clock64() - t0) > a.spin;
             if (!__any(more) || broken) break;
             __builtin_amdgcn_s_sleep(1);
         }
@@ -179,10 +184,13 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
     if (broken && lane == 0) atomicOr(a.status, 1);
 }
 
-// an expired poll leaves garbage: mark the result (phi[0] <- NaN) so that it
-// cannot pass for a solution
-__global__ void k_jp_status(const int *status, float *phi) {
-    if (*status) phi[0] = __int_as_float(0x7fc00000);
+// an expired poll leaves garbage: the whole result becomes NaN (so it cannot
+// pass for a solution: the health check, v5.py:601, sees it) and the device's
+// failure counter counts the solve.  One workgroup that normally exits at once.
+__global__ __launch_bounds__(1024) void k_jp_status(const int *status, float *phi, size_t n, int *fail) {
+    if (!*status) return;
+    for (size_t c = threadIdx.x; c < n; c += blockDim.x) phi[c] = __int_as_float(0x7fc00000);
+    if (threadIdx.x == 0 && fail) atomicAdd(fail, 1);
 }
 
 int jtiles_for(int NI, int ny, int nx, int *nseg) {
@@ -191,18 +199,23 @@ int jtiles_for(int NI, int ny, int nx, int *nseg) {
     return *nseg * ceil_div(ny - 2, OUT);
 }
 
+// workgroups of jacobi2d_persist<MASK, NI> the current device holds at once
+// (an idle device; -1: query failed), cached per device
 template <bool MASK, int NI>
 int jresident_tiles() {
-    static int resident = 0;
-    if (resident == 0) {
-        int dev = 0, per_cu = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+    static std::atomic<int> cache[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return -1;
+    int r = cache[dev].load(std::memory_order_relaxed);
+    if (r == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jacobi2d_persist<MASK, NI>, 1024, 0) != hipSuccess)
             return -1;
-        resident = per_cu * cus;
+        r = per_cu * cus;
+        cache[dev].store(r, std::memory_order_relaxed);
     }
-    return resident;
+    return r;
 }
 
 // The granule ring and the status word live in a library-owned device buffer,
@@ -258,6 +271,19 @@ void ring_release(int dev, hipStream_t s) {
 
 }  // namespace
 
+void release_thread_rings() {
+    JRing &r = t_ring;
+    for (int d = 0; d < kMaxDevices; ++d) {
+        if (r.done[d]) (void)hipEventSynchronize(r.done[d]);
+        if (r.p[d]) (void)hipFree(r.p[d]);
+        if (r.done[d]) (void)hipEventDestroy(r.done[d]);
+        r.p[d] = nullptr;
+        r.bytes[d] = 0;
+        r.done[d] = nullptr;
+        r.last[d] = nullptr;
+    }
+}
+
 int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t *mask, int ny, int nx,
                            float dx2, float dtv, int iterations, hipStream_t s, int *rc) {
     *rc = CFD_OK;
@@ -308,15 +334,20 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
         set_error("jacobi2d persistent: ring reset failed");
         return 1;
     }
-#define CFD_LAUNCH(N_)                                                                                      \
-    do {                                                                                                    \
-        if (mask) hipLaunchKernelGGL((jacobi2d_persist<true, N_>), dim3(ntiles), dim3(1024), 0, s, a);      \
-        else hipLaunchKernelGGL((jacobi2d_persist<false, N_>), dim3(ntiles), dim3(1024), 0, s, a);          \
-    } while (0)
-    CFD_JN(CFD_LAUNCH)
-#undef CFD_LAUNCH
+    a.fail = persist_fail_word();
+    a.spin = persist_poll_ticks();
+    const void *f = nullptr;
+#define CFD_KF(N_) f = mask ? (const void *)jacobi2d_persist<true, N_> : (const void *)jacobi2d_persist<false, N_>
+    CFD_JN(CFD_KF)
+#undef CFD_KF
 #undef CFD_JN
-    hipLaunchKernelGGL(k_jp_status, dim3(1), dim3(1), 0, s, a.status, phi);
+    const int lr = launch_persistent(f, ntiles, 1024, &a, s);
+    if (lr == 0) return 0;  // not co-resident now: the launch-per-pass path
+    if (lr < 0) {
+        *rc = CFD_E_HIP;
+        return 1;
+    }
+    hipLaunchKernelGGL(k_jp_status, dim3(1), dim3(1024), 0, s, a.status, phi, plane, a.fail);
     ring_release(dev, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -45,12 +45,15 @@
 // ring (8 blocks): block j's flags go out at block j + 1, after this tile
 // ruled out a stop in block j - 2, so every tile has published block j - 2's
 // flags, i.e. is in block j - 1 or later and reads flags of block j - 4 or
-// later.  Every poll is bounded (20 s of the
-// 100 MHz clock from the kernel's start, as the slab sync kernel), so a tile
-// that never arrives (another kernel holding the CUs) ends the solve with a
-// status bit instead of a hang; the launcher also checks that every tile is
-// resident at once before choosing this path.
+// later.  The launch is cooperative (launch_persistent): the runtime
+// guarantees that every tile is resident at once, or refuses it and the
+// launch-per-block path runs.  Every poll is still bounded (20 s of the 100
+// MHz clock from the kernel's start by default, cfd_set_persistent_launch):
+// an expired one ends the solve with phi all NaN, *iters_done = -1 and a
+// failure counted for cfd_persistent_status, instead of a hang.
 #include "internal.hpp"
+
+#include <atomic>
 
 namespace cfd {
 namespace {
@@ -61,7 +64,6 @@ constexpr int kPGSlots = kPLag + 1;                    // granule planes (block 
 constexpr int kPMSlots = 8;                            // per-block flag ring (>= kPLag + 2)
 constexpr int kPMaxTiles = 256;                        // one tile per CU at most
 constexpr int kPMaxNI = 4;
-constexpr unsigned long long kPSpinLimit = 2000000000ull;  // 20 s at 100 MHz
 
 struct PersistArgs {
     const float *in;
@@ -72,6 +74,7 @@ struct PersistArgs {
     unsigned long long *M;  // kPMSlots x ntiles flag granules
     RbgsWs *ws;
     unsigned long long *trace;  // optional: 4 timestamps per tile and block
+    unsigned long long spin;    // poll bound, 100 MHz ticks
     int ny, nx, nseg, ntiles, niters;
     float cx, cy, cd, dt_inv, tol;
 };
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
     const unsigned long long t0 = wall_clock64();
     bool broken = false;  // a poll expired (per wave; the result is garbage then)
     auto expired = [&]() {
-        broken = broken || wall_clock64() - t0 > kPSpinLimit;
+        broken = broken || (unsigned long long)(wall_clock64() - t0) > a.spin;
         return broken;
     };
 
@@ -417,16 +420,22 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
     if (broken) atomicOr(&a.ws->flags[3], 1);
 }
 
-// phi <- out (the solve's result), and the count (or -1 after an expired poll)
+// phi <- out (the solve's result), and the count; after an expired poll phi
+// becomes all NaN instead (it cannot pass for a solution), the count -1, and
+// the device's failure counter (cfd_persistent_status) counts the solve
 __global__ void rbgs_persist_finish(const RbgsWs *__restrict__ ws, float *__restrict__ phi,
-                                    const float *__restrict__ src, size_t n, int *iters_done) {
+                                    const float *__restrict__ src, size_t n, int *iters_done, int *fail) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const size_t n4 = n / 4;
+    const bool bad = ws->flags[3] != 0;
+    const float4 nan4 = make_float4(__int_as_float(0x7fc00000), __int_as_float(0x7fc00000),
+                                    __int_as_float(0x7fc00000), __int_as_float(0x7fc00000));
     for (size_t k = t0; k < n4; k += stride)
-        reinterpret_cast<float4 *>(phi)[k] = reinterpret_cast<const float4 *>(src)[k];
-    for (size_t k = 4 * n4 + t0; k < n; k += stride) phi[k] = src[k];
-    if (t0 == 0 && iters_done) *iters_done = ws->flags[3] ? -1 : ws->flags[1];
+        reinterpret_cast<float4 *>(phi)[k] = bad ? nan4 : reinterpret_cast<const float4 *>(src)[k];
+    for (size_t k = 4 * n4 + t0; k < n; k += stride) phi[k] = bad ? nan4.x : src[k];
+    if (t0 == 0 && iters_done) *iters_done = bad ? -1 : ws->flags[1];
+    if (t0 == 0 && bad && fail) atomicAdd(fail, 1);
 }
 
 int tiles_for(int NI, int ny, int nx, int *nseg) {
@@ -438,18 +447,22 @@ int tiles_for(int NI, int ny, int nx, int *nseg) {
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // workgroups of rbgs2d_persist<MASK, NI, PAIRS> the chip holds at once (-1: query failed)
+// (an idle device's count, cached per device)
 template <bool MASK, int NI, bool PAIRS>
 int resident_tiles() {
-    static int resident = 0;
-    if (resident == 0) {
-        int dev = 0, per_cu = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+    int r = cache[dev].load(std::memory_order_relaxed);
+    if (r == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rbgs2d_persist<MASK, NI, PAIRS>, 1024, 0) != hipSuccess)
             return -1;
-        resident = per_cu * cus;
+        r = per_cu * cus;
+        cache[dev].store(r, std::memory_order_relaxed);
     }
-    return resident;
+    return r;
 }
 
 }  // namespace
@@ -520,25 +533,23 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
         set_error("rbgs2d persistent: ring reset failed");
         return 1;
     }
-#define CFD_LAUNCH(N_)                                                                                     \
-    do {                                                                                                   \
-        if (pairs && mask) hipLaunchKernelGGL((rbgs2d_persist<true, N_, true>), dim3(a.ntiles), dim3(1024), 0, s, a);   \
-        else if (pairs) hipLaunchKernelGGL((rbgs2d_persist<false, N_, true>), dim3(a.ntiles), dim3(1024), 0, s, a);    \
-        else if (mask) hipLaunchKernelGGL((rbgs2d_persist<true, N_, false>), dim3(a.ntiles), dim3(1024), 0, s, a);     \
-        else hipLaunchKernelGGL((rbgs2d_persist<false, N_, false>), dim3(a.ntiles), dim3(1024), 0, s, a);              \
-    } while (0)
-    CFD_PERS_N(CFD_LAUNCH)
-#undef CFD_LAUNCH
+    a.spin = persist_poll_ticks();
+    const void *f = nullptr;
+#define CFD_KF(N_)                                                                                    \
+    f = pairs ? (mask ? (const void *)rbgs2d_persist<true, N_, true> : (const void *)rbgs2d_persist<false, N_, true>) \
+              : (mask ? (const void *)rbgs2d_persist<true, N_, false> : (const void *)rbgs2d_persist<false, N_, false>)
+    CFD_PERS_N(CFD_KF)
+#undef CFD_KF
 #undef CFD_PERS_N
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
+    const int lr = launch_persistent(f, a.ntiles, 1024, &a, s);
+    if (lr == 0) return 0;  // not co-resident now: the launch-per-block path (the rings are re-reset there)
+    if (lr < 0) {
         *rc = CFD_E_HIP;
-        set_error("rbgs2d persistent launch failed: %s", hipGetErrorString(e));
         return 1;
     }
     const size_t n = (size_t)ny * nx;
     hipLaunchKernelGGL(rbgs_persist_finish, dim3(ceil_div((long)(n / 4 + 1), 256)), dim3(256), 0, s, ws, phi,
-                       phi_tmp, n, iters_done);
+                       phi_tmp, n, iters_done, persist_fail_word());
     const hipError_t e2 = hipGetLastError();
     if (e2 != hipSuccess) {
         *rc = CFD_E_HIP;

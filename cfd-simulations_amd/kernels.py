@@ -22,7 +22,7 @@ __all__ = [
     "solve_pressure_gauss_seidel_fast", "solve_pressure_jacobi", "apply_ibm_fast",
     "clean_divergence_fast", "predictor_fused", "project_velocity", "solve_pressure_jacobi3d",
     "solve_pressure_jacobi3d_zero",
-    "solve_pressure_gauss_seidel3d",
+    "solve_pressure_gauss_seidel3d", "persistent_failures",
 ]
 
 
@@ -295,3 +295,13 @@ def project_velocity(phi, u_star, v_star, dx, dy, dt, u=None, v=None, gradmax=No
     call(_fields("cfd_project2d", phi, u_star, v_star, u, v, gradmax), ptr(phi), ptr(u_star), ptr(v_star), ptr(u),
          ptr(v), ny, nx, float(dx), float(dy), _dt_arg(dt, phi.dtype), ptr(gradmax), stream_handle())
     return u, v
+
+
+def persistent_failures() -> int:
+    """Synchronises the device and returns how many persistent small-grid
+    solves (the one-launch 2-D Jacobi / red-black GS) had a tile wait expire
+    since the last call; their phi is all NaN (cfd_persistent_status)."""
+    import ctypes
+    n = ctypes.c_int(0)
+    call("cfd_persistent_status", ctypes.byref(n))
+    return int(n.value)

@@ -16,6 +16,7 @@ v5.py:60,381-384), plotting and video (OptimizedVisualizer), and HDF5 output
 """
 from __future__ import annotations
 
+import logging
 import os
 from dataclasses import dataclass, field
 
@@ -460,6 +461,12 @@ def monitor_simulation_health(solver: OptimizedTurbulentSolver, step: int) -> bo
          float(cfg.dy), ptr(red[1:2]), s)
     n_bad = int(cnt.item())
     vel_max, div_max = (float(x) for x in red.cpu().numpy())
+    # a persistent pressure solve whose tiles could not all run (a wait for a
+    # neighbour tile expired) left phi all NaN: a failed step, reported here
+    if K.persistent_failures():
+        logging.getLogger(__name__).error("Step %d: a persistent pressure solve failed (a tile wait expired)",
+                                          step)
+        return False
     if n_bad:
         return False
     if vel_max > cfg.max_velocity:

@@ -432,6 +432,27 @@ int cfd_set_small2d_gs_persistent(int mode);
  * on = 0 default (on), 1 off, 2 on; sweeps_per_block 0 = default (8), or
  * 4, 6, 8.  Its exchange ring lives in a library-owned device buffer. */
 int cfd_set_small2d_jacobi_persistent(int on, int sweeps_per_block);
+/* Both persistent small-grid solves (the GS above and the Jacobi below) are
+ * launched cooperatively by default (cooperative = 1): the HIP runtime then
+ * guarantees that every tile is resident at once or refuses the launch, and a
+ * refused launch takes the launch-per-pass path (same bits).  cooperative = 0:
+ * a plain launch after the library's own occupancy check (which assumes the
+ * device is otherwise idle).  poll_ticks bounds each wait of a tile for its
+ * neighbours, in ticks of the 100 MHz device clock (0 = the default, 20 s; a
+ * tiny value forces the failure path in tests).  A solve whose wait expired
+ * leaves phi all NaN, the GS's *iters_done = -1, and counts one failure for
+ * cfd_persistent_status. */
+int cfd_set_persistent_launch(int cooperative, long long poll_ticks);
+/* Synchronises the current device, then returns in *expired the number of
+ * persistent solves on it whose neighbour wait expired since the last call
+ * (and clears the count).  The Python solver checks it in
+ * monitor_simulation_health (v5.py:599-613). */
+int cfd_persistent_status(int *expired);
+/* Frees the calling thread's library-owned device buffers: the persistent
+ * Jacobi's exchange rings (24 B per cell of the largest grid the thread
+ * solved, one per device), after the solves that use them have finished.
+ * Later solves on the thread allocate them again. */
+int cfd_release_thread_resources(void);
 /* Diagnostics: the persistent GS writes 4 timestamps (100 MHz device clock)
  * per tile and block into buf -- block start, halo received, tile ready,
  * levels done; layout [block][tile][4] u64 -- when bytes covers the solve

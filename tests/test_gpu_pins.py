@@ -408,6 +408,7 @@ def test_jacobi2d_persistent_streams_and_threads():
             K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), dev(mask), iters)
             s.synchronize()
             res[i] = phi.cpu().numpy()
+        call("cfd_release_thread_resources")  # this thread's ring, freed after its solve
 
     th = [threading.Thread(target=work, args=(i,)) for i in range(len(cases))]
     for t in th:
@@ -416,6 +417,66 @@ def test_jacobi2d_persistent_streams_and_threads():
         t.join(timeout=120)
     for r, (_, _, ref) in zip(res, cases):
         assert r is not None and np.array_equal(r, ref)
+
+
+@pytest.mark.parametrize("cooperative", [1, 0])
+def test_persistent_cooperative_and_plain_launch_bitexact(cooperative):
+    """Both persistent small-grid solves, launched cooperatively (the default)
+    and plainly, on the cylinder grid: bit-exact, and no failure counted."""
+    call("cfd_set_persistent_launch", cooperative, 0)
+    shape = (180, 600)
+    rng = np.random.default_rng(21 + cooperative)
+    div = rng.standard_normal(shape).astype(np.float32)
+    mask = rng.random(shape) < 0.03
+    ref = oracle.jacobi2d(div, dx=20 / 599, dt=np.float32(5e-5), iters=300, mask=mask)
+    phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), dev(mask), 300)
+    assert np.array_equal(host(phi), ref)
+    gdiv = div * np.float32(1e-3)
+    gref, n_ref = oracle.rbgs2d(gdiv, dx=20 / 599, dy=4 / 179, dt=np.float32(5e-5), mask=mask, iters=200, tol=1e-8)
+    phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(int(lib().cfd_rbgs2d_workspace_bytes(shape[0], shape[1], 200)), dtype=torch.uint8, device=DEV)
+    K.solve_pressure_gauss_seidel_fast(phi, dev(gdiv), 20 / 599, 4 / 179, np.float32(5e-5), dev(mask), 200, 1e-8,
+                                       workspace=ws, iters_done=done, phi_tmp=torch.zeros_like(phi))
+    assert np.array_equal(host(phi), gref) and int(host(done)[0]) == n_ref
+    assert K.persistent_failures() == 0
+
+
+def test_persistent_forced_expiry_fails_loudly():
+    """A neighbour wait that expires (forced by a 1-tick poll bound) must not
+    pass silently: the persistent Jacobi leaves phi all NaN, the persistent
+    GS phi all NaN and iters_done = -1, each counts a failure that
+    cfd_persistent_status returns, and the solver's health check
+    (monitor_simulation_health, v5.py:599-613) reports the step as failed.
+    The next solve with the default bound is correct again."""
+    from cfd_simulations_amd.solver import OptimizedTurbulentConfig, OptimizedTurbulentSolver, \
+        monitor_simulation_health
+    assert K.persistent_failures() == 0
+    shape = (180, 600)
+    rng = np.random.default_rng(5)
+    div = rng.standard_normal(shape).astype(np.float32)
+    call("cfd_set_persistent_launch", 1, 1)
+    phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), None, 300)
+    assert np.isnan(host(phi)).all()
+    assert K.persistent_failures() == 1
+    phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(int(lib().cfd_rbgs2d_workspace_bytes(shape[0], shape[1], 100)), dtype=torch.uint8, device=DEV)
+    K.solve_pressure_gauss_seidel_fast(phi, dev(div), 20 / 599, 4 / 179, np.float32(5e-5), None, 100, 1e-8,
+                                       workspace=ws, iters_done=done, phi_tmp=torch.zeros_like(phi))
+    assert int(host(done)[0]) == -1 and np.isnan(host(phi)).all()
+    assert K.persistent_failures() == 1
+    for fast in (False, True):
+        solver = OptimizedTurbulentSolver(OptimizedTurbulentConfig(use_fast_pressure=fast, pressure_iterations=64))
+        solver.time_step()
+        assert monitor_simulation_health(solver, 1) is False
+    call("cfd_set_persistent_launch", 1, 0)
+    phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), None, 300)
+    assert np.array_equal(host(phi), oracle.jacobi2d(div, dx=20 / 599, dt=np.float32(5e-5), iters=300))
+    assert K.persistent_failures() == 0
 
 
 # ------------------------------------------- zero-start solve, fused first pass
