@@ -22,6 +22,11 @@
 // every result bit-equal) and on the device against the oracle's libm calls
 // (tests/test_gpu_pins.py).  Shared by the host check (CFD_LIBM_HOST) and the
 // HIP kernels.
+//
+// Licence: this file restates an algorithm and constant tables published in
+// the GNU C Library (glibc, LGPL-2.1-or-later), which took them from Arm's
+// optimized-routines (MIT OR Apache-2.0 WITH LLVM-exception); see those
+// projects for the upstream licence texts.
 #pragma once
 #ifdef CFD_LIBM_HOST
 #include <cmath>

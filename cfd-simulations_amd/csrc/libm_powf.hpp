@@ -19,6 +19,11 @@
 // uses); the x86_64 FMA variant of libm agrees with the unfused form on all of
 // them too.  tests/test_gpu_parity.py checks this device copy against the
 // oracle's libm calls.  No multiply-add is fused here (-ffp-contract=off).
+//
+// Licence: this file restates an algorithm and constant tables published in
+// the GNU C Library (glibc, LGPL-2.1-or-later), which took them from Arm's
+// optimized-routines (MIT OR Apache-2.0 WITH LLVM-exception); see those
+// projects for the upstream licence texts.
 #pragma once
 #ifdef CFD_LIBM_HOST
 #include <cstdint>

@@ -40,7 +40,7 @@ for s in "$@"; do
     benchch) step benchch 600 python bench.py --workload jacobi3d_channel --no-cpu-baseline ;;
     testsk) step pytest_k 900 python -m pytest tests -m gpu -q -k "k_levels or variants_agree or temporal or full_size" ;;
     ksweep) step ksweep 900 bash -c 'for cfg in ${KSWEEP:-"3 0 1 0" "3 16 2 0" "3 16 1 256" "4 0 1 0" "2 0 1 0"}; do set -- $cfg; echo "K=$1 rows=$2 PD=$3 zchunk=$4"; python bench.py --no-cpu-baseline --steps 5 --tb $1 --tb-rows $2 --tb-prefetch $3 --tb-zchunk $4 | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
-    testspred) step pytest_pred 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "predictor or powf or time_step or golden" ;;
+    testspred) step pytest_pred 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "predictor or powf or time_step or golden or persistent" ;;
     benchpred) step benchpred 600 python bench.py --workload predictor2d_8192 --steps 20 --warmup 3 ;;
     benchpred64) step benchpred64 600 python bench.py --workload predictor2d_8192_f64 --steps 20 --warmup 3 ;;
     benchpredv1) step benchpredv1 600 env CFD_PRED_VARIANT=1 python bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --no-cpu-baseline ;;
