@@ -47,7 +47,7 @@ PROTOTYPES = {
     "cfd_laplacian2d_f32": (c_int, [P, P, c_float, P, c_int, c_int, c_double, c_double, P]),
     "cfd_predictor2d_f32": (c_int, [P, P, P, c_float, P, P, P, c_int, c_int, c_double, c_double,
                                     c_float, c_int, P]),
-    "cfd_set_predictor2d_config": (c_int, [c_int, c_int]),
+    "cfd_set_predictor2d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_persistent_launch": (c_int, [c_int, ctypes.c_longlong]),
     "cfd_persistent_status": (c_int, [P]),
     "cfd_release_thread_resources": (c_int, []),

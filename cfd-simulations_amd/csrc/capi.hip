@@ -60,6 +60,10 @@ static Tuning process_defaults() {
         t.gs_pairs = env_int("CFD_GS_PAIRS", t.gs_pairs) != 0;
         const int pv = env_int("CFD_PRED_VARIANT", t.pred_variant);
         t.pred_variant = pv >= 0 && pv <= 2 ? pv : t.pred_variant;
+        const int pw = env_int("CFD_PRED_VEC", t.pred_vec);
+        t.pred_vec = pw == 1 || pw == 2 || pw == 4 ? pw : t.pred_vec;
+        const int pr = env_int("CFD_PRED_ROWS", t.pred_rows);
+        t.pred_rows = pr >= 0 ? pr : t.pred_rows;
         const int ni = env_int("CFD_GS_SMALL_NI", t.gs_ni);
         t.gs_ni = ni >= 1 && ni <= 4 ? ni : t.gs_ni;
         return t;

@@ -58,14 +58,15 @@ __device__ inline float supg_tau(float u, float v, float nu, float dt, const Pre
 }
 // the same from |V|^2 = u**2 + v**2 already formed (the row-march predictor
 // forms the squares and roots of a lane's four cells in batches)
+// (branch-free: both sides formed, one selected, so the row march can
+// interleave its four cells' division chains)
 __device__ inline float supg_tau_vm(float vm, float nu, float dt, const PredConst &k) {
-    if (vm > k.eps) {
-        const float pe = (vm * k.h) / (nu + k.eps);
-        const float half = pe / 2.0f;
-        const float lim = half < 1.0f ? half : 1.0f;
-        return (k.h / (2.0f * vm)) * lim;
-    }
-    return dt / 2.0f;
+    const float pe = (vm * k.h) / (nu + k.eps);
+    const float half = pe / 2.0f;
+    const float lim = half < 1.0f ? half : 1.0f;
+    float t = (k.h / (2.0f * vm)) * lim;
+    asm volatile("" : "+v"(t));  // keeps the divisions out of a branch on vm > eps
+    return vm > k.eps ? t : dt / 2.0f;
 }
 
 // compute_convection_supg_fast body, v5.py:135-146
@@ -80,6 +81,21 @@ __device__ inline float conv_supg(float uc, float vc, float C, float E, float W,
         return cs - t * (uc * d2x + vc * d2y);
     }
     return cs;
+}
+
+// conv_supg without the branch on t > 0 (both forms, one selected; the asm
+// keeps the compiler from sinking the second-derivative part into a branch):
+// the row march interleaves its four cells
+__device__ inline float conv_supg_sel(float uc, float vc, float C, float E, float W, float N, float S,
+                                      float t, const PredConst &k) {
+    const float ddx = (E - W) * k.c1x;
+    const float ddy = (N - S) * k.c1y;
+    const float cs = uc * ddx + vc * ddy;
+    const float d2x = ((E - 2.0f * C) + W) * k.c2x;
+    const float d2y = ((N - 2.0f * C) + S) * k.c2y;
+    float cd = cs - t * (uc * d2x + vc * d2y);
+    asm volatile("" : "+v"(cd));
+    return t > 0.0f ? cd : cs;
 }
 
 // compute_convection_fast body (first-order upwind), v5.py:120-124
@@ -178,29 +194,33 @@ __global__ __launch_bounds__(256) void k_predictor(const float *__restrict__ u,
 }
 
 // ---- row-march predictor (r04): the fused predictor as a tiled stencil ------
-// One wave owns a 256-column segment of the grid (64 lanes x one float4 of 4
-// cells) and marches down a chunk of rows.  Rows i-1, i, i+1 of u and v sit in
-// a 4-slot register queue (row i+2 is in flight: each row is loaded once, as
-// one 1 KiB coalesced dwordx4 load per field, two steps ahead), rotated
-// through compile-time slots by a 4-fold unrolled march.  y-neighbours are
-// the queue's other slots, x-neighbours are the lane's own float4 plus DPP
-// wave shifts (wave_shr / wave_shl) for cells 0 and 3; the two columns just
-// outside the segment arrive as one dword load per row and field (lane 0:
-// column xs - 1, lane 63: column xs + 256) and enter the shifts as their
-// `old` operand.  The four waves of a workgroup take four adjacent segments;
-// workgroups are dealt chunk by chunk, XCD-swizzled, so the two halo rows a
-// chunk shares with its neighbours are read from the same L2.  u*, v* and tau
-// leave as streaming float4 stores.  HBM: u, v read once (+2 halo rows per
-// chunk), u*, v*, tau written once: 20 B per cell (16 without tau).
+// One wave owns a segment of 64 * VEC columns (64 lanes x VEC adjacent cells:
+// one float, float2 or float4 per lane) and marches down a chunk of rows.
+// Rows i-1, i, i+1 of u and v sit in registers (row i+2 is in flight: each row
+// is loaded once, one coalesced 64 * VEC * 4 B load per field, two steps
+// ahead), rotated by moves at the end of a step.  y-neighbours are the other
+// rows, x-neighbours the lane's own cells plus DPP wave shifts (wave_shr /
+// wave_shl) for its first and last cell; the two columns just outside the
+// segment arrive as one dword load per row and field (lane 0: column xs - 1,
+// lane 63: column xs + 64 VEC) and enter the shifts as their `old` operand.
+// The four waves of a workgroup take four adjacent segments; workgroups are
+// dealt chunk by chunk, XCD-swizzled, so the two halo rows a chunk shares with
+// its neighbours are read from the same L2.  u*, v* and tau leave as
+// streaming stores.  HBM: u, v read once (+2 halo rows per chunk), u*, v*,
+// tau written once: 20 B per cell (16 without tau).
 //
-// |V| = (u**2 + v**2)**0.5 through powf_sq / powf_sqrt (libm_powf.hpp): a
-// lane's 8 squares, then its 4 roots, are formed exactly in double; the rare
-// ones near a float rounding midpoint (~0.36 % per call) are re-done by the
-// full glibc powf in a per-lane loop over a bit mask, so the wave runs ONE
-// powf body per batch at most instead of one per call.  Arithmetic per cell is
-// k_predictor's, operation for operation (bit-identical).
-typedef float pv4f __attribute__((ext_vector_type(4)));
-
+// tau runs on proven fast paths: |V| = (u**2 + v**2)**0.5 through powf_sq_fast
+// / powf_sqrt_fast (libm_powf.hpp: float ops and an fma residual each, equal
+// to glibc's powf unless near a rounding midpoint, ~0.36 % / ~0.75 % per
+// call) and its two divisions through div_fast (v_rcp_f32 + one Newton step,
+// proven correctly rounded by the residual).  A cell none of whose checks can
+// be proven is NOT computed in the march (one such lane would hold its whole
+// wave in the full powf at almost every row): the lane skips its stores and
+// queues its cells with their stencil inputs in a per-wave LDS ring; whenever
+// the ring holds 64 (and at the end of the chunk) each lane computes one
+// queued cell by the exact per-cell form (pred_cell_from: the full glibc powf
+// and IEEE divisions) and stores its three outputs.  Arithmetic per cell is
+// k_predictor's, operation for operation: the outputs are bit-identical.
 struct PredRowArgs {
     const float *u, *v, *nu;  // nu: the nu_eff array, or null (nu_s)
     float *us, *vs, *tau;     // tau: null = not written
@@ -209,8 +229,41 @@ struct PredRowArgs {
     PredConst k;
 };
 
-__device__ inline pv4f pld4(__amdgpu_buffer_rsrc_t r, uint32_t ofs) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)ofs, 0, 0);
+// a lane's VEC cells of one row through a buffer resource (kOob: zeros / dropped)
+template <int VEC>
+struct Cells {
+    float x[VEC];
+};
+template <int VEC>
+__device__ inline Cells<VEC> pldv(__amdgpu_buffer_rsrc_t r, uint32_t ofs) {
+    Cells<VEC> c;
+    if constexpr (VEC == 4) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)ofs, 0, 0);
+        for (int k = 0; k < 4; ++k) c.x[k] = __uint_as_float(v[k]);
+    } else if constexpr (VEC == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)ofs, 0, 0);
+        for (int k = 0; k < 2; ++k) c.x[k] = __uint_as_float(v[k]);
+    } else {
+        c.x[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)ofs, 0, 0));
+    }
+    return c;
+}
+template <int VEC>
+__device__ inline void pstv(const Cells<VEC> &c, __amdgpu_buffer_rsrc_t r, uint32_t ofs) {
+    constexpr int kNt = 2;  // streaming store policy
+    // (the builtins take unsigned words: pass the float bits, not a conversion)
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    if constexpr (VEC == 4) {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u4{__float_as_uint(c.x[0]), __float_as_uint(c.x[1]), __float_as_uint(c.x[2]), __float_as_uint(c.x[3])}, r,
+            (int)ofs, 0, kNt);
+    } else if constexpr (VEC == 2) {
+        __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(c.x[0]), __float_as_uint(c.x[1])}, r, (int)ofs, 0,
+                                              kNt);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(c.x[0]), r, (int)ofs, 0, kNt);
+    }
 }
 __device__ inline float pld1(__amdgpu_buffer_rsrc_t r, uint32_t ofs) {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)ofs, 0, 0));
@@ -222,58 +275,68 @@ __device__ inline float shr_old(float old, float src) {
 __device__ inline float shl_old(float old, float src) {
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x130, 0xf, 0xf, false));
 }
-template <int N>
-__device__ inline float pick(const float (&a)[N], int q) {
-    float x = a[0];
-#pragma unroll
-    for (int c = 1; c < N; ++c) x = q == c ? a[c] : x;
-    return x;
-}
-template <int N>
-__device__ inline void place(float (&a)[N], int q, float r) {
-#pragma unroll
-    for (int c = 0; c < N; ++c) a[c] = q == c ? r : a[c];
-}
-
-// |V| of a lane's four cells, v5.py:155, bit for bit
-__device__ inline void vel_mag4(const pv4f &u, const pv4f &v, float (&vm)[4]) {
-    float sq[8];
-    uint32_t slow = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const double a = (double)u[c] * (double)u[c], b = (double)v[c] * (double)v[c];
-        sq[c] = (float)a;
-        sq[4 + c] = (float)b;
-        slow |= (libm::powf_window_ok(a, libm::kPowfSqWin) ? 0u : 1u) << c;
-        slow |= (libm::powf_window_ok(b, libm::kPowfSqWin) ? 0u : 1u) << (4 + c);
-    }
-    if (slow) {
-        const float in[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
-        do {
-            const int q = __builtin_ctz(slow);
-            place(sq, q, libm::powf(pick(in, q), 2.0f));
-            slow &= slow - 1;
-        } while (slow);
-    }
-    float s[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        s[c] = sq[c] + sq[4 + c];
-        const double d = __builtin_sqrt((double)s[c]);
-        vm[c] = (float)d;
-        slow |= (s[c] > 0.0f && libm::powf_window_ok(d, libm::kPowfSqrtWin) ? 0u : 1u) << c;
-    }
-    if (slow) {
-        do {
-            const int q = __builtin_ctz(slow);
-            place(vm, q, libm::powf(pick(s, q), 0.5f));
-            slow &= slow - 1;
-        } while (slow);
-    }
+// a / b, correctly rounded, from rb ~ 1/b (v_rcp_f32) and one Newton step:
+// q1 = q0 + (a - q0 b) rb.  With the exact residual r = a - q1 b (one fma:
+// exact for q1 within an ulp of a/b, no underflow), a/b = q1 + r/b, so
+// |r| < (1/2 - 2^-10) |b| ulp(q1) proves q1 = RN(a/b) (the ulp taken below
+// q1's last bit, as in powf_sq_fast: the lower binade's for a power of two;
+// the 2^-10 margin covers the rounding of the threshold).  False otherwise
+// (near a midpoint, q1 tiny, inf, NaN): the caller takes the exact path.
+constexpr float kDivT = (float)((0.5 - 0x1p-10) * 0x1p-23);
+__device__ inline bool div_fast(float a, float b, float rb, float &q) {
+    const float q0 = a * rb;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-q0, b, a), rb, q0);
+    const float r = __builtin_fmaf(-q1, b, a);
+    const float ul = __uint_as_float(((__float_as_uint(q1) & 0x7fffffffu) - 1u) & 0x7f800000u) * kDivT;
+    q = q1;
+    return __builtin_fabsf(q1) >= 0x1p-100f && __builtin_fabsf(r) < __builtin_fabsf(b) * ul;
 }
 
-template <bool SUPG, bool NUA>
-__global__ __launch_bounds__(256) void k_predictor_rows(PredRowArgs a) {
+// supg_tau_vm on the fast division: tau, and whether it is proven exact
+// (rnu = an approximate 1 / (nu + eps))
+__device__ inline float supg_tau_fast(float vm, float nu, float rnu, float dt, const PredConst &k, bool &ok) {
+    float pe, q;
+    const bool o1 = div_fast(vm * k.h, nu + k.eps, rnu, pe);
+    const float half = pe / 2.0f;
+    const float lim = half < 1.0f ? half : 1.0f;
+    const float d = 2.0f * vm;
+    const bool o2 = div_fast(k.h, d, __builtin_amdgcn_rcpf(d), q);
+    float t = q * lim;
+    asm volatile("" : "+v"(t));  // formed unconditionally (no branch on vm > eps)
+    const bool big = vm > k.eps;
+    ok = !big || (o1 && o2);
+    return big ? t : dt / 2.0f;
+}
+
+// one cell of the fused SUPG predictor, exactly (k_predictor's body: the
+// full glibc powf wherever the fast paths do not apply, IEEE divisions), from
+// the stencil inputs the row march queued: {uc, vc, uE, uW, uN, uS, vE, vW,
+// vN, vS}; bit 31 of idx marks a face cell (conv = lap = tau = 0)
+__device__ inline void pred_cell_from(const PredRowArgs &a, uint32_t idx, const float (&f)[11], float nu) {
+    const uint32_t c = idx & 0x7fffffffu;
+    const float uc = f[0], vc = f[1];
+    float cu = 0.0f, cv = 0.0f, lu = 0.0f, lv = 0.0f, t = 0.0f;
+    if (!(idx >> 31)) {
+        t = supg_tau(uc, vc, nu, a.dt, a.k);
+        cu = conv_supg(uc, vc, uc, f[2], f[3], f[4], f[5], t, a.k);
+        cv = conv_supg(uc, vc, vc, f[6], f[7], f[8], f[9], t, a.k);
+        lu = laplacian(nu, uc, f[2], f[3], f[4], f[5], a.k);
+        lv = laplacian(nu, vc, f[6], f[7], f[8], f[9], a.k);
+    }
+    a.us[c] = uc + a.dt * (-cu + lu);
+    a.vs[c] = vc + a.dt * (-cv + lv);
+    if (a.tau) a.tau[c] = t;
+}
+
+#ifndef CFD_PRED_WPE
+#define CFD_PRED_WPE 1
+#endif
+#ifndef CFD_PRED_ABL
+#define CFD_PRED_ABL 0
+#endif
+template <bool SUPG, bool NUA, int VEC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WPE, 8))) void k_predictor_rows(PredRowArgs a) {
+    constexpr int SW = 64 * VEC;  // segment width (columns)
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int b = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
@@ -283,9 +346,9 @@ __global__ __launch_bounds__(256) void k_predictor_rows(PredRowArgs a) {
     const int ny = a.ny, nx = a.nx;
     const int r0 = chunk * a.rows;
     const int r1 = min(r0 + a.rows, ny);
-    const int xs = seg * 256;
-    const int x0 = xs + lane * 4;
-    const bool lane_in = x0 < nx;  // nx % 4 == 0: a lane's float4 is all in or all out
+    const int xs = seg * SW;
+    const int x0 = xs + lane * VEC;
+    const bool lane_in = x0 < nx;  // nx % VEC == 0: a lane's cells are all in or all out
     const int bytes = (int)((size_t)ny * nx * sizeof(float));
     const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.u), 0, bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.v), 0, bytes, 0x00020000);
@@ -294,91 +357,169 @@ __global__ __launch_bounds__(256) void k_predictor_rows(PredRowArgs a) {
     const __amdgpu_buffer_rsrc_t rus = __builtin_amdgcn_make_buffer_rsrc(a.us, 0, bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rvs = __builtin_amdgcn_make_buffer_rsrc(a.vs, 0, bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(a.tau ? a.tau : a.us, 0, a.tau ? bytes : 0, 0x00020000);
-    // byte offset of this lane's float4 in row i (kOob outside the grid: reads 0, stores dropped)
+    // byte offset of this lane's cells in row i (kOob outside the grid: reads 0, stores dropped)
     auto rofs = [&](int i) -> uint32_t {
         return (i >= 0 && i < ny && lane_in) ? (uint32_t)(((size_t)i * nx + x0) * sizeof(float)) : kOob;
     };
-    // the segment's x-halo cells of row i: lane 0 column xs - 1, lane 63 column xs + 256
-    const int hx = lane == 0 ? xs - 1 : (lane == kWave - 1 ? xs + 256 : -1);
+    // the segment's x-halo cells of row i: lane 0 column xs - 1, lane 63 column xs + SW
+    const int hx = lane == 0 ? xs - 1 : (lane == kWave - 1 ? xs + SW : -1);
     const bool h_in = hx >= 0 && hx < nx;
     auto hofs = [&](int i) -> uint32_t {
         return (i >= 0 && i < ny && h_in) ? (uint32_t)(((size_t)i * nx + hx) * sizeof(float)) : kOob;
     };
-    const bool c0_in = x0 >= 1;           // cell 0 off the x = 0 face
-    const bool c3_in = x0 + 3 <= nx - 2;  // cell 3 off the x = nx-1 face (cells 1, 2 never touch one)
     const float dt = a.dt;
+    const float rnu_s = __builtin_amdgcn_rcpf(a.nu_s + a.k.eps);
 
-    pv4f U[4], V[4], NU[4];
-    float HU[4], HV[4];
-    U[3] = pld4(ru, rofs(r0 - 1));
-    V[3] = pld4(rv, rofs(r0 - 1));
-    U[0] = pld4(ru, rofs(r0));
-    V[0] = pld4(rv, rofs(r0));
-    HU[0] = pld1(ru, hofs(r0));
-    HV[0] = pld1(rv, hofs(r0));
-    U[1] = pld4(ru, rofs(r0 + 1));
-    V[1] = pld4(rv, rofs(r0 + 1));
-    HU[1] = pld1(ru, hofs(r0 + 1));
-    HV[1] = pld1(rv, hofs(r0 + 1));
+    // The wave's patch queue: a ring in LDS of the cells whose tau the fast
+    // paths left unproven (~1.5 % of cells) -- with VEC > 1 every cell of such
+    // a lane -- holding each cell's linear index and its stencil inputs.  The
+    // march stores none of those cells; once the queue holds a wave's worth
+    // (64), each lane computes one queued cell by the exact per-cell form
+    // (pred_cell_from) and stores its three outputs; the rest at the end of
+    // the chunk.  No output is written twice, and the inputs come from LDS.
+    constexpr int kPQ = 128;             // >= 64 + the 64 one cell slot appends
+    constexpr int kPF = NUA ? 11 : 10;   // floats per entry
+    __shared__ uint32_t pq_idx_all[4][kPQ];
+    __shared__ float pq_val_all[4][kPF][kPQ];
+    uint32_t *const pq_idx = pq_idx_all[wv];
+    float(*const pq_val)[kPQ] = pq_val_all[wv];
+    int qh = 0, qn = 0;  // head and count, wave-uniform
+    auto drain = [&](int n) {
+        if (lane < n) {
+            const int e = (qh + lane) & (kPQ - 1);
+            float in_[11];
+#pragma unroll
+            for (int f = 0; f < kPF; ++f) in_[f] = pq_val[f][e];
+            pred_cell_from(a, pq_idx[e], in_, NUA ? in_[10] : a.nu_s);
+        }
+        qh = (qh + n) & (kPQ - 1);
+        qn -= n;
+    };
+
+    // rows i-1 (m), i (c), i+1 (p) and i+2 (n, in flight) of u and v; the
+    // segment's x-halo cells and the nu_eff row of rows i, i+1, i+2
+    Cells<VEC> Um = pldv<VEC>(ru, rofs(r0 - 1)), Vm = pldv<VEC>(rv, rofs(r0 - 1));
+    Cells<VEC> Uc = pldv<VEC>(ru, rofs(r0)), Vc = pldv<VEC>(rv, rofs(r0));
+    float HUc = pld1(ru, hofs(r0)), HVc = pld1(rv, hofs(r0));
+    Cells<VEC> Up = pldv<VEC>(ru, rofs(r0 + 1)), Vp = pldv<VEC>(rv, rofs(r0 + 1));
+    float HUp = pld1(ru, hofs(r0 + 1)), HVp = pld1(rv, hofs(r0 + 1));
+    Cells<VEC> NUc = {}, NUp = {};
     if (NUA) {
-        NU[0] = pld4(rn, rofs(r0));
-        NU[1] = pld4(rn, rofs(r0 + 1));
+        NUc = pldv<VEC>(rn, rofs(r0));
+        NUp = pldv<VEC>(rn, rofs(r0 + 1));
     }
-    for (int i0 = r0; i0 < r1; i0 += 4) {
+    for (int i = r0; i < r1; ++i) {
+        // two rows ahead: row i+2 (and its halo cells / nu row)
+        const Cells<VEC> Un = pldv<VEC>(ru, rofs(i + 2)), Vn = pldv<VEC>(rv, rofs(i + 2));
+        const float HUn = pld1(ru, hofs(i + 2)), HVn = pld1(rv, hofs(i + 2));
+        Cells<VEC> NUn = {};
+        if (NUA) NUn = pldv<VEC>(rn, rofs(i + 2));
+        Cells<VEC> uo = Uc, vo = Vc, to = {};
+        uint32_t slow = 0;  // this lane's cells whose tau is unproven
+        if (i >= 1 && i <= ny - 2) {  // wave-uniform: boundary rows keep u* = u + dt*(-0 + 0)
+            const float *uc = Uc.x, *vc = Vc.x;
+            float uE[VEC], uW[VEC], vE[VEC], vW[VEC];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int i = i0 + q;
-            if (i >= r1) break;
-            // two rows ahead: row i+2 (and its halo cells / nu row)
-            U[(q + 2) & 3] = pld4(ru, rofs(i + 2));
-            V[(q + 2) & 3] = pld4(rv, rofs(i + 2));
-            HU[(q + 2) & 3] = pld1(ru, hofs(i + 2));
-            HV[(q + 2) & 3] = pld1(rv, hofs(i + 2));
-            if (NUA) NU[(q + 2) & 3] = pld4(rn, rofs(i + 2));
-            const pv4f uc = U[q], vc = V[q];
-            pv4f uo = uc, vo = vc, to = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (i >= 1 && i <= ny - 2) {  // wave-uniform: boundary rows keep u* = u + dt*(-0 + 0)
-                const pv4f uS = U[(q + 3) & 3], uN = U[(q + 1) & 3];
-                const pv4f vS = V[(q + 3) & 3], vN = V[(q + 1) & 3];
-                const float uE[4] = {uc[1], uc[2], uc[3], shl_old(HU[q], uc[0])};
-                const float uW[4] = {shr_old(HU[q], uc[3]), uc[0], uc[1], uc[2]};
-                const float vE[4] = {vc[1], vc[2], vc[3], shl_old(HV[q], vc[0])};
-                const float vW[4] = {shr_old(HV[q], vc[3]), vc[0], vc[1], vc[2]};
-                float vm[4];
-                if (SUPG) vel_mag4(uc, vc, vm);
+            for (int c = 0; c < VEC; ++c) {
+                uE[c] = c < VEC - 1 ? uc[c + 1] : shl_old(HUc, uc[0]);
+                uW[c] = c > 0 ? uc[c - 1] : shr_old(HUc, uc[VEC - 1]);
+                vE[c] = c < VEC - 1 ? vc[c + 1] : shl_old(HVc, vc[0]);
+                vW[c] = c > 0 ? vc[c - 1] : shr_old(HVc, vc[VEC - 1]);
+            }
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float nu = NUA ? NU[q][c] : a.nu_s;
-                    float cu, cv, t = 0.0f;
-                    if (SUPG) {
-                        t = supg_tau_vm(vm[c], nu, dt, a.k);
-                        cu = conv_supg(uc[c], vc[c], uc[c], uE[c], uW[c], uN[c], uS[c], t, a.k);
-                        cv = conv_supg(uc[c], vc[c], vc[c], vE[c], vW[c], vN[c], vS[c], t, a.k);
-                    } else {
-                        cu = conv_upwind(uc[c], vc[c], uc[c], uE[c], uW[c], uN[c], uS[c], a.k);
-                        cv = conv_upwind(uc[c], vc[c], vc[c], vE[c], vW[c], vN[c], vS[c], a.k);
-                    }
-                    const float lu = laplacian(nu, uc[c], uE[c], uW[c], uN[c], uS[c], a.k);
-                    const float lv = laplacian(nu, vc[c], vE[c], vW[c], vN[c], vS[c], a.k);
-                    const bool in = c == 0 ? c0_in : (c == 3 ? c3_in : true);
-                    // a face cell: conv = lap = tau = 0 (np.zeros_like rings)
-                    uo[c] = uc[c] + dt * (-(in ? cu : 0.0f) + (in ? lu : 0.0f));
-                    vo[c] = vc[c] + dt * (-(in ? cv : 0.0f) + (in ? lv : 0.0f));
-                    to[c] = in ? t : 0.0f;
+            for (int c = 0; c < VEC; ++c) {
+                const float nu = NUA ? NUc.x[c] : a.nu_s;
+                float cu, cv, t = 0.0f;
+                bool ok = true;
+                if (SUPG) {
+                    // |V| (v5.py:155) and tau (v5.py:156-161) on the fast paths
+                    float p, q, vm;
+#if CFD_PRED_ABL & 1  // ablation (timing aid only): no checks on the squares / root
+                    p = uc[c] * uc[c];
+                    q = vc[c] * vc[c];
+                    vm = __builtin_amdgcn_sqrtf(p + q);
+                    const bool oa = true, ob = true, os = true;
+#else
+                    const bool oa = libm::powf_sq_fast(uc[c], p);
+                    const bool ob = libm::powf_sq_fast(vc[c], q);
+                    const bool os = libm::powf_sqrt_fast(p + q, vm);
+#endif
+                    bool od;
+#if CFD_PRED_ABL & 2  // ablation: no divisions
+                    t = vm > a.k.eps ? vm * a.k.h * rnu_s : dt;
+                    od = true;
+#else
+                    t = supg_tau_fast(vm, nu, NUA ? __builtin_amdgcn_rcpf(nu + a.k.eps) : rnu_s, dt, a.k, od);
+#endif
+                    ok = oa && ob && os && od;
+#if CFD_PRED_ABL & 4  // ablation: no patch queue
+                    ok = true;
+#endif
+                    cu = conv_supg_sel(uc[c], vc[c], uc[c], uE[c], uW[c], Up.x[c], Um.x[c], t, a.k);
+                    cv = conv_supg_sel(uc[c], vc[c], vc[c], vE[c], vW[c], Vp.x[c], Vm.x[c], t, a.k);
+                } else {
+                    cu = conv_upwind(uc[c], vc[c], uc[c], uE[c], uW[c], Up.x[c], Um.x[c], a.k);
+                    cv = conv_upwind(uc[c], vc[c], vc[c], vE[c], vW[c], Vp.x[c], Vm.x[c], a.k);
                 }
-            } else {
+                const float lu = laplacian(nu, uc[c], uE[c], uW[c], Up.x[c], Um.x[c], a.k);
+                const float lv = laplacian(nu, vc[c], vE[c], vW[c], Vp.x[c], Vm.x[c], a.k);
+                const bool in = x0 + c >= 1 && x0 + c <= nx - 2;
+                // a face cell: conv = lap = tau = 0 (np.zeros_like rings)
+                uo.x[c] = uc[c] + dt * (-(in ? cu : 0.0f) + (in ? lu : 0.0f));
+                vo.x[c] = vc[c] + dt * (-(in ? cv : 0.0f) + (in ? lv : 0.0f));
+                to.x[c] = in ? t : 0.0f;
+                if (SUPG) slow |= (in && lane_in && !ok ? 1u : 0u) << c;
+            }
+            if (SUPG && __builtin_amdgcn_ballot_w64(slow != 0)) {
+                // queue every cell of a lane with an unproven one (its vector
+                // store is dropped below): positions by a ballot and mbcnt
+                const bool ql = slow != 0;
+                const uint64_t m = __builtin_amdgcn_ballot_w64(ql);
+                const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                const int n = __builtin_popcountll(m);
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    uo[c] = uc[c] + dt * (-0.0f + 0.0f);
-                    vo[c] = vc[c] + dt * (-0.0f + 0.0f);
+                for (int c = 0; c < VEC; ++c) {
+                    if (ql) {
+                        const int e = (qh + qn + r) & (kPQ - 1);
+                        const bool in = x0 + c >= 1 && x0 + c <= nx - 2;
+                        // bit 31: a face cell (u* = u + dt*(-0 + 0), tau = 0)
+                        pq_idx[e] = (uint32_t)((size_t)i * nx + x0 + c) | (in ? 0u : 0x80000000u);
+                        const float vals[11] = {uc[c], vc[c], uE[c], uW[c], Up.x[c], Um.x[c],
+                                                vE[c], vW[c], Vp.x[c], Vm.x[c], NUA ? NUc.x[c] : 0.0f};
+#pragma unroll
+                        for (int f = 0; f < kPF; ++f) pq_val[f][e] = vals[f];
+                    }
+                    qn += n;
+                    if (qn >= kWave) drain(kWave);
                 }
             }
-            const uint32_t o = rofs(i);
-            __builtin_amdgcn_raw_buffer_store_b128(uo, rus, (int)o, 0, 2 /* nt */);
-            __builtin_amdgcn_raw_buffer_store_b128(vo, rvs, (int)o, 0, 2);
-            if (SUPG && a.tau) __builtin_amdgcn_raw_buffer_store_b128(to, rt, (int)o, 0, 2);
+        } else {
+#pragma unroll
+            for (int c = 0; c < VEC; ++c) {
+                uo.x[c] = Uc.x[c] + dt * (-0.0f + 0.0f);
+                vo.x[c] = Vc.x[c] + dt * (-0.0f + 0.0f);
+            }
+        }
+        const uint32_t o = slow ? kOob : rofs(i);  // a queued lane stores nothing here
+        pstv<VEC>(uo, rus, o);
+        pstv<VEC>(vo, rvs, o);
+        if (SUPG && a.tau) pstv<VEC>(to, rt, o);
+        Um = Uc;
+        Vm = Vc;
+        Uc = Up;
+        Vc = Vp;
+        Up = Un;
+        Vp = Vn;
+        HUc = HUp;
+        HVc = HVp;
+        HUp = HUn;
+        HVp = HVn;
+        if (NUA) {
+            NUc = NUp;
+            NUp = NUn;
         }
     }
+    if (SUPG && qn) drain(qn);
 }
 
 // compute_divergence_fast, v5.py:178-187 (+ max|div| diagnostic, v5.py:410)
@@ -1005,12 +1146,20 @@ __global__ void k_numpy_powf(const float *__restrict__ x, float y, float *__rest
 
 static dim3 grid2d(int ny, int nx) { return dim3(ceil_div(nx, 256), ny); }
 
-// workgroups of the row-march predictor resident on the device at once
-static int pred_rows_resident(bool supg, bool nua) {
+// the row-march kernel for (SUPG, array nu, cells per lane)
+static const void *pred_rows_kernel(bool supg, bool nua, int vec) {
+#define CFD_PRK(V_)                                                                                         \
+    return supg ? (nua ? (const void *)k_predictor_rows<true, true, V_> : (const void *)k_predictor_rows<true, false, V_>) \
+                : (nua ? (const void *)k_predictor_rows<false, true, V_> : (const void *)k_predictor_rows<false, false, V_>)
+    if (vec == 4) CFD_PRK(4);
+    if (vec == 2) CFD_PRK(2);
+    CFD_PRK(1);
+#undef CFD_PRK
+}
+// workgroups of that kernel resident on the device at once
+static int pred_rows_resident(const void *f) {
     int dev = 0, cus = 256, per = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void *f = supg ? (nua ? (const void *)k_predictor_rows<true, true> : (const void *)k_predictor_rows<true, false>)
-                         : (nua ? (const void *)k_predictor_rows<false, true> : (const void *)k_predictor_rows<false, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per < 1) per = 1;
     return per * cus;
 }
@@ -1078,9 +1227,16 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
     CFD_SHAPE2D(ny, nx);
     const PredConst k = make_pred_const(dx, dy);
     hipStream_t s = as_stream(stream);
-    const bool rows_ok = nx % 4 == 0 && (size_t)ny * nx * sizeof(float) < ((size_t)1 << 31) && aligned16(u) &&
-                         aligned16(v) && aligned16(u_star) && aligned16(v_star) && (!tau || aligned16(tau)) &&
-                         (!nu_eff || aligned16(nu_eff));
+    // cells per lane of the row march: the preferred count (tuning; auto 4),
+    // lowered until nx and every array's alignment allow it
+    int vec = tuning().pred_vec ? tuning().pred_vec : 4;
+    auto fits = [&](int w) {
+        const uintptr_t m = (uintptr_t)(4 * w - 1);
+        auto al = [&](const void *p_) { return !p_ || ((uintptr_t)p_ & m) == 0; };
+        return nx % w == 0 && al(u) && al(v) && al(u_star) && al(v_star) && al(tau) && al(nu_eff);
+    };
+    while (vec > 1 && !fits(vec)) vec /= 2;
+    const bool rows_ok = (size_t)ny * nx * sizeof(float) < ((size_t)1 << 31) && fits(vec);
     const int tk = timing_begin(s);
     if (tuning().pred_variant != 1 && rows_ok) {
         PredRowArgs a;
@@ -1094,26 +1250,22 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
         a.dt = dt;
         a.ny = ny;
         a.nx = nx;
-        a.nseg = ceil_div(nx, 256);
+        a.nseg = ceil_div(nx, 64 * vec);
         a.groups = ceil_div(a.nseg, 4);
         a.k = k;
+        const void *f = pred_rows_kernel(use_supg != 0, nu_eff != nullptr, vec);
         // rows per chunk: every workgroup resident at once (one round at the
         // kernel's occupancy), chunks of at least 8 rows (2 halo rows each)
         a.rows = tuning().pred_rows;
         if (a.rows <= 0) {
-            const int resident = pred_rows_resident(use_supg != 0, nu_eff != nullptr);
+            const int resident = pred_rows_resident(f);
             const int chunks = resident / a.groups > 0 ? resident / a.groups : 1;
             a.rows = ceil_div(ny, chunks);
             if (a.rows < 8) a.rows = 8;
         }
         const int nblk = a.groups * ceil_div(ny, a.rows);
-        if (use_supg) {
-            if (nu_eff) hipLaunchKernelGGL((k_predictor_rows<true, true>), dim3(nblk), dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((k_predictor_rows<true, false>), dim3(nblk), dim3(256), 0, s, a);
-        } else {
-            if (nu_eff) hipLaunchKernelGGL((k_predictor_rows<false, true>), dim3(nblk), dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((k_predictor_rows<false, false>), dim3(nblk), dim3(256), 0, s, a);
-        }
+        void *args[] = {&a};
+        CFD_CHECK_HIP(hipLaunchKernel(f, dim3(nblk), dim3(256), args, 0, s));
     } else if (use_supg) {
         hipLaunchKernelGGL(k_predictor<true>, grid2d(ny, nx), dim3(256), 0, s, u, v, nu_eff, nu_eff_scalar, u_star,
                            v_star, tau, ny, nx, dt, k);
@@ -1127,11 +1279,15 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
 }
 
 // 0: auto (row march when the shape allows it), 1: one thread per cell
-// (k_predictor), 2: row march; rows per chunk (0: auto)
-int cfd_set_predictor2d_config(int variant, int rows) {
+// (k_predictor), 2: row march; rows per chunk (0: auto); cells per lane
+// (0: auto, 1, 2, 4)
+int cfd_set_predictor2d_config(int variant, int rows, int cells_per_lane) {
     CFD_REQUIRE(variant >= 0 && variant <= 2 && rows >= 0, "predictor2d config: variant 0..2, rows >= 0");
+    CFD_REQUIRE(cells_per_lane == 0 || cells_per_lane == 1 || cells_per_lane == 2 || cells_per_lane == 4,
+                "predictor2d config: cells per lane 0 (auto), 1, 2 or 4");
     tuning().pred_variant = variant;
     tuning().pred_rows = rows;
+    tuning().pred_vec = cells_per_lane;
     return CFD_OK;
 }
 

@@ -54,6 +54,8 @@ struct Tuning {
     // nx % 4 == 0 and the arrays are 16-byte aligned), 1 one thread per cell,
     // 2 row march; rows per chunk of the row march (0: one resident round)
     int pred_variant = 0, pred_rows = 0;
+    // row march: cells per lane (0 auto, 1, 2, 4)
+    int pred_vec = 0;
     // persistent small-grid solves (jacobi2d_persist, rbgs2d_persist): launch
     // cooperatively (the runtime guarantees every tile co-resident or refuses
     // the launch, which then takes the launch-per-pass path); the bound of a

@@ -31,12 +31,16 @@
 #include <cmath>
 #define CFD_HDF inline
 #define CFD_LIBMF_TABLE static
-#define CFD_SQRT_D(x) std::sqrt(x)
+#define CFD_SQRTF(x) std::sqrt(x)
+#define CFD_FMAF(a, b, c) std::fma(a, b, c)
+#define CFD_FABSF(x) std::fabs(x)
 #else
 #include "common.hpp"
 #define CFD_HDF __device__ inline
 #define CFD_LIBMF_TABLE __device__ __constant__
-#define CFD_SQRT_D(x) __builtin_sqrt(x)
+#define CFD_SQRTF(x) __builtin_sqrtf(x)
+#define CFD_FMAF(a, b, c) __builtin_fmaf(a, b, c)
+#define CFD_FABSF(x) __builtin_fabsf(x)
 #endif
 // fast-path windows: oracle/powf_window.cpp measure (1.05x the largest error + 4)
 #ifndef CFD_POWF_SQ_WIN
@@ -182,43 +186,60 @@ CFD_HDF float powf(float x, float y) {
 }
 
 // ---- fast exact paths for the two exponents the reference uses ------------
-// powf(x, 2) and powf(x, 0.5) are x*x and sqrt(x) computed in double and
-// rounded once to float, except that glibc's double result carries a small
-// error before that rounding.  It can only change the rounded float when the
-// exact value lies within that error of a rounding midpoint.  So: form the
-// exact square (48 significant bits: exact in double) or the double sqrt, and
-// look at the 29 bits below the float's last place; if they are at least
-// kPowfWin units (of 2^-29 float ulp) away from the midpoint 2^28, return the
-// rounded exact value; otherwise (and for zero, subnormal, huge, inf or nan
-// inputs) run the full powf.  kPowfWin is 1.05x (+4) the largest |e - exact| glibc's
-// algorithm shows over EVERY float input (oracle/powf_window.cpp measures it:
-// y = 2 over all 2^32 floats, y = 0.5 over all 2^31 non-negative ones), and the
-// same program checks powf_sq / powf_sqrt against libm's powf for every
-// input, bit for bit.  A lane leaves the fast path with probability ~2 *
-// kPowfWin / 2^29 per call.
+// glibc's powf forms its result in double and rounds it once to float; that
+// double carries an error of at most kPowfSqWin / kPowfSqrtWin units of 2^-29
+// of the result's float ulp (oracle/powf_window.cpp measures the maxima over
+// EVERY float input, and these windows are 1.05x those + 4).  So the float
+// result equals the correctly rounded x*x (or sqrt(x)) unless the exact value
+// lies within that window of a rounding midpoint.  The fast paths decide that
+// in float arithmetic, with the exact residual of an fma:
+//  * x*x: p = x*x rounded, e = fma(x, x, -p) = x^2 - p exactly; the square is
+//    clear of the midpoints if |e| < (1/2 - w) ulp(p);
+//  * sqrt(s): r = sqrtf(s), e = fma(-r, r, s) = s - r^2 exactly; sqrt(s) =
+//    r + e / (2r) (+ a term below 2^-40 ulp), clear if |e| < (1 - 2w) r ulp(r)
+//    -- which also proves r correctly rounded, whatever sqrtf's accuracy;
+// and any other case (p or s below 2^-100, inf, NaN, s < 0) runs the full
+// powf.  A call leaves the fast path with probability ~2w =
+// 0.36 % on O(1) inputs.  powf_window.cpp checks powf_sq / powf_sqrt against
+// libm's powf for all 2^32 float inputs, bit for bit.
 constexpr uint32_t kPowfSqWin = CFD_POWF_SQ_WIN;
 constexpr uint32_t kPowfSqrtWin = CFD_POWF_SQRT_WIN;
+// (1/2 - w) 2^-23 and (1 - 2w) 2^-23 with w = window / 2^29
+constexpr float kPowfSqT = (float)((0.5 - (double)CFD_POWF_SQ_WIN / 536870912.0) * 0x1p-23);
+constexpr float kPowfSqrtT = (float)((1.0 - 2.0 * (double)CFD_POWF_SQRT_WIN / 536870912.0) * 0x1p-23);
 
-CFD_HDF bool powf_window_ok(double d, uint32_t win) {
-    const uint64_t b = asu64d(d);
-    const uint32_t ex = (uint32_t)(b >> 52) & 0x7ffu;
-    const int32_t frac = (int32_t)(uint32_t)(b & 0x1fffffffull) - (1 << 28);
-    const uint32_t dist = (uint32_t)(frac < 0 ? -frac : frac);
-    // d a positive float-normal value below 2^127 (so (float)d cannot overflow)
-    return (ex - (1023u - 126u)) < 253u && dist >= win;
+// p = x*x rounded; true when p is glibc's powf(x, 2).  The window is taken
+// in the ulp of the binade below p's last bit (exponent of bits(p) - 1): for
+// p = 2^k that is the lower binade, whose midpoints are the nearer ones when
+// the exact square lies below p; for every other p it is p's own ulp.
+CFD_HDF bool powf_sq_fast(float x, float &p) {
+    p = x * x;
+    const float e = CFD_FMAF(x, x, -p);
+    const float t = asf32u((asu32f(p) - 1u) & 0x7f800000u) * kPowfSqT;
+    // p >= 2^-100 keeps e exact (no underflow); inf / NaN fail the compare
+    return p >= 0x1p-100f && CFD_FABSF(e) < t;
+}
+// r = sqrt(s) rounded; true when r is glibc's powf(s, 0.5) (the window in
+// the ulp below r's last bit, as above)
+CFD_HDF bool powf_sqrt_fast(float s, float &r) {
+    r = CFD_SQRTF(s);
+    const float e = CFD_FMAF(-r, r, s);
+    const float t = r * (asf32u((asu32f(r) - 1u) & 0x7f800000u) * kPowfSqrtT);
+    // s >= 2^-100 keeps e exact; s < 0, inf or NaN fail the compare
+    return s >= 0x1p-100f && CFD_FABSF(e) < t;
 }
 
 // NumPy float32 scalar x**2, bit for bit (glibc powf(x, 2.0f))
 CFD_HDF float powf_sq(float x) {
-    const double d = (double)x * (double)x;
-    if (powf_window_ok(d, kPowfSqWin)) return (float)d;
+    float p;
+    if (powf_sq_fast(x, p)) return p;
     return powf(x, 2.0f);
 }
 
 // NumPy float32 scalar x**0.5, bit for bit (glibc powf(x, 0.5f))
 CFD_HDF float powf_sqrt(float x) {
-    const double d = CFD_SQRT_D((double)x);
-    if (x > 0.0f && powf_window_ok(d, kPowfSqrtWin)) return (float)d;
+    float r;
+    if (powf_sqrt_fast(x, r)) return r;
     return powf(x, 0.5f);
 }
 

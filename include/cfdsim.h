@@ -166,11 +166,13 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
                         float *u_star, float *v_star, float *tau, int ny, int nx,
                         double dx, double dy, float dt, int use_supg, void *stream);
 /* Kernel of cfd_predictor2d_f32 (tuning, per host thread; same bits either
- * way): variant 0 = auto (the row-march tile kernel when nx % 4 == 0, every
- * array 16-byte aligned and ny*nx < 2^29; else one thread per cell), 1 = one
- * thread per cell, 2 = row march where it applies; rows = rows per row-march
- * chunk (0 = auto: every workgroup resident in one round). */
-int cfd_set_predictor2d_config(int variant, int rows);
+ * way): variant 0 = auto (the row-march tile kernel when ny*nx < 2^29; else
+ * one thread per cell), 1 = one thread per cell, 2 = row march where it
+ * applies; rows = rows per row-march chunk (0 = auto: every workgroup resident
+ * in one round); cells_per_lane = adjacent cells per lane of the row march (0 =
+ * auto, 1, 2, 4), lowered until nx % it == 0 and every array is aligned to
+ * 4 * it bytes. */
+int cfd_set_predictor2d_config(int variant, int rows, int cells_per_lane);
 
 /* compute_divergence_fast, v5.py:178-187.  absmax (device float*, optional):
  * receives max|div| (the v5.py:410 diagnostic); must be zeroed by the caller. */

@@ -9,10 +9,10 @@
 //    sqrt, itself within 2^-29 float ulp of the exact root).  The unit is 2^-29
 //    of the result's float ulp: the bits below the float's last place in a
 //    double.  Prints the maxima and the windows (1.05x + 4) to compile in.
-// 2. With -DCFD_POWF_SQ_WIN=.. -DCFD_POWF_SQRT_WIN=.. (the windows), checks
-//    powf_sq(x) == libm powf(x, 2.0f) and powf_sqrt(x) == libm powf(x, 0.5f)
-//    bit for bit for every float x (NaNs: both NaN), and reports how often the
-//    fast path is left.
+// 2. Checks powf_sq(x) == libm powf(x, 2.0f) and powf_sqrt(x) == libm
+//    powf(x, 0.5f) bit for bit for every float x (NaNs: both NaN), with the
+//    windows libm_powf.hpp compiles in (or -DCFD_POWF_SQ_WIN=..
+//    -DCFD_POWF_SQRT_WIN=..), and reports how often the fast path is left.
 //
 //   g++ -O2 -fopenmp -ffp-contract=off -fno-builtin -DCFD_LIBM_HOST \
 //       [-DCFD_POWF_SQ_WIN=W2 -DCFD_POWF_SQRT_WIN=W5] powf_window.cpp -o powf_window
@@ -84,7 +84,8 @@ static int verify() {
             if (bad2 < 5) printf("  y=2 x=%a libm=%a fast=%a\n", (double)x, (double)w2, (double)g2);
             ++bad2;
         }
-        if (!powf_window_ok((double)x * (double)x, kPowfSqWin)) ++slow2;
+        float tmp;
+        if (!powf_sq_fast(x, tmp)) ++slow2;
         const float w5 = ::powf(x, 0.5f), g5 = powf_sqrt(x);
         if (!(asu32f(w5) == asu32f(g5) || (std::isnan(w5) && std::isnan(g5)))) {
             if (bad5 < 5) printf("  y=0.5 x=%a libm=%a fast=%a\n", (double)x, (double)w5, (double)g5);
@@ -92,7 +93,7 @@ static int verify() {
         }
         if (!(ix >> 31)) {
             ++nonneg;
-            if (!(x > 0.0f && powf_window_ok(std::sqrt((double)x), kPowfSqrtWin))) ++slow5;
+            if (!powf_sqrt_fast(x, tmp)) ++slow5;
         }
     }
     printf("windows: sq %u, sqrt %u (units of 2^-29 float ulp)\n", kPowfSqWin, kPowfSqrtWin);

@@ -48,6 +48,7 @@ for s in "$@"; do
     profpred64) step profpred64 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profpred64 -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 20 --warmup 3 --no-cpu-baseline ;;
     pmc_fetch_pred) step pmc_fetch_pred 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_pred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline ;;
     pmc_write_pred) step pmc_write_pred 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_pred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline ;;
+    predsweep) step predsweep 600 python scripts/pred_sweep.py ;;
     sq_pred) step sq_pred 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES -d gpurun_out/sq_pred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline ;;
     tests2d) step pytest_2d 900 python -m pytest tests -m gpu -q -k "jacobi2d or rbgs2d or time_step or golden" ;;
     sweep2d) step sweep2d 900 bash -c 'for K in ${K2D:-8 10 12}; do echo "K=$K"; python bench.py --workload jacobi2d_8192_f64 --no-cpu-baseline --steps 3 --tb $K | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;

@@ -71,8 +71,8 @@ def test_predictor_8192_bench_workload_bitexact():
 
 
 def test_predictor_8192_variants_agree():
-    """Row march and one thread per cell, SUPG / upwind, array / scalar nu:
-    the same bits at 8192^2."""
+    """Row march (1, 2 and 4 cells per lane) and one thread per cell, SUPG /
+    upwind, array / scalar nu: the same bits at 8192^2."""
     ny = nx = 8192
     c, nu = _cfg(ny, nx)
     g = torch.Generator(device=DEV).manual_seed(11)
@@ -83,57 +83,79 @@ def test_predictor_8192_variants_agree():
     for supg in (True, False):
         for nu_in in (float(nu), nua):
             outs = []
-            for variant in (2, 1):
-                call("cfd_set_predictor2d_config", variant, 0)
-                outs.append([t.clone() for t in K.predictor_fused(u, v, c.dx, c.dy, dt, nu_in, supg)])
-            for a, b in zip(outs[0], outs[1]):
-                if a is not None:
-                    assert torch.equal(a, b)
+            for variant, vec in ((1, 0), (2, 4), (2, 2), (2, 1)):
+                call("cfd_set_predictor2d_config", variant, 0, vec)
+                outs.append([None if t is None else t.clone()
+                             for t in K.predictor_fused(u, v, c.dx, c.dy, dt, nu_in, supg)])
+            for o in outs[1:]:
+                for a, b in zip(outs[0], o):
+                    if a is not None:
+                        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("shape", [(40, 56), (180, 600), (37, 260), (5, 4), (3, 8), (64, 1028), (9, 58), (33, 2)])
 @pytest.mark.parametrize("rows", [0, 1, 3])
+@pytest.mark.parametrize("vec", [0, 1, 2, 4])
 @pytest.mark.parametrize("supg,nu_array", [(True, False), (True, True), (False, True)])
-def test_predictor_shapes_bitexact(shape, rows, supg, nu_array):
+def test_predictor_shapes_bitexact(shape, rows, vec, supg, nu_array):
     ny, nx = shape
     c, nu = _cfg(ny, nx)
     rng = np.random.default_rng(ny * 1000 + nx)
     u = rng.uniform(-1.5, 1.5, shape).astype(np.float32)
     v = rng.uniform(-1.5, 1.5, shape).astype(np.float32)
-    call("cfd_set_predictor2d_config", 0, rows)
+    call("cfd_set_predictor2d_config", 0, rows, vec)
     _check(u, v, nu, c, np.float32(2e-5), supg, nu_array)
 
 
-def _near_midpoint(rng, n, root):
-    """float32 values u whose exact square (root=False), or the square root of
-    whose rounded square (root=True: |V| with v = 0), lies within twice the
-    fast-path window of a float rounding midpoint."""
+def _near_midpoint(rng, n):
+    """float32 values whose exact square lies within twice the fast-path
+    window of a float rounding midpoint."""
     x = rng.uniform(0.01, 4.0, n * 400).astype(np.float32)
-    sq = x.astype(np.float64) ** 2
-    d = np.sqrt(sq.astype(np.float32).astype(np.float64)) if root else sq
+    d = x.astype(np.float64) ** 2
     lo = (d.view(np.uint64) & np.uint64((1 << 29) - 1)).astype(np.int64) - (1 << 28)
-    sel = x[np.abs(lo) < 2 * (SQRT_WIN if root else SQ_WIN)]
+    sel = x[np.abs(lo) < 2 * SQ_WIN]
     assert sel.size >= n
     return sel[:n]
 
 
-def test_predictor_slow_path_and_special_values():
+def _near_midpoint_roots(rng, n):
+    """float32 pairs (u, v) whose |V| = (f32(u^2) + f32(v^2))**0.5 lies within
+    twice the fast-path window of a float rounding midpoint."""
+    u = rng.uniform(-2.0, 2.0, n * 400).astype(np.float32)
+    v = rng.uniform(-2.0, 2.0, n * 400).astype(np.float32)
+    s = (u.astype(np.float64) ** 2).astype(np.float32) + (v.astype(np.float64) ** 2).astype(np.float32)
+    d = np.sqrt(s.astype(np.float64))
+    lo = (d.view(np.uint64) & np.uint64((1 << 29) - 1)).astype(np.int64) - (1 << 28)
+    sel = np.abs(lo) < 2 * SQRT_WIN
+    assert sel.sum() >= n
+    return u[sel][:n], v[sel][:n]
+
+
+@pytest.mark.parametrize("density", [1.0, 0.03])
+@pytest.mark.parametrize("vec", [1, 2, 4])
+def test_predictor_slow_path_and_special_values(density, vec):
     """u, v drawn from values whose squares sit near a rounding midpoint (the
     full glibc powf must run), values whose u^2 + v^2 root does, and zeros,
-    subnormals, huge values, inf and NaN scattered over the grid."""
+    subnormals, huge values, inf and NaN scattered over the grid.  density
+    1: nearly every cell leaves the fast paths (the row march's patch queue
+    overflows and the chunk is redone per cell); 0.03: the queue path."""
     ny, nx = 64, 512
     c, nu = _cfg(ny, nx)
     rng = np.random.default_rng(5)
-    sq = _near_midpoint(rng, ny * nx, False)
+    sq = _near_midpoint(rng, ny * nx)
     u = (sq * np.where(rng.random(ny * nx) < 0.5, -1, 1)).astype(np.float32).reshape(ny, nx)
     v = rng.permutation(sq).astype(np.float32).reshape(ny, nx)
-    # a third of the cells: v = 0 and u such that |V| = (u**2)**0.5 is near a midpoint
-    roots = _near_midpoint(rng, ny * nx // 3, True)
-    idx = rng.choice(ny * nx, roots.size, replace=False)
+    if density < 1.0:  # plain values elsewhere
+        plain = rng.random((ny, nx)) >= density
+        u[plain] = rng.uniform(-1, 1, plain.sum()).astype(np.float32)
+        v[plain] = rng.uniform(-1, 1, plain.sum()).astype(np.float32)
+    # a third of the cells: (u, v) pairs whose |V| root is near a midpoint
+    ru, rv = _near_midpoint_roots(rng, int(ny * nx * density) // 3)
+    idx = rng.choice(ny * nx, ru.size, replace=False)
     vf = v.reshape(-1)
     uf = u.reshape(-1)
-    uf[idx] = roots
-    vf[idx] = 0.0
+    uf[idx] = ru
+    vf[idx] = rv
     special = np.array([0.0, -0.0, 1e-45, -3e-39, 1e-20, 3e19, -2e30, np.inf, -np.inf, np.nan], np.float32)
     for k, val in enumerate(special):
         pos = rng.choice(ny * nx, 12, replace=False)
@@ -142,5 +164,5 @@ def test_predictor_slow_path_and_special_values():
     with np.errstate(all="ignore"):
         for supg in (True, False):
             for rows in (0, 2):
-                call("cfd_set_predictor2d_config", 2, rows)
+                call("cfd_set_predictor2d_config", 2, rows, vec)
                 _check(u, v, nu, c, np.float32(2e-5), supg, False)
