@@ -300,7 +300,8 @@ def predictor_bench():
     cells = ny * nx
     alg = cells * bpc
     achieved = alg / (launch_ms * 1e-3) / 1e9
-    kern = "k_predictor64<SUPG> (one thread per cell)" if f64 else "k_predictor_rows<SUPG, scalar nu> (row march)"
+    kern = ("k_predictor64<SUPG> (one thread per cell)" if f64 else
+            "k_predictor_rows<SUPG, scalar nu, 2 cells per lane> (row march, 16-row chunks)")
     out = {
         "metric": "Gcell-updates/s of the fused advection-diffusion predictor; achieved HBM GB/s vs peak",
         "value": round(cells * ARGS.steps / elapsed / 1e9, 3), "unit": "Gcell-updates/s", "n_gpus": 1,

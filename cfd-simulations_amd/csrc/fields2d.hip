@@ -46,8 +46,9 @@ static PredConst make_pred_const(double dx, double dy) {
 // (u**2 + v**2) ** 0.5 on float32 scalars, i.e. libm powf three times
 // (powf_sq / powf_sqrt: glibc powf at y = 2 / 0.5 bit for bit, with a cheap
 // exact path away from rounding midpoints -- libm_powf.hpp)
-__device__ inline float supg_tau(float u, float v, float nu, float dt, const PredConst &k) {
-    const float vm = libm::powf_sqrt(libm::powf_sq(u) + libm::powf_sq(v));
+__device__ inline float supg_tau(float u, float v, float nu, float dt, const PredConst &k,
+                                 const libm::PowfTables &T = libm::kPowfTables) {
+    const float vm = libm::powf_sqrt(libm::powf_sq(u, T) + libm::powf_sq(v, T), T);
     if (vm > k.eps) {
         const float pe = (vm * k.h) / (nu + k.eps);
         const float half = pe / 2.0f;
@@ -214,12 +215,12 @@ __global__ __launch_bounds__(256) void k_predictor(const float *__restrict__ u,
 // to glibc's powf unless near a rounding midpoint, ~0.36 % / ~0.75 % per
 // call) and its two divisions through div_fast (v_rcp_f32 + one Newton step,
 // proven correctly rounded by the residual).  A cell none of whose checks can
-// be proven is NOT computed in the march (one such lane would hold its whole
-// wave in the full powf at almost every row): the lane skips its stores and
-// queues its cells with their stencil inputs in a per-wave LDS ring; whenever
-// the ring holds 64 (and at the end of the chunk) each lane computes one
-// queued cell by the exact per-cell form (pred_cell_from: the full glibc powf
-// and IEEE divisions) and stores its three outputs.  Arithmetic per cell is
+// be proven is NOT re-done in the march (one such lane would hold its whole
+// wave in the full powf at almost every row): its linear index goes to a
+// per-wave patch queue in LDS; whenever the queue holds 64 (and at the end of
+// the chunk) each lane recomputes one queued cell by the exact per-cell form
+// (pred_cell_exact: the full glibc powf, its tables in LDS, and IEEE
+// divisions) and overwrites the cell's three outputs.  Arithmetic per cell is
 // k_predictor's, operation for operation: the outputs are bit-identical.
 struct PredRowArgs {
     const float *u, *v, *nu;  // nu: the nu_eff array, or null (nu_s)
@@ -308,26 +309,32 @@ __device__ inline float supg_tau_fast(float vm, float nu, float rnu, float dt, c
     return big ? t : dt / 2.0f;
 }
 
-// one cell of the fused SUPG predictor, exactly (k_predictor's body: the
-// full glibc powf wherever the fast paths do not apply, IEEE divisions), from
-// the stencil inputs the row march queued: {uc, vc, uE, uW, uN, uS, vE, vW,
-// vN, vS}; bit 31 of idx marks a face cell (conv = lap = tau = 0)
-__device__ inline void pred_cell_from(const PredRowArgs &a, uint32_t idx, const float (&f)[11], float nu) {
-    const uint32_t c = idx & 0x7fffffffu;
-    const float uc = f[0], vc = f[1];
-    float cu = 0.0f, cv = 0.0f, lu = 0.0f, lv = 0.0f, t = 0.0f;
-    if (!(idx >> 31)) {
-        t = supg_tau(uc, vc, nu, a.dt, a.k);
-        cu = conv_supg(uc, vc, uc, f[2], f[3], f[4], f[5], t, a.k);
-        cv = conv_supg(uc, vc, vc, f[6], f[7], f[8], f[9], t, a.k);
-        lu = laplacian(nu, uc, f[2], f[3], f[4], f[5], a.k);
-        lv = laplacian(nu, vc, f[6], f[7], f[8], f[9], a.k);
-    }
+// one interior cell of the fused SUPG predictor, exactly (k_predictor's
+// body: the full glibc powf wherever the fast paths do not apply, IEEE
+// divisions), its inputs re-read from global memory (L2: the march read them
+// a few rows ago)
+template <bool NUA>
+__device__ inline void pred_cell_exact(const PredRowArgs &a, uint32_t c, const libm::PowfTables &T) {
+    const float *__restrict__ u = a.u;
+    const float *__restrict__ v = a.v;
+    const int nx = a.nx;
+    const float uc = u[c], vc = v[c];
+    const float nu = NUA ? a.nu[c] : a.nu_s;
+    const float uE = u[c + 1], uW = u[c - 1], uN = u[c + nx], uS = u[c - nx];
+    const float vE = v[c + 1], vW = v[c - 1], vN = v[c + nx], vS = v[c - nx];
+    const float t = supg_tau(uc, vc, nu, a.dt, a.k, T);
+    const float cu = conv_supg(uc, vc, uc, uE, uW, uN, uS, t, a.k);
+    const float cv = conv_supg(uc, vc, vc, vE, vW, vN, vS, t, a.k);
+    const float lu = laplacian(nu, uc, uE, uW, uN, uS, a.k);
+    const float lv = laplacian(nu, vc, vE, vW, vN, vS, a.k);
     a.us[c] = uc + a.dt * (-cu + lu);
     a.vs[c] = vc + a.dt * (-cv + lv);
     if (a.tau) a.tau[c] = t;
 }
 
+#ifdef CFD_PRED_COUNT
+__device__ unsigned long long g_pred_count;
+#endif
 #ifndef CFD_PRED_WPE
 #define CFD_PRED_WPE 1
 #endif
@@ -339,6 +346,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
     constexpr int SW = 64 * VEC;  // segment width (columns)
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    // the glibc powf tables of the queue drain's slow paths, in LDS: a table
+    // load from global memory would wait (vmcnt) for every row load and store
+    // in flight (copied before any wave of the workgroup can leave)
+    __shared__ libm::PowfTables ptab;
+    if (SUPG) {
+        const unsigned long long *src = reinterpret_cast<const unsigned long long *>(&libm::kPowfTables);
+        unsigned long long *dst = reinterpret_cast<unsigned long long *>(&ptab);
+        for (int k = threadIdx.x; k < (int)(sizeof(libm::PowfTables) / 8); k += blockDim.x) dst[k] = src[k];
+        __syncthreads();
+    }
     const int b = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
     const int chunk = b / a.groups;
     const int seg = (b - chunk * a.groups) * 4 + wv;
@@ -370,30 +387,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
     const float dt = a.dt;
     const float rnu_s = __builtin_amdgcn_rcpf(a.nu_s + a.k.eps);
 
-    // The wave's patch queue: a ring in LDS of the cells whose tau the fast
-    // paths left unproven (~1.5 % of cells) -- with VEC > 1 every cell of such
-    // a lane -- holding each cell's linear index and its stencil inputs.  The
-    // march stores none of those cells; once the queue holds a wave's worth
-    // (64), each lane computes one queued cell by the exact per-cell form
-    // (pred_cell_from) and stores its three outputs; the rest at the end of
-    // the chunk.  No output is written twice, and the inputs come from LDS.
-    constexpr int kPQ = 128;             // >= 64 + the 64 one cell slot appends
-    constexpr int kPF = NUA ? 11 : 10;   // floats per entry
+    // The wave's patch queue: a ring in LDS of the linear indices of the
+    // interior cells whose tau the fast paths left unproven (~1.6 % of
+    // cells).  The march stores every cell; once the queue holds a wave's
+    // worth (64), and at the end of the chunk, each lane recomputes one queued
+    // cell by the exact per-cell form (pred_cell_exact) and overwrites its
+    // three outputs, after the march's own stores of it have completed
+    // (vmcnt(0)).  (Queueing the cells' stencil inputs in LDS instead and
+    // skipping their march stores measured 25 % slower: more live registers
+    // and a drain per 64 cells of the same cost.)
+    constexpr int kPQ = 512;  // >= 63 + the 64 VEC cells one row appends
     __shared__ uint32_t pq_idx_all[4][kPQ];
-    __shared__ float pq_val_all[4][kPF][kPQ];
     uint32_t *const pq_idx = pq_idx_all[wv];
-    float(*const pq_val)[kPQ] = pq_val_all[wv];
     int qh = 0, qn = 0;  // head and count, wave-uniform
+#ifdef CFD_PRED_COUNT
+    int qtot = 0;
+#endif
     auto drain = [&](int n) {
-        if (lane < n) {
-            const int e = (qh + lane) & (kPQ - 1);
-            float in_[11];
-#pragma unroll
-            for (int f = 0; f < kPF; ++f) in_[f] = pq_val[f][e];
-            pred_cell_from(a, pq_idx[e], in_, NUA ? in_[10] : a.nu_s);
-        }
+#if CFD_PRED_ABL & 8  // ablation (timing aid only): no wait before the patch stores
+#else
+        wait_vmcnt<0>();
+#endif
+#if CFD_PRED_ABL & 16  // ablation: queued cells dropped, not recomputed
+#else
+        if (lane < n) pred_cell_exact<NUA>(a, pq_idx[(qh + lane) & (kPQ - 1)], ptab);
+#endif
         qh = (qh + n) & (kPQ - 1);
         qn -= n;
+#ifdef CFD_PRED_COUNT
+        qtot += n;
+#endif
     };
 
     // rows i-1 (m), i (c), i+1 (p) and i+2 (n, in flight) of u and v; the
@@ -471,26 +494,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
                 if (SUPG) slow |= (in && lane_in && !ok ? 1u : 0u) << c;
             }
             if (SUPG && __builtin_amdgcn_ballot_w64(slow != 0)) {
-                // queue every cell of a lane with an unproven one (its vector
-                // store is dropped below): positions by a ballot and mbcnt
-                const bool ql = slow != 0;
-                const uint64_t m = __builtin_amdgcn_ballot_w64(ql);
-                const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                const int n = __builtin_popcountll(m);
+                // queue the unproven cells, cell slot by cell slot: positions
+                // by a ballot and mbcnt (no LDS round trips)
 #pragma unroll
                 for (int c = 0; c < VEC; ++c) {
-                    if (ql) {
-                        const int e = (qh + qn + r) & (kPQ - 1);
-                        const bool in = x0 + c >= 1 && x0 + c <= nx - 2;
-                        // bit 31: a face cell (u* = u + dt*(-0 + 0), tau = 0)
-                        pq_idx[e] = (uint32_t)((size_t)i * nx + x0 + c) | (in ? 0u : 0x80000000u);
-                        const float vals[11] = {uc[c], vc[c], uE[c], uW[c], Up.x[c], Um.x[c],
-                                                vE[c], vW[c], Vp.x[c], Vm.x[c], NUA ? NUc.x[c] : 0.0f};
-#pragma unroll
-                        for (int f = 0; f < kPF; ++f) pq_val[f][e] = vals[f];
+                    const uint64_t m = __builtin_amdgcn_ballot_w64((slow >> c) & 1u);
+                    if (m) {
+                        if ((slow >> c) & 1u) {
+                            const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            pq_idx[(qh + qn + r) & (kPQ - 1)] = (uint32_t)((size_t)i * nx + x0 + c);
+                        }
+                        qn += __builtin_popcountll(m);
                     }
-                    qn += n;
-                    if (qn >= kWave) drain(kWave);
                 }
             }
         } else {
@@ -500,10 +516,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
                 vo.x[c] = Vc.x[c] + dt * (-0.0f + 0.0f);
             }
         }
-        const uint32_t o = slow ? kOob : rofs(i);  // a queued lane stores nothing here
+        const uint32_t o = rofs(i);
         pstv<VEC>(uo, rus, o);
         pstv<VEC>(vo, rvs, o);
         if (SUPG && a.tau) pstv<VEC>(to, rt, o);
+        while (SUPG && qn >= kWave) drain(kWave);  // (after the row's stores)
         Um = Uc;
         Vm = Vc;
         Uc = Up;
@@ -520,6 +537,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
         }
     }
     if (SUPG && qn) drain(qn);
+#ifdef CFD_PRED_COUNT  // measurement aid only: cells drained
+    if (SUPG && lane == 0) atomicAdd(&g_pred_count, (unsigned long long)qtot);
+#endif
 }
 
 // compute_divergence_fast, v5.py:178-187 (+ max|div| diagnostic, v5.py:410)
@@ -1229,7 +1249,7 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
     hipStream_t s = as_stream(stream);
     // cells per lane of the row march: the preferred count (tuning; auto 4),
     // lowered until nx and every array's alignment allow it
-    int vec = tuning().pred_vec ? tuning().pred_vec : 4;
+    int vec = tuning().pred_vec ? tuning().pred_vec : 2;
     auto fits = [&](int w) {
         const uintptr_t m = (uintptr_t)(4 * w - 1);
         auto al = [&](const void *p_) { return !p_ || ((uintptr_t)p_ & m) == 0; };
@@ -1256,11 +1276,15 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
         const void *f = pred_rows_kernel(use_supg != 0, nu_eff != nullptr, vec);
         // rows per chunk: every workgroup resident at once (one round at the
         // kernel's occupancy), chunks of at least 8 rows (2 halo rows each)
+        // (r04 sweep, 8192^2 SUPG: 16-row chunks -- several rounds -- beat one
+        // resident round of 64-row chunks by 8-15 %: the patch queue drains
+        // at chunk ends, and short chunks spread those drains over the run)
         a.rows = tuning().pred_rows;
         if (a.rows <= 0) {
             const int resident = pred_rows_resident(f);
             const int chunks = resident / a.groups > 0 ? resident / a.groups : 1;
             a.rows = ceil_div(ny, chunks);
+            if (a.rows > 16) a.rows = 16;
             if (a.rows < 8) a.rows = 8;
         }
         const int nblk = a.groups * ceil_div(ny, a.rows);
@@ -1501,3 +1525,17 @@ int cfd_nonfinite_count_f32(const float *a, const float *b, size_t n, int *out, 
 }
 
 }  // extern "C"
+
+#ifdef CFD_PRED_COUNT
+// measurement aid (a -DCFD_PRED_COUNT build only): cells the row march queued
+extern "C" unsigned long long cfd_debug_pred_count(int reset) {
+    unsigned long long h = 0;
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(&h, HIP_SYMBOL(cfd::g_pred_count), sizeof(h));
+    if (reset) {
+        const unsigned long long z = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(cfd::g_pred_count), &z, sizeof(z));
+    }
+    return h;
+}
+#endif

@@ -74,26 +74,32 @@ CFD_HDF double asf64d(uint64_t u) {
     return x;
 }
 
-CFD_LIBMF_TABLE const double kLog2InvC[16] = {
-    0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
+// glibc's __powf_log2_data (1/c, log2 c) and __exp2f_data (tab[i] =
+// bits(2^(i/32)) - (i << 47)).  A kernel whose slow path should not wait on
+// global memory copies them into LDS (PowfTables in __shared__) and passes
+// that copy to the *_t forms below.
+struct PowfTables {
+    double invc[16];
+    double logc[16];
+    unsigned long long exp2[32];
+};
+CFD_LIBMF_TABLE const PowfTables kPowfTables = {
+    {0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
     0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
     0x1.0953f419900a7p+0, 0x1p+0,               0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
-    0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
-CFD_LIBMF_TABLE const double kLog2C[16] = {
-    -0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2,
+    0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1},
+    {-0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2,
     -0x1.01d9bf3f2b631p-2, -0x1.97c1d1b3b7afp-3,  -0x1.2f9e393af3c9fp-3, -0x1.960cbbf788d5cp-4,
     -0x1.a6f9db6475fcep-5, 0x0p+0,                0x1.338ca9f24f53dp-4,  0x1.476a9543891bap-3,
-    0x1.e840b4ac4e4d2p-3,  0x1.40645f0c6651cp-2,  0x1.88e9c2c1b9ff8p-2,  0x1.ce0a44eb17bccp-2};
-// tab[i] = bits(2^(i/32)) - (i << 47)
-CFD_LIBMF_TABLE const unsigned long long kExp2Tab[32] = {
-    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x1.e840b4ac4e4d2p-3,  0x1.40645f0c6651cp-2,  0x1.88e9c2c1b9ff8p-2,  0x1.ce0a44eb17bccp-2},
+    {0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
     0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
     0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
     0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
     0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
     0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
-    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull}};
 
 CFD_HDF bool zeroinfnan(uint32_t i) { return 2u * i - 1u >= 2u * 0x7f800000u - 1u; }
 // 0: not an integer, 1: odd integer, 2: even integer
@@ -107,13 +113,13 @@ CFD_HDF int checkint(uint32_t iy) {
 }
 
 // log2(x) for a positive normal(ised) float's bits (POWF_SCALE_BITS = 0 on x86_64)
-CFD_HDF double powf_log2(uint32_t ix) {
+CFD_HDF double powf_log2(uint32_t ix, const PowfTables &T = kPowfTables) {
     const uint32_t tmp = ix - 0x3f330000u;
     const int i = (tmp >> 19) % 16;
     const uint32_t top = tmp & 0xff800000u;
     const uint32_t iz = ix - top;
     const int k = (int32_t)top >> 23;
-    const double invc = kLog2InvC[i], logc = kLog2C[i];
+    const double invc = T.invc[i], logc = T.logc[i];
     const double z = (double)asf32u(iz);
     const double r = z * invc - 1.0;
     const double y0 = logc + (double)k;
@@ -129,12 +135,12 @@ CFD_HDF double powf_log2(uint32_t ix) {
 
 // 2^ylogx in double, before the final rounding to float (EXP2F_TABLE_BITS = 5,
 // shift 0x1.8p+52 / 32)
-CFD_HDF double powf_exp2(double ylogx, uint32_t sign_bias) {
+CFD_HDF double powf_exp2(double ylogx, uint32_t sign_bias, const PowfTables &T = kPowfTables) {
     double kd = ylogx + 0x1.8p+47;
     const unsigned long long ki = asu64d(kd);
     kd -= 0x1.8p+47;
     const double rr = ylogx - kd;
-    unsigned long long t = kExp2Tab[ki % 32];
+    unsigned long long t = T.exp2[ki % 32];
     t += (ki + sign_bias) << 47;
     const double s = asf64d(t);
     const double zz = 0x1.c6af84b912394p-5 * rr + 0x1.ebfce50fac4f3p-3;
@@ -145,7 +151,7 @@ CFD_HDF double powf_exp2(double ylogx, uint32_t sign_bias) {
     return e;
 }
 
-CFD_HDF float powf(float x, float y) {
+CFD_HDF float powf(float x, float y, const PowfTables &T = kPowfTables) {
     uint32_t sign_bias = 0;
     uint32_t ix = asu32f(x);
     const uint32_t iy = asu32f(y);
@@ -176,13 +182,13 @@ CFD_HDF float powf(float x, float y) {
             ix -= 23u << 23;
         }
     }
-    const double ylogx = (double)y * powf_log2(ix);
+    const double ylogx = (double)y * powf_log2(ix, T);
     if ((asu64d(ylogx) >> 47 & 0xffff) >=
         (asu64d(126.0) >> 47)) {
         if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -asf32u(0x7f800000u) : asf32u(0x7f800000u);
         if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
     }
-    return (float)powf_exp2(ylogx, sign_bias);
+    return (float)powf_exp2(ylogx, sign_bias, T);
 }
 
 // ---- fast exact paths for the two exponents the reference uses ------------
@@ -230,17 +236,17 @@ CFD_HDF bool powf_sqrt_fast(float s, float &r) {
 }
 
 // NumPy float32 scalar x**2, bit for bit (glibc powf(x, 2.0f))
-CFD_HDF float powf_sq(float x) {
+CFD_HDF float powf_sq(float x, const PowfTables &T = kPowfTables) {
     float p;
     if (powf_sq_fast(x, p)) return p;
-    return powf(x, 2.0f);
+    return powf(x, 2.0f, T);
 }
 
 // NumPy float32 scalar x**0.5, bit for bit (glibc powf(x, 0.5f))
-CFD_HDF float powf_sqrt(float x) {
+CFD_HDF float powf_sqrt(float x, const PowfTables &T = kPowfTables) {
     float r;
     if (powf_sqrt_fast(x, r)) return r;
-    return powf(x, 0.5f);
+    return powf(x, 0.5f, T);
 }
 
 }  // namespace libm
