@@ -50,6 +50,8 @@ for s in "$@"; do
     pmc_write_pred) step pmc_write_pred 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_pred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline ;;
     predsweep) step predsweep 600 python scripts/pred_sweep.py ;;
     sq_pred) step sq_pred 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES -d gpurun_out/sq_pred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline ;;
+    sq_k4a) step sq_k4a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES -d gpurun_out/sq_k4a -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 40 --no-cpu-baseline ;;
+    sq_k4b) step sq_k4b 300 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_WAVES -d gpurun_out/sq_k4b -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 40 --no-cpu-baseline ;;
     tests2d) step pytest_2d 900 python -m pytest tests -m gpu -q -k "jacobi2d or rbgs2d or time_step or golden" ;;
     sweep2d) step sweep2d 900 bash -c 'for K in ${K2D:-8 10 12}; do echo "K=$K"; python bench.py --workload jacobi2d_8192_f64 --no-cpu-baseline --steps 3 --tb $K | grep -o "\"value\": [0-9.]*\|avg_launch_ms\": [0-9.]*" | tr "\n" " "; echo; done' ;;
     testslocal) step pytest_local 900 python -m pytest tests -m gpu -q -x -k "local_group" ;;
