@@ -63,6 +63,8 @@ PROTOTYPES = {
     "cfd_absmax_f32": (c_int, [P, c_size_t, P, P]),
     "cfd_absmax2_f32": (c_int, [P, P, c_size_t, P, P]),
     "cfd_energy_mean2d_f32": (c_int, [P, P, c_size_t, P, P]),
+    "cfd_energy_mean_clip2d_f32": (c_int, [P, P, c_size_t, P, c_float, c_float, P]),
+    "cfd_apply_bc_ibm2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_int, P, c_double, P]),
     "cfd_vorticity_absmax2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, P, P]),
     "cfd_vorticity2d_f32": (c_int, [P, P, P, P, c_int, c_int, c_double, c_double, P]),
     "cfd_nonfinite_count_f32": (c_int, [P, P, c_size_t, P, P]),
@@ -84,6 +86,8 @@ PROTOTYPES = {
     "cfd_numpy_pow_f64": (c_int, [P, c_double, P, c_size_t, P]),
     "cfd_absmax2_f64": (c_int, [P, P, c_size_t, P, P]),
     "cfd_energy_mean2d_f64": (c_int, [P, P, c_size_t, P, P]),
+    "cfd_energy_mean_clip2d_f64": (c_int, [P, P, c_size_t, P, c_double, c_double, P]),
+    "cfd_apply_bc_ibm2d_f64": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_int, P, c_double, P]),
     "cfd_vorticity2d_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_double, P]),
     "cfd_nonfinite_count_f64": (c_int, [P, P, c_size_t, P, P]),
     "cfd_rbgs2d_f64": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_float, c_int, c_double, P, P, P]),
@@ -123,6 +127,7 @@ PROTOTYPES = {
     "cfd_set_jacobi3d_prefetch": (c_int, [c_int]),
     "cfd_set_jacobi2d_blocking": (c_int, [c_int]),
     "cfd_set_jacobi2d_staging": (c_int, [c_int]),
+    "cfd_set_jacobi2d_workgroup_march": (c_int, [c_int]),
     "cfd_reset_tuning": (c_int, []),
     "cfd_get_last_tbr_shape": (c_int, [ctypes.POINTER(c_int)] * 4),
     "cfd_set_small2d_shape": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),

@@ -49,6 +49,8 @@ static Tuning process_defaults() {
         t.j2s_vec = env_int("CFD_J2_SMALL_VEC", 1) == 1 ? 1 : 0;  // 0: 16 bytes per lane
         const int dd = env_int("CFD_J2_DMA", t.j2_dma);
         t.j2_dma = dd == 0 || dd == 4 || dd == 6 ? dd : t.j2_dma;
+        const int wg = env_int("CFD_J2_WGM", t.j2_wgm);
+        t.j2_wgm = wg == 0 || wg == 2 || wg == 4 || wg == 8 ? wg : t.j2_wgm;
         t.gs_rw = env_int("CFD_GS_SMALL_RW", 2) == 1 ? 1 : 2;
         t.gs_vec = env_int("CFD_GS_SMALL_VEC", 1) == 4 ? 4 : 1;
         t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;
@@ -91,6 +93,11 @@ int timing_begin(hipStream_t s) {
     const int k = (int)g_timing.used++;
     if (hipEventRecord(g_timing.start[k], s) != hipSuccess) return -1;
     return k;
+}
+
+// a timing_begin whose work did not run (the last pair only)
+void timing_cancel(int k) {
+    if (k >= 0 && (size_t)k + 1 == g_timing.used) --g_timing.used;
 }
 
 void timing_end(int k, hipStream_t s, long long sweeps) {

@@ -24,6 +24,7 @@ void set_error(const char *fmt, ...);
 // bench timing hooks (capi.hip): event pair around a solve's sweep launches
 int timing_begin(hipStream_t s);
 void timing_end(int k, hipStream_t s, long long sweeps);
+void timing_cancel(int k);
 
 #define CFD_CHECK_HIP(expr)                                                          \
     do {                                                                             \
@@ -155,6 +156,27 @@ __device__ inline double dpp_from_upper(double v) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// the same shifts with an `old` operand: lane 0 (from_lower) / lane 63
+// (from_upper) receive `old`, the value a neighbouring wave supplies
+__device__ inline float dpp_from_lower_old(float old, float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ inline float dpp_from_upper_old(float old, float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+__device__ inline double dpp_from_lower_old(double old, double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v), o = (unsigned long long)__double_as_longlong(old);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)o, (int)(unsigned)b, 0x138, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(o >> 32), (int)(unsigned)(b >> 32), 0x138, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ inline double dpp_from_upper_old(double old, double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v), o = (unsigned long long)__double_as_longlong(old);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)o, (int)(unsigned)b, 0x130, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(o >> 32), (int)(unsigned)(b >> 32), 0x130, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // LDS-DMA of one 1 KiB row (64 lanes x 16 B) into lds_row[0..255]: the data
 // lands in LDS without passing through VGPRs (buffer_load_dwordx4 ... lds,
 // destination M0 + 16 * lane; a lane whose offset is outside the resource
@@ -200,9 +222,14 @@ __device__ inline void wait_vmcnt() {
 // serialised ~1700 same-address double atomics (22 us at 600 x 180).  The
 // per-cell energy is formed in T, summed in double, then scaled by 1/n.
 constexpr size_t kEnergyOneBlock = (size_t)1 << 20;
+// CLIP: the step's two np.clip calls (v5.py:437-438) fused in -- each cell's
+// energy is formed from the value loaded (before the clip, as v5.py:431-435
+// reads it), then the clipped value is stored (NaN passes like np.clip).
 template <typename T>
-__global__ __launch_bounds__(1024) void k_energy_mean_1blk(const T *__restrict__ u, const T *__restrict__ v,
-                                                           size_t n, double *out) {
+__device__ inline T clip_val(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
+template <typename T, bool CLIP = false>
+__global__ __launch_bounds__(1024) void k_energy_mean_1blk(T *__restrict__ u, T *__restrict__ v, size_t n,
+                                                           double *out, T lo, T hi) {
     // 8 independent partial sums per thread (8 loads of each field in flight,
     // elements c, c + 1024, ..., c + 7 * 1024 of a round), folded in a fixed order
     constexpr int U = 8;
@@ -220,10 +247,24 @@ __global__ __launch_bounds__(1024) void k_energy_mean_1blk(const T *__restrict__
         }
 #pragma unroll
         for (int q = 0; q < U; ++q) s[q] += (double)(T(0.5) * (a[q] * a[q] + b[q] * b[q]));
+        if constexpr (CLIP) {
+#pragma unroll
+            for (int q = 0; q < U; ++q) {
+                u[c + q * 1024] = clip_val(a[q], lo, hi);
+                v[c + q * 1024] = clip_val(b[q], lo, hi);
+            }
+        }
     }
 #pragma unroll
     for (int q = 0; q < U; ++q)
-        if (c + q * 1024 < n) s[q] += (double)(T(0.5) * (u[c + q * 1024] * u[c + q * 1024] + v[c + q * 1024] * v[c + q * 1024]));
+        if (c + q * 1024 < n) {
+            const T a = u[c + q * 1024], b = v[c + q * 1024];
+            s[q] += (double)(T(0.5) * (a * a + b * b));
+            if constexpr (CLIP) {
+                u[c + q * 1024] = clip_val(a, lo, hi);
+                v[c + q * 1024] = clip_val(b, lo, hi);
+            }
+        }
     double t = s[0];
 #pragma unroll
     for (int q = 1; q < U; ++q) t += s[q];
@@ -236,6 +277,66 @@ __global__ __launch_bounds__(1024) void k_energy_mean_1blk(const T *__restrict__
 #pragma unroll
         for (int k = 0; k < 16; ++k) r += part[k];
         *out = r * (1.0 / (double)n);
+    }
+}
+
+// apply_ibm_fast's factor on one cell (v5.py:228-237): float64 mask, float64
+// product, rounded to the field's type
+template <typename T>
+__device__ inline T ibm_cell(T x, double mv, double fs) {
+    return mv > 0.0 ? (T)((double)x * (1.0 - mv * fs)) : x;
+}
+
+// apply_boundary_conditions (v5.py:349-360, net effect as k_bc in
+// fields2d.hip) followed by apply_ibm_fast (v5.py:228-237) in ONE launch.
+// Every cell is written by one thread, which applies the BC assignment and
+// then the IBM factor, the reference's order: threads t < nx own rows 0 and
+// ny - 1; threads 1 <= t < ny - 1 own columns 0, nx - 2 and nx - 1 of row t
+// (the outlet copy reads column nx - 2 before its IBM factor); the rest of
+// the cells go to a grid-stride loop over the mask.  m == nullptr: no IBM.
+template <typename T>
+__global__ void k_bc_ibm(T *__restrict__ u, T *__restrict__ v, const double *__restrict__ y,
+                         const double *__restrict__ m, int ny, int nx, double y_max, double v_inf, int step,
+                         double fs) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    auto mk = [&](size_t c) { return m ? m[c] : 0.0; };
+    if (t < nx) {
+        const size_t c0 = t, c1 = (size_t)(ny - 1) * nx + t;
+        u[c0] = ibm_cell(T(0), mk(c0), fs);
+        v[c0] = ibm_cell(T(0), mk(c0), fs);
+        u[c1] = ibm_cell(T(0), mk(c1), fs);
+        v[c1] = ibm_cell(T(0), mk(c1), fs);
+    }
+    if (t >= 1 && t < ny - 1) {
+        const double s = (double)step;
+        double scale = s / 1000.0;
+        scale = (1.0 < scale ? 1.0 : scale) * 0.01;
+        const double two_pi = 2.0 * 3.141592653589793;
+        const double pert = scale * sin(two_pi * y[t] / y_max + 0.02 * s);
+        const size_t r = (size_t)t * nx;
+        const T inlet = (T)(v_inf * (1.0 + pert));
+        // the outlet copy's source: column nx - 2 after the inlet assignment
+        const T uo = nx == 2 ? inlet : u[r + nx - 2], vo = nx == 2 ? T(0) : v[r + nx - 2];
+        u[r] = ibm_cell(inlet, mk(r), fs);
+        v[r] = ibm_cell(T(0), mk(r), fs);
+        if (nx > 2) {
+            u[r + nx - 2] = ibm_cell(uo, mk(r + nx - 2), fs);
+            v[r + nx - 2] = ibm_cell(vo, mk(r + nx - 2), fs);
+        }
+        u[r + nx - 1] = ibm_cell(uo, mk(r + nx - 1), fs);
+        v[r + nx - 1] = ibm_cell(vo, mk(r + nx - 1), fs);
+    }
+    if (!m) return;
+    const size_t n = (size_t)ny * nx;
+    for (size_t c = t; c < n; c += (size_t)gridDim.x * blockDim.x) {
+        const double mv = m[c];
+        if (mv > 0.0) {
+            const int i = (int)(c / nx), j = (int)(c % nx);
+            if (i >= 1 && i < ny - 1 && j >= 1 && j < nx - 2) {
+                u[c] = ibm_cell(u[c], mv, fs);
+                v[c] = ibm_cell(v[c], mv, fs);
+            }
+        }
     }
 }
 

@@ -837,6 +837,9 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
 //    and at row ends 16 single-word stores), so the wait for a chunk's DMAs is
 //    an exact vmcnt that leaves the later chunks' DMAs in flight.
 // ~13 VALU per step (the LDS-DMA kernel above: ~40).  Up to 256 rows per band.
+#ifndef CFD_LEX_ABL  // measurement aid only: 1 no barrier, 2 no stores, 4 no DMA wait, 16 no arithmetic
+#define CFD_LEX_ABL 0
+#endif
 constexpr int kLexC = 16;                     // steps per chunk
 constexpr int kLexR = 4;                      // chunks in the DMA ring
 constexpr int kLexPadL = 16, kLexPadR = 32;   // LDS row copy padding (floats)
@@ -910,7 +913,9 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
             for (int r = 0; r < kLexR; ++r) {
                 const int c = c0 + r;
                 // this chunk's DMAs: 12 (kLexR - 1) memory ops were issued after them
+#if !(CFD_LEX_ABL & 4)
                 wait_vmcnt<12 * (kLexR - 1)>();
+#endif
                 float Er[kLexC], Dr[kLexC];
                 const float4 *slot = lex_ring + (size_t)r * 8 * nt + t;
 #pragma unroll
@@ -955,9 +960,13 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
                         __float_as_int(N63[k]), __float_as_int(E), 0x130, 0xf, 0xf, false));  // wave_shl:1
                     const float S = __int_as_float(__builtin_amdgcn_update_dpp(
                         __float_as_int(S0[k]), __float_as_int(vprev), 0x138, 0xf, 0xf, false));  // wave_shr:1
+#if CFD_LEX_ABL & 16
+                    const float v = E + Dr[k] + N + S;
+#else
                     const float a = cx * (E + w);
                     const float bb = cy * (N + S);
                     const float v = ((a + bb) - Dr[k]) * cd;
+#endif
                     act[k] = rowok && (uint32_t)(jc + k - 1) < (uint32_t)jmax;
                     w = act[k] ? v : w;
                     vprev = v;
@@ -973,6 +982,7 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
                 // results: one 16-byte store per 4 columns all inside the row,
                 // single words where a group is cut by a row end
                 bool partial = false;
+#if !(CFD_LEX_ABL & 2)
 #pragma unroll
                 for (int q = 0; q < kLexC / 4; ++q) {
                     const bool full = act[4 * q] && act[4 * q + 3];
@@ -987,8 +997,14 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
                         buf_store_x1(out[k], act[k] && !full ? oW + 64u * c + 4u * k : kOob, rp);
                     }
                 }
+#else
+#pragma unroll
+                for (int q = 0; q < kLexC / 4; ++q) buf_store_x1(0.f, kOob, rp);
+#endif
                 issue(c + kLexR, r);
+#if !(CFD_LEX_ABL & 1)
                 lex_lds_barrier();
+#endif
             }
         }
     }
@@ -1475,13 +1491,43 @@ int cfd_energy_mean2d_f32(const float *u, const float *v, size_t n, double *out,
     CFD_REQUIRE(u && v && out && n > 0, "energy_mean2d: bad arguments");
     hipStream_t s = as_stream(stream);
     if (n <= kEnergyOneBlock) {
-        hipLaunchKernelGGL(k_energy_mean_1blk<float>, dim3(1), dim3(1024), 0, s, u, v, n, out);
+        hipLaunchKernelGGL((k_energy_mean_1blk<float, false>), dim3(1), dim3(1024), 0, s, const_cast<float *>(u),
+                           const_cast<float *>(v), n, out, float(0), float(0));
         CFD_LAUNCH_CHECK();
         return CFD_OK;
     }
     CFD_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(double), s));
     hipLaunchKernelGGL(k_energy_sum, dim3(grid1d(n)), dim3(256), 0, s, u, v, n, out);
     hipLaunchKernelGGL(k_scale_double, dim3(1), dim3(1), 0, s, out, 1.0 / (double)n);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_energy_mean_clip2d_f32(float *u, float *v, size_t n, double *out, float lo, float hi, void *stream) {
+    CFD_REQUIRE(u && v && out && n > 0, "energy_mean_clip2d_f32: bad arguments");
+    hipStream_t s = as_stream(stream);
+    if (n <= kEnergyOneBlock) {
+        hipLaunchKernelGGL((k_energy_mean_1blk<float, true>), dim3(1), dim3(1024), 0, s, u, v, n, out, lo, hi);
+        CFD_LAUNCH_CHECK();
+        return CFD_OK;
+    }
+    int rc = cfd_energy_mean2d_f32(u, v, n, out, stream);
+    if (!rc) rc = cfd_clip_f32(u, n, lo, hi, stream);
+    if (!rc) rc = cfd_clip_f32(v, n, lo, hi, stream);
+    return rc;
+}
+
+int cfd_apply_bc_ibm2d_f32(float *u, float *v, const double *y, int ny, int nx, double y_max, double v_inf, int step,
+                           const double *ibm_mask, double force_strength, void *stream) {
+    CFD_REQUIRE(u && v && y, "apply_bc_ibm2d_f32: null pointer");
+    CFD_REQUIRE(ny >= 2 && nx >= 2, "apply_bc_ibm2d_f32: grid must be at least 2x2");
+    int blocks = ceil_div(ny > nx ? ny : nx, 256);
+    if (ibm_mask) {
+        const int g = grid1d((size_t)ny * nx);
+        if (g > blocks) blocks = g;
+    }
+    hipLaunchKernelGGL(k_bc_ibm<float>, dim3(blocks), dim3(256), 0, as_stream(stream), u, v, y, ibm_mask, ny, nx,
+                       y_max, v_inf, step, force_strength);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }

@@ -628,13 +628,43 @@ int cfd_energy_mean2d_f64(const double *u, const double *v, size_t n, double *ou
     CFD_REQUIRE(u && v && out && n > 0, "energy_mean2d_f64: bad arguments");
     hipStream_t s = as_stream(stream);
     if (n <= kEnergyOneBlock) {
-        hipLaunchKernelGGL(k_energy_mean_1blk<double>, dim3(1), dim3(1024), 0, s, u, v, n, out);
+        hipLaunchKernelGGL((k_energy_mean_1blk<double, false>), dim3(1), dim3(1024), 0, s, const_cast<double *>(u),
+                           const_cast<double *>(v), n, out, double(0), double(0));
         CFD_LAUNCH_CHECK();
         return CFD_OK;
     }
     CFD_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(double), s));
     hipLaunchKernelGGL(k_energy_sum64, dim3(grid1d64(n)), dim3(256), 0, s, u, v, n, out);
     hipLaunchKernelGGL(k_scale64, dim3(1), dim3(1), 0, s, out, 1.0 / (double)n);
+    CFD_LAUNCH_CHECK();
+    return CFD_OK;
+}
+
+int cfd_energy_mean_clip2d_f64(double *u, double *v, size_t n, double *out, double lo, double hi, void *stream) {
+    CFD_REQUIRE(u && v && out && n > 0, "energy_mean_clip2d_f64: bad arguments");
+    hipStream_t s = as_stream(stream);
+    if (n <= kEnergyOneBlock) {
+        hipLaunchKernelGGL((k_energy_mean_1blk<double, true>), dim3(1), dim3(1024), 0, s, u, v, n, out, lo, hi);
+        CFD_LAUNCH_CHECK();
+        return CFD_OK;
+    }
+    int rc = cfd_energy_mean2d_f64(u, v, n, out, stream);
+    if (!rc) rc = cfd_clip_f64(u, n, lo, hi, stream);
+    if (!rc) rc = cfd_clip_f64(v, n, lo, hi, stream);
+    return rc;
+}
+
+int cfd_apply_bc_ibm2d_f64(double *u, double *v, const double *y, int ny, int nx, double y_max, double v_inf, int step,
+                           const double *ibm_mask, double force_strength, void *stream) {
+    CFD_REQUIRE(u && v && y, "apply_bc_ibm2d_f64: null pointer");
+    CFD_REQUIRE(ny >= 2 && nx >= 2, "apply_bc_ibm2d_f64: grid must be at least 2x2");
+    int blocks = ceil_div(ny > nx ? ny : nx, 256);
+    if (ibm_mask) {
+        const int g = grid1d64((size_t)ny * nx);
+        if (g > blocks) blocks = g;
+    }
+    hipLaunchKernelGGL(k_bc_ibm<double>, dim3(blocks), dim3(256), 0, as_stream(stream), u, v, y, ibm_mask, ny, nx,
+                       y_max, v_inf, step, force_strength);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }

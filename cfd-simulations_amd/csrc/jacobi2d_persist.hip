@@ -10,7 +10,7 @@
 // intermediate levels eroding into an NI-row / NI-lane halo, and owns its
 // inner (32 - 2 NI) x (64 - 2 NI) cells.  Own cells stay in registers from
 // block to block; after a block the tile publishes them as 8-byte {value,
-// tag} granules (sc1 stores, tag = block + 1) into a ring of granule planes,
+// tag} granules (sc1 stores, tag = solve epoch << 16 | block + 1) into a ring of granule planes,
 // and before the next block it polls its halo cells (owned by its 8
 // neighbour tiles) until their tags match.  A level is one LDS exchange of the
 // waves' rows (double-buffered: one barrier per level); x-neighbours by DPP.
@@ -31,7 +31,9 @@
 // a neighbour read phi only at its start, which preceded its block 0 output
 // that this tile consumed (hence nb >= 2 blocks, iterations > NI).  Every poll
 // is bounded (20 s of the 100 MHz clock by default, cfd_set_persistent_launch);
-// an expired one leaves phi all NaN and counts a failure (cfd_persistent_status).
+// an expired one leaves phi all NaN and counts a failure (cfd_persistent_status):
+// the last workgroup to finish (a ticket counter) checks and resets the status,
+// so a solve is this one launch with no prologue or epilogue kernel.
 // The launch is cooperative (launch_persistent): the runtime guarantees that
 // every tile is resident at once, or refuses and the launch-per-pass path runs.
 #include "internal.hpp"
@@ -51,8 +53,9 @@ struct JPersistArgs {
     const float *src;   // div, or the precomputed rhs (pre)
     const uint8_t *mask;
     unsigned long long *G;  // kJGSlots planes of ny * nx granules
-    int *status;            // bit 0: a poll expired
+    int *status;            // [0]: bit 0 a poll expired; [1]: workgroups finished (both 0 between solves)
     int *fail;              // the device's persistent-failure counter (cfd_persistent_status)
+    unsigned epoch;         // this solve's tag prefix: granule tags are epoch << 16 | block + 1
     unsigned long long spin;  // poll bound, 100 MHz ticks
     int ny, nx, nseg, niters, pre;
     float dx2, dtv;
@@ -121,7 +124,7 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
             bool more = false;
 #pragma unroll
             for (int j = 0; j < kJRW; ++j) {
-                if (need[j] && (unsigned)(g[j] >> 32) == (unsigned)k) {
+                if (need[j] && (unsigned)(g[j] >> 32) == (a.epoch << 16 | (unsigned)k)) {
                     A[j] = __uint_as_float((unsigned)g[j]);
                     need[j] = false;
                 }
@@ -172,7 +175,8 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
         if (k + 1 < nb) {
 #pragma unroll
             for (int j = 0; j < kJRW; ++j)
-                if (own[j]) jgstore(a.G + (size_t)(k % kJGSlots) * plane + off[j], A[j], (unsigned)(k + 1));
+                if (own[j])
+                    jgstore(a.G + (size_t)(k % kJGSlots) * plane + off[j], A[j], a.epoch << 16 | (unsigned)(k + 1));
         }
         lds_barrier_j();  // the next block's LDS writes follow every wave's last reads
     }
@@ -181,16 +185,29 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
         if (own[j]) a.phi[off[j]] = A[j];
         if (MASK && edgez[j]) a.phi[off[j]] = 0.f;
     }
-    if (broken && lane == 0) atomicOr(a.status, 1);
-}
-
-// an expired poll leaves garbage: the whole result becomes NaN (so it cannot
-// pass for a solution: the health check, v5.py:601, sees it) and the device's
-// failure counter counts the solve.  One workgroup that normally exits at once.
-__global__ __launch_bounds__(1024) void k_jp_status(const int *status, float *phi, size_t n, int *fail) {
-    if (!*status) return;
-    for (size_t c = threadIdx.x; c < n; c += blockDim.x) phi[c] = __int_as_float(0x7fc00000);
-    if (threadIdx.x == 0 && fail) atomicAdd(fail, 1);
+    // The last workgroup to finish reads the status: an expired poll left
+    // garbage, so the whole result becomes NaN (it cannot pass for a solution:
+    // the health check, v5.py:601, sees it) and the device's failure counter
+    // counts the solve.  It then zeroes both words for the ring's next solve.
+    __shared__ int last;
+    const int any_broken = __syncthreads_or(broken ? 1 : 0);
+    if (threadIdx.x == 0) {
+        if (any_broken) atomicOr(a.status, 1);
+        __threadfence();  // this workgroup's phi stores and status before its ticket
+        last = atomicAdd(a.status + 1, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        for (size_t c = threadIdx.x; c < plane; c += blockDim.x) a.phi[c] = __int_as_float(0x7fc00000);
+        if (threadIdx.x == 0 && a.fail) atomicAdd(a.fail, 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(a.status, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.status + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 int jtiles_for(int NI, int ny, int nx, int *nseg) {
@@ -229,6 +246,7 @@ int jresident_tiles() {
 struct JRing {
     void *p[kMaxDevices] = {};
     size_t bytes[kMaxDevices] = {};
+    unsigned epoch[kMaxDevices] = {};  // the last solve's tag prefix (0: reset the ring first)
     hipEvent_t done[kMaxDevices] = {};
     hipStream_t last[kMaxDevices] = {};
 };
@@ -245,6 +263,7 @@ void *ring_acquire(int dev, size_t bytes, hipStream_t s, int *rc) {
         }
         r.p[dev] = nullptr;
         r.bytes[dev] = 0;
+        r.epoch[dev] = 0;
         if (hipMalloc(&r.p[dev], bytes) != hipSuccess) {
             *rc = CFD_E_HIP;
             set_error("jacobi2d persistent: ring allocation of %zu bytes failed", bytes);
@@ -264,6 +283,7 @@ void *ring_acquire(int dev, size_t bytes, hipStream_t s, int *rc) {
     }
     return r.p[dev];
 }
+unsigned &t_ring_epoch(int dev) { return t_ring.epoch[dev]; }
 void ring_release(int dev, hipStream_t s) {
     JRing &r = t_ring;
     if (hipEventRecord(r.done[dev], s) == hipSuccess) r.last[dev] = s;
@@ -279,6 +299,7 @@ void release_thread_rings() {
         if (r.done[d]) (void)hipEventDestroy(r.done[d]);
         r.p[d] = nullptr;
         r.bytes[d] = 0;
+        r.epoch[d] = 0;
         r.done[d] = nullptr;
         r.last[d] = nullptr;
     }
@@ -289,6 +310,7 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
     *rc = CFD_OK;
     const int NI = tuning().j2p_ni;
     if (!tuning().j2_persist || iterations <= NI || ny < 3 || nx < 3) return 0;
+    if ((iterations + NI - 1) / NI >= 0xffff) return 0;  // block numbers are 16-bit tag fields
     JPersistArgs a;
     a.phi = phi;
     a.src = src;
@@ -328,12 +350,20 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
     if (!p) return 1;
     a.G = reinterpret_cast<unsigned long long *>(p);
     a.status = reinterpret_cast<int *>(p + gbytes);
-    // a stale granule of an earlier solve carries a valid-looking tag: reset the ring
-    if (hipMemsetAsync(p, 0, gbytes + 256, s) != hipSuccess) {
-        *rc = CFD_E_HIP;
-        set_error("jacobi2d persistent: ring reset failed");
-        return 1;
+    // Granule tags carry a per-ring solve epoch, so a granule left by an earlier
+    // solve never matches a poll of this one.  The ring is zeroed only when it
+    // is new or the 16-bit epoch wraps (a plane a run of short solves leaves
+    // alone could otherwise hold a same-tag granule 65536 solves old).
+    unsigned &ep = t_ring_epoch(dev);
+    if (ep == 0 || ep == 0xffffu) {
+        if (hipMemsetAsync(p, 0, gbytes + 256, s) != hipSuccess) {
+            *rc = CFD_E_HIP;
+            set_error("jacobi2d persistent: ring reset failed");
+            return 1;
+        }
+        ep = 0;
     }
+    a.epoch = ++ep;
     a.fail = persist_fail_word();
     a.spin = persist_poll_ticks();
     const void *f = nullptr;
@@ -347,7 +377,6 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
         *rc = CFD_E_HIP;
         return 1;
     }
-    hipLaunchKernelGGL(k_jp_status, dim3(1), dim3(1024), 0, s, a.status, phi, plane, a.fail);
     ring_release(dev, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -335,6 +335,23 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
     CFD_REQUIRE(resid_every <= 0 || resid_out, "jacobi2d: resid_every > 0 needs resid_out");
     if (iters == 0) return CFD_OK;
     int rc;
+    if constexpr (std::is_same_v<T, float>) {
+        // small f32 grids (those the launch-per-pass kernel would take): the
+        // whole solve as one persistent launch, any row length.  It keeps the
+        // edge rows itself and forms dx2 * div / dt per cell, so neither the
+        // edge-row copy nor the RHS prologue below runs.
+        if (tuning().j2_blocking == 0 && resid_every <= 0 && ny >= 3 &&
+            auto_levels2d<T>(ny, nx) != kDefaultLevels2d) {
+            int prc = CFD_OK;
+            const int tk = timing_begin(s);
+            if (jacobi2d_persist_solve(phi, div, false, mask, ny, nx, dx2, dtv, iters, s, &prc)) {
+                if (prc) return prc;
+                timing_end(tk, s, iters);
+                return CFD_OK;
+            }
+            timing_cancel(tk);
+        }
+    }
     // Dirichlet rows 0 and ny-1 of the first output buffer (masked -> 0)
     if ((rc = fix_edge_rows<T>(phi, tmp, mask, ny, nx, s))) return rc;
     const int nres = resid_every > 0 ? iters / resid_every : 0;
@@ -354,19 +371,6 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
     const bool vec_ok = (nx % V == 0) && aligned16(src) && aligned16(phi) && aligned16(tmp);
     T *a = phi, *b = tmp;
     const int tk = timing_begin(s);
-    if constexpr (std::is_same_v<T, float>) {
-        // small f32 grids (those the launch-per-pass kernel would take): the
-        // whole solve as one persistent launch, any row length
-        if (tuning().j2_blocking == 0 && resid_every <= 0 && ny >= 3 &&
-            auto_levels2d<T>(ny, nx) != kDefaultLevels2d) {
-            int prc = CFD_OK;
-            if (jacobi2d_persist_solve(phi, src, pre, mask, ny, nx, dx2, dtv, iters, s, &prc)) {
-                if (prc) return prc;
-                timing_end(tk, s, iters);
-                return CFD_OK;
-            }
-        }
-    }
     if (tuning().j2_blocking != 1 && vec_ok && resid_every <= 0 && iters >= 2 && ny >= 3) {
         // temporally blocked: passes of K sweeps, the remainder last
         // small grids (auto depth 2) take the preloaded kernel, 4 sweeps a pass
@@ -1193,6 +1197,13 @@ int cfd_set_jacobi2d_staging(int rows_ahead) {
     CFD_REQUIRE(rows_ahead == 0 || rows_ahead == 4 || rows_ahead == 6,
                 "2-D staging depth must be 0 (register prefetch), 4 or 6 rows");
     tuning().j2_dma = rows_ahead;
+    return CFD_OK;
+}
+
+int cfd_set_jacobi2d_workgroup_march(int waves) {
+    CFD_REQUIRE(waves == 0 || waves == 2 || waves == 4 || waves == 8,
+                "workgroup march: 0 (per-wave march), 2, 4 or 8 waves");
+    tuning().j2_wgm = waves;
     return CFD_OK;
 }
 

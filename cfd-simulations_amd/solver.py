@@ -232,6 +232,14 @@ class OptimizedTurbulentSolver:
         call("cfd_apply_bc2d" + self._sfx, ptr(u), ptr(v), ptr(self._y_dev), cfg.ny, cfg.nx, float(cfg.y_max),
              float(cfg.V_inf), int(self.step), stream_handle())
 
+    def _bc_ibm(self, u, v, force_strength):
+        """apply_boundary_conditions followed by apply_ibm_fast (when the
+        cylinder mask exists) as one kernel, bit-identical to the two calls."""
+        cfg = self.config
+        call("cfd_apply_bc_ibm2d" + self._sfx, ptr(u), ptr(v), ptr(self._y_dev), cfg.ny, cfg.nx, float(cfg.y_max),
+             float(cfg.V_inf), int(self.step), ptr(self.ibm_mask) if self._has_ibm else None, float(force_strength),
+             stream_handle())
+
     def compute_energy(self):  # v5.py:362-363
         return 0.5 * (self.u ** 2 + self.v ** 2)
 
@@ -298,10 +306,9 @@ class OptimizedTurbulentSolver:
                           u_star=self.u_star, v_star=self.v_star, tau=self.tau_supg)
         if not cfg.use_supg:
             self.tau_supg.zero_()
-        self.apply_boundary_conditions(self.u_star, self.v_star)
         force_strength = min(1.0, self.step / cfg.initial_steps)
-        if self._has_ibm:
-            K.apply_ibm_fast(self.u_star, self.v_star, self.ibm_mask, force_strength)
+        # apply_boundary_conditions then apply_ibm_fast (v5.py:405-407), one launch
+        self._bc_ibm(self.u_star, self.v_star, force_strength)
         call("cfd_divergence2d" + self._sfx, ptr(self.u_star), ptr(self.v_star), ptr(self.div_u_star), cfg.ny,
              cfg.nx, float(cfg.dx), float(cfg.dy), ptr(self._scal[1:2]) if diag else None, s)
         self.solve_pressure_fast(self.div_u_star)
@@ -314,21 +321,18 @@ class OptimizedTurbulentSolver:
             # the reference recomputes div for logging only; keep div_u_star as the pre-pressure one
             call("cfd_divergence2d" + self._sfx, ptr(self.u_star), ptr(self.v_star), ptr(self.div_u_star),
                  cfg.ny, cfg.nx, float(cfg.dx), float(cfg.dy), None, s)
-        self.apply_boundary_conditions(self.u, self.v)
-        if self._has_ibm:
-            K.apply_ibm_fast(self.u, self.v, self.ibm_mask, force_strength)
+        self._bc_ibm(self.u, self.v, force_strength)  # v5.py:424-425
         if diag and self.dtype == torch.float64:
             call("cfd_vorticity2d_f64", ptr(self.u), ptr(self.v), ptr(self._mask_u8), None, ptr(self._scal[4:5]),
                  cfg.ny, cfg.nx, float(cfg.dx), float(cfg.dy), s)
         elif diag:
             call("cfd_vorticity_absmax2d_f32", ptr(self.u), ptr(self.v), ptr(self._mask_u8), cfg.ny,
                  cfg.nx, float(cfg.dx), float(cfg.dy), ptr(self._scal[4:5]), s)
-        call("cfd_energy_mean2d" + self._sfx, ptr(self.u), ptr(self.v), self.u.numel(), ptr(self._energy_slot()),
-             s)
+        # the energy of the unclipped fields (v5.py:431-435), then both clips (v5.py:437-438)
+        call("cfd_energy_mean_clip2d" + self._sfx, ptr(self.u), ptr(self.v), self.u.numel(),
+             ptr(self._energy_slot()), -float(cfg.max_velocity), float(cfg.max_velocity), s)
         self._energy_steps.append(self.step)
         self.times.append(self.step * dt)
-        call("cfd_clip" + self._sfx, ptr(self.u), self.u.numel(), -float(cfg.max_velocity), float(cfg.max_velocity), s)
-        call("cfd_clip" + self._sfx, ptr(self.v), self.v.numel(), -float(cfg.max_velocity), float(cfg.max_velocity), s)
         self.step += 1
         return dt
 

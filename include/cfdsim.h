@@ -86,6 +86,12 @@ int cfd_get_jacobi2d_levels(void);
  * the faster of the two on MI355X).  Same bits either way (a tuning knob, per
  * host thread like the others). */
 int cfd_set_jacobi2d_staging(int rows_ahead);
+/* Unmasked 8-sweep 2-D passes as a workgroup-wide row march of `waves` waves
+ * side by side in x (2, 4 or 8; x-halos between the waves through LDS, halo
+ * lanes only at the workgroup's outer edges); 0 = the per-wave march
+ * (default).  Bit-identical either way.  Per host thread, like the other
+ * tuning setters; env CFD_J2_WGM sets the process default. */
+int cfd_set_jacobi2d_workgroup_march(int waves);
 int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, double *resid_out, void *stream);
@@ -210,6 +216,17 @@ int cfd_apply_ibm2d_f32(float *u, float *v, const double *ibm_mask, int n, doubl
                         void *stream);
 /* np.clip(a, lo, hi, out=a), v5.py:437-438. */
 int cfd_clip_f32(float *a, size_t n, float lo, float hi, void *stream);
+/* The solver step's fused tails (one launch each; the same results as the
+ * separate calls in the reference's order):
+ *   apply_boundary_conditions then apply_ibm_fast (v5.py:349-360, :228-237;
+ *   ibm_mask may be NULL: BC only), and
+ *   the mean kinetic energy (v5.py:431-435) of u, v followed by the two
+ *   np.clip calls (v5.py:437-438): the energy is of the unclipped values. */
+int cfd_apply_bc_ibm2d_f32(float *u, float *v, const double *y, int ny, int nx, double y_max,
+                           double v_inf, int step, const double *ibm_mask, double force_strength,
+                           void *stream);
+int cfd_energy_mean_clip2d_f32(float *u, float *v, size_t n, double *out, float lo, float hi,
+                               void *stream);
 
 /* ------------------------------------------------------------- reductions */
 /* Each writes one value to a device scalar; the caller zeroes `out` for the
@@ -274,6 +291,11 @@ int cfd_numpy_pow_f64(const double *x, double y, double *out, size_t n, void *st
 /* max(|a|, |b|) (b may be NULL) into a zeroed device double */
 int cfd_absmax2_f64(const double *a, const double *b, size_t n, double *out, void *stream);
 int cfd_energy_mean2d_f64(const double *u, const double *v, size_t n, double *out, void *stream);
+int cfd_apply_bc_ibm2d_f64(double *u, double *v, const double *y, int ny, int nx, double y_max,
+                           double v_inf, int step, const double *ibm_mask, double force_strength,
+                           void *stream);
+int cfd_energy_mean_clip2d_f64(double *u, double *v, size_t n, double *out, double lo, double hi,
+                               void *stream);
 /* compute_vorticity into w (may be NULL) and/or nanmax|w| into a zeroed
  * device double absmax (may be NULL) */
 int cfd_vorticity2d_f64(const double *u, const double *v, const uint8_t *mask, double *w,

@@ -101,6 +101,31 @@ def test_jacobi2d_staged_rows_bitexact(dtype, shape, iters, pre, blocking, stagi
         call("cfd_set_jacobi2d_blocking", 0)
 
 
+@pytest.mark.parametrize("waves", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("shape,iters,pre", [((37, 53), 17, False), ((130, 260), 31, True), ((9, 124), 16, True),
+                                             ((71, 1000), 24, False), ((300, 1500), 9, True), ((517, 40), 8, False),
+                                             ((4, 600), 8, True), ((1030, 2044), 16, True)])
+def test_jacobi2d_workgroup_march_bitexact(dtype, shape, iters, pre, waves):
+    """The workgroup-wide row march (waves side by side, x-halos through LDS)
+    at 8 sweeps per pass: bit-exact against the oracle, ragged widths
+    included (a segment's last wave partly or wholly past the row end)."""
+    call("cfd_set_jacobi2d_blocking", 8)
+    call("cfd_set_jacobi2d_workgroup_march", waves)
+    try:
+        rng = np.random.default_rng(23)
+        div = rng.standard_normal(shape).astype(dtype)
+        phi0 = rng.standard_normal(shape).astype(dtype)
+        ref = oracle.jacobi2d(div, phi0, dx=0.017, dt=np.float32(2e-4), iters=iters)
+        phi = dev(phi0)
+        K.solve_pressure_jacobi(phi, dev(div), 0.017, np.float32(2e-4), None, iters,
+                                rhs_ws=torch.empty_like(phi) if pre else None)
+        assert np.array_equal(host(phi), ref)
+    finally:
+        call("cfd_set_jacobi2d_workgroup_march", 0)
+        call("cfd_set_jacobi2d_blocking", 0)
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_jacobi2d_rhs_workspace_bitexact(dtype):
     """The RHS prologue (rhs_ws) gives the same bits as the in-register RHS."""
@@ -491,6 +516,55 @@ def test_bc_ibm_clip_bitexact(golden):
     t = dev(a)
     call("cfd_clip_f32", ptr(t), t.numel(), -5.0, 5.0, stream_handle())
     assert np.array_equal(host(t), np.clip(a, -5, 5), equal_nan=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("ny,nx", [(36, 120), (7, 2), (5, 3), (300, 257)])
+def test_fused_step_tails_match_separate_calls(dtype, ny, nx):
+    """The solver step's fused tails are the separate calls in the reference's
+    order, bit for bit: apply_bc_ibm2d == apply_bc2d then apply_ibm2d (mask
+    values on every edge row and column, so the outlet copy's source is itself
+    forced), energy_mean_clip2d == energy_mean2d then two clips."""
+    sfx = "_f32" if dtype == torch.float32 else "_f64"
+    rng = np.random.default_rng(ny * 7 + nx)
+    npd = np.float32 if dtype == torch.float32 else np.float64
+    u0 = (rng.uniform(-3, 3, (ny, nx))).astype(npd)
+    v0 = (rng.uniform(-3, 3, (ny, nx))).astype(npd)
+    m = np.where(rng.uniform(size=(ny, nx)) < 0.4, rng.uniform(0, 1, (ny, nx)), 0.0)
+    m[:, -2:] = rng.uniform(0.1, 1, (ny, 2))
+    m[0, :] = 0.5
+    # device inputs stay referenced until the kernels have run (a temporary's
+    # block can be reused by the next host-to-device copy)
+    yd, md = dev(np.linspace(-2.0, 2.0, ny)), dev(m)
+    s = stream_handle()
+    for step, mask in ((0, md), (7, md), (1500, None)):
+        fs = min(1.0, step / 1000)
+        a_u, a_v = dev(u0), dev(v0)
+        call("cfd_apply_bc2d" + sfx, ptr(a_u), ptr(a_v), ptr(yd), ny, nx, 2.0, 1.0, step, s)
+        if mask is not None:
+            call("cfd_apply_ibm2d" + sfx, ptr(a_u), ptr(a_v), ptr(mask), ny * nx, fs, s)
+        b_u, b_v = dev(u0), dev(v0)
+        call("cfd_apply_bc_ibm2d" + sfx, ptr(b_u), ptr(b_v), ptr(yd), ny, nx, 2.0, 1.0, step,
+             ptr(mask) if mask is not None else None, fs, s)
+        assert np.array_equal(host(a_u), host(b_u)) and np.array_equal(host(a_v), host(b_v)), step
+    u0[0, 0] = np.nan
+    e1 = torch.zeros(1, dtype=torch.float64, device="cuda")
+    e2 = torch.zeros(1, dtype=torch.float64, device="cuda")
+    a_u, a_v = dev(u0), dev(v0)
+    call("cfd_energy_mean2d" + sfx, ptr(a_u), ptr(a_v), a_u.numel(), ptr(e1), s)
+    call("cfd_clip" + sfx, ptr(a_u), a_u.numel(), -2.0, 2.0, s)
+    call("cfd_clip" + sfx, ptr(a_v), a_v.numel(), -2.0, 2.0, s)
+    u0[0, 0] = 0.25
+    for uu in (u0,):
+        b_u, b_v = dev(uu), dev(v0)
+        call("cfd_energy_mean_clip2d" + sfx, ptr(b_u), ptr(b_v), b_u.numel(), ptr(e2), -2.0, 2.0, s)
+        ref_u = np.clip(uu, -2, 2)
+        assert np.array_equal(host(b_u), ref_u) and np.array_equal(host(b_v), host(a_v))
+    assert np.isnan(host(e1)[0]) and np.array_equal(host(a_u)[1:], host(b_u)[1:])
+    # with the NaN cell replaced the fused energy equals the separate one
+    c_u, c_v = dev(u0), dev(v0)
+    call("cfd_energy_mean2d" + sfx, ptr(c_u), ptr(c_v), c_u.numel(), ptr(e1), s)
+    assert host(e1)[0] == host(e2)[0]
 
 
 @pytest.mark.parametrize("branch", ["gs", "jacobi"])
