@@ -837,6 +837,9 @@ __global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ ph
 //    and at row ends 16 single-word stores), so the wait for a chunk's DMAs is
 //    an exact vmcnt that leaves the later chunks' DMAs in flight.
 // ~13 VALU per step (the LDS-DMA kernel above: ~40).  Up to 256 rows per band.
+#ifndef CFD_LEX_TSTORE  // results stored transposed through LDS (0: per-lane row stores)
+#define CFD_LEX_TSTORE 1
+#endif
 #ifndef CFD_LEX_ABL  // measurement aid only: 1 no barrier, 2 no stores, 4 no DMA wait, 16 no arithmetic
 #define CFD_LEX_ABL 0
 #endif
@@ -982,7 +985,42 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
                 // results: one 16-byte store per 4 columns all inside the row,
                 // single words where a group is cut by a row end
                 bool partial = false;
-#if !(CFD_LEX_ABL & 2)
+#if CFD_LEX_TSTORE && !(CFD_LEX_ABL & 2)
+                // transposed through this wave's quarter of the ring slot just
+                // read (free until its refill below): lane l stores row
+                // 16 q + (l & 15), columns 4 (l >> 4) .. + 3 of the chunk, so
+                // a store instruction writes 16 rows x 64 contiguous bytes
+                // instead of 64 rows x 16 bytes (the scattered stores cost
+                // ~23 us of a 98 us sweep: CFD_LEX_ABL=2)
+                {
+                    float4 *tw = lex_ring + (size_t)r * 8 * nt + 64 * wv;
+#pragma unroll
+                    for (int q = 0; q < kLexC / 4; ++q)
+                        tw[q * nt + lane] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+                    const int g = lane >> 4;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int rho = 16 * q + (lane & 15), tr = 64 * wv + rho;
+                        const float4 v4 = tw[g * nt + rho];
+                        const int j0 = 1 - lag - tr + kLexC * c + 4 * g;  // first column of these 4
+                        const bool rok = tr < nrows;
+                        bool ae[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) ae[e] = rok && (uint32_t)(j0 + e - 1) < (uint32_t)jmax;
+                        const bool full = ae[0] && ae[3];
+                        const uint32_t o = (uint32_t)((b0 + tr) * nx + j0) * 4u;
+                        buf_store_x4(v4, full ? o : kOob, rp);
+                        const bool part = !full && (ae[0] || ae[1] || ae[2] || ae[3]);
+                        if (__any(part)) {
+                            buf_store_x1(v4.x, part && ae[0] ? o : kOob, rp);
+                            buf_store_x1(v4.y, part && ae[1] ? o + 4u : kOob, rp);
+                            buf_store_x1(v4.z, part && ae[2] ? o + 8u : kOob, rp);
+                            buf_store_x1(v4.w, part && ae[3] ? o + 12u : kOob, rp);
+                        }
+                    }
+                    (void)partial;
+                }
+#elif !(CFD_LEX_ABL & 2)
 #pragma unroll
                 for (int q = 0; q < kLexC / 4; ++q) {
                     const bool full = act[4 * q] && act[4 * q + 3];
