@@ -396,6 +396,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
     // (vmcnt(0)).  (Queueing the cells' stencil inputs in LDS instead and
     // skipping their march stores measured 25 % slower: more live registers
     // and a drain per 64 cells of the same cost.)
+#ifndef CFD_PRED_DTH
+#define CFD_PRED_DTH 64  // queued cells that trigger a drain (1..64)
+#endif
     constexpr int kPQ = 512;  // >= 63 + the 64 VEC cells one row appends
     __shared__ uint32_t pq_idx_all[4][kPQ];
     uint32_t *const pq_idx = pq_idx_all[wv];
@@ -520,7 +523,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
         pstv<VEC>(uo, rus, o);
         pstv<VEC>(vo, rvs, o);
         if (SUPG && a.tau) pstv<VEC>(to, rt, o);
-        while (SUPG && qn >= kWave) drain(kWave);  // (after the row's stores)
+        // (after the row's stores; at CFD_PRED_DTH queued cells: their
+        // stencil rows are still in L2 when few rows have passed)
+        while (SUPG && qn >= CFD_PRED_DTH) drain(qn < kWave ? qn : kWave);
         Um = Uc;
         Vm = Vc;
         Uc = Up;
