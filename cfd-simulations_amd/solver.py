@@ -234,8 +234,15 @@ class OptimizedTurbulentSolver:
 
     def _bc_ibm(self, u, v, force_strength):
         """apply_boundary_conditions followed by apply_ibm_fast (when the
-        cylinder mask exists) as one kernel, bit-identical to the two calls."""
+        cylinder mask exists) as one kernel, bit-identical to the two calls.
+        A subclass with its own boundary conditions (the lid-driven cavity)
+        gets its method, then the IBM call."""
         cfg = self.config
+        if type(self).apply_boundary_conditions is not OptimizedTurbulentSolver.apply_boundary_conditions:
+            self.apply_boundary_conditions(u, v)
+            if self._has_ibm:
+                K.apply_ibm_fast(u, v, self.ibm_mask, force_strength)
+            return
         call("cfd_apply_bc_ibm2d" + self._sfx, ptr(u), ptr(v), ptr(self._y_dev), cfg.ny, cfg.nx, float(cfg.y_max),
              float(cfg.V_inf), int(self.step), ptr(self.ibm_mask) if self._has_ibm else None, float(force_strength),
              stream_handle())
