@@ -201,6 +201,12 @@ int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star
 size_t cfd_clean_divergence_workspace_bytes(int ny, int nx);
 int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, double dy,
                                int iterations, void *ws, void *stream);
+/* on = 1: two iterations on grids of at most 322 rows run as one pipelined
+ * launch (sweep 2 trailing sweep 1; fields2d.hip k_clean2_pipe) between
+ * div(u, v) and the final correction; 0 (default) = one iteration after the
+ * other, measured faster on MI355X.  Same bits.  Per
+ * host thread (env CFD_CLEAN_PIPE sets the process default). */
+int cfd_set_clean_divergence_pipeline(int on);
 /* OptimizedTurbulentSolver.apply_boundary_conditions, v5.py:349-360.
  * y: device float64 (ny) grid coordinates (np.linspace, v5.py:272). */
 int cfd_apply_bc2d_f32(float *u, float *v, const double *y, int ny, int nx, double y_max,

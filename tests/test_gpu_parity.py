@@ -476,20 +476,32 @@ def test_project_and_clean_divergence_bitexact(golden):
     assert np.array_equal(host(u), cu) and np.array_equal(host(v), cv)
 
 
+@pytest.mark.parametrize("pipe", [1, 0])
 @pytest.mark.parametrize("ny,nx", [(3, 3), (3, 50), (4, 7), (66, 30), (67, 30), (130, 17), (180, 600),
+                                   (194, 33), (258, 70), (322, 51), (323, 20), (36, 1200),
                                    (514, 9), (515, 9), (1030, 40)])
-def test_clean_divergence_lexicographic_shapes(ny, nx):
+def test_clean_divergence_lexicographic_shapes(ny, nx, pipe):
     """The serial lexicographic phi sweep of clean_divergence_fast (v5.py:250-253)
     on ragged shapes: one and several waves per band, a band edge inside a wave,
-    a single-row last band (row above and below both from memory), several bands."""
-    rng = np.random.default_rng(ny * 1000 + nx)
-    u0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
-    v0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
-    dx, dy = 20.0 / (nx - 1), 6.0 / (ny - 1)
-    cu, cv = oracle.clean_divergence2d(u0, v0, dx=dx, dy=dy, iterations=2)
-    u, v = dev(u0), dev(v0)
-    K.clean_divergence_fast(u, v, dx, dy, iterations=2)
-    assert np.array_equal(host(u), cu) and np.array_equal(host(v), cv)
+    a single-row last band (row above and below both from memory), several bands;
+    both iterations pipelined in one launch (pipe, up to 322 rows) or one after
+    the other."""
+    call("cfd_set_clean_divergence_pipeline", pipe)
+    try:
+        rng = np.random.default_rng(ny * 1000 + nx)
+        u0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+        v0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+        dx, dy = 20.0 / (nx - 1), 6.0 / (ny - 1)
+        cu, cv = oracle.clean_divergence2d(u0, v0, dx=dx, dy=dy, iterations=2)
+        u, v = dev(u0), dev(v0)
+        K.clean_divergence_fast(u, v, dx, dy, iterations=2)
+        assert np.array_equal(host(u), cu) and np.array_equal(host(v), cv)
+        cu1, cv1 = oracle.clean_divergence2d(u0, v0, dx=dx, dy=dy, iterations=1)
+        u, v = dev(u0), dev(v0)
+        K.clean_divergence_fast(u, v, dx, dy, iterations=1)
+        assert np.array_equal(host(u), cu1) and np.array_equal(host(v), cv1)
+    finally:
+        call("cfd_set_clean_divergence_pipeline", 0)
 
 
 def test_bc_ibm_clip_bitexact(golden):
