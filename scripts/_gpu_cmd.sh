@@ -1,11 +1,18 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -q -x --timeout 120 --timeout-method thread tests -m gpu -k "clean_divergence" > gpurun_out/t1.log 2>&1; rc=$?
-tail -3 gpurun_out/t1.log; grep -E "^FAILED|Error" gpurun_out/t1.log | head -10
-[ $rc -eq 0 ] || exit 1
-timeout -k 10 300 python -u -m pytest -q -x --timeout 120 --timeout-method thread tests -m gpu -k "time_step or golden or cavity" > gpurun_out/t2.log 2>&1; rc=$?
-tail -2 gpurun_out/t2.log; [ $rc -eq 0 ] || exit 1
-for p in 0 1 0 1; do CFD_CLEAN_PIPE=$p timeout -k 10 120 python scripts/lex_bench.py || exit 1; done
-for p in 0 1; do for br in "--jacobi" ""; do
-  CFD_CLEAN_PIPE=$p timeout -k 10 300 python scripts/cylinder_bench.py --steps 40 --cpu-steps 0 $br > gpurun_out/cyl.json || exit 1
-  echo "pipe=$p $br $(python3 -c "import json; d=json.load(open('gpurun_out/cyl.json')); print(d['ms_per_step'], d['pressure_ms'])")"
-done; done
+: > gpurun_out/r04_slab_rehearsal.jsonl
+for R in 8 4 2; do
+  timeout -k 10 300 python scripts/slab_rehearsal.py --self --ranks $R --workload jacobi --ghost 3 >> gpurun_out/r04_slab_rehearsal.jsonl || exit 1
+  timeout -k 10 300 python scripts/slab_rehearsal.py --self --ranks $R --workload rbgs >> gpurun_out/r04_slab_rehearsal.jsonl || exit 1
+done
+tail -c 1500 gpurun_out/r04_slab_rehearsal.jsonl
+for w in rbgs3d_1024 jacobi2d_8192_f64 jacobi3d_512 jacobi3d_channel cavity2d_128; do
+  timeout -k 10 400 python bench.py --workload $w > gpurun_out/r04_bench_${w}_n1.json || exit 1
+  echo "$w $(grep -o '"value": [0-9.]*\|"frac": [0-9.]*\|avg_launch_ms": [0-9.]*' gpurun_out/r04_bench_${w}_n1.json | tr '\n' ' ')"
+done
+timeout -k 10 400 python bench.py > gpurun_out/r04_bench_jacobi3d_1024_n1.json || exit 1
+echo "headline $(grep -o '"value": [0-9.]*\|"frac": [0-9.]*\|avg_launch_ms": [0-9.]*' gpurun_out/r04_bench_jacobi3d_1024_n1.json | tr '\n' ' ')"
+timeout -k 10 400 python bench.py --workload predictor2d_8192 > gpurun_out/r04_bench_predictor2d_8192_n1.json || exit 1
+timeout -k 10 400 python bench.py --workload predictor2d_8192_f64 > gpurun_out/r04_bench_predictor2d_8192_f64_n1.json || exit 1
+timeout -k 10 300 python scripts/cylinder_bench.py --steps 30 > gpurun_out/r04_cyl_gs.json || exit 1
+timeout -k 10 300 python scripts/cylinder_bench.py --steps 30 --jacobi > gpurun_out/r04_cyl_j.json || exit 1
+cat gpurun_out/r04_cyl_gs.json gpurun_out/r04_cyl_j.json
