@@ -194,7 +194,7 @@ def cavity_bench():
     import _pkgpath
     _pkgpath.load()
     import oracle
-    from cfd_simulations_amd._lib import call
+    from cfd_simulations_amd._lib import call, lib
     from cfd_simulations_amd.solver import LidDrivenCavityConfig, LidDrivenCavitySolver
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("the cavity workload (config 1) is single-GPU")
@@ -216,9 +216,12 @@ def cavity_bench():
     ny, nx = cfg.ny, cfg.nx
     cells = (ny - 2) * (nx - 2)
     iters = cfg.pressure_iterations
-    # the solve is ONE persistent launch (jacobi2d_persist, r03) of all the
-    # sweeps; it moves the grid's 12 B per cell through HBM once per launch
-    spl = iters
+    # the small-grid solve is ONE persistent launch (jacobi2d_persist, r03) of
+    # all the sweeps, moving the grid's 12 B per cell through HBM once; if the
+    # library took the launch-per-pass path instead, it reports its depth
+    spl_c = ctypes.c_int(0)
+    persistent = int(lib().cfd_get_last_jacobi2d_path(ctypes.byref(spl_c))) == 1
+    spl = max(int(spl_c.value), 1)
     launch_ms = ms.value / max(nsw.value, 1) * spl
     alg = cells * 12
     achieved = alg / (launch_ms * 1e-3) / 1e9
@@ -233,7 +236,8 @@ def cavity_bench():
                            "projection, divergence cleaning, energy)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "kernel": "jacobi2d_persist<MASK, 8> (the whole solve in one launch; latency-bound: 190 KB per solve)",
+                     "kernel": ("jacobi2d_persist<MASK, 8> (the whole solve in one launch; latency-bound: 190 KB per solve)"
+                                if persistent else f"jacobi2d_small ({spl} sweeps per launch)"),
                      "sweeps_per_launch": spl, "cells_per_launch": cells, "algorithmic_bytes_per_launch": alg,
                      "avg_launch_ms": round(launch_ms, 5)},
         "cpu_baseline": None,

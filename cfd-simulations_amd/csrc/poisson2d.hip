@@ -325,6 +325,10 @@ __global__ void k_rhs2d(const T *__restrict__ div, T *__restrict__ rhs, size_t n
         rhs[k] = (dx2 * div[k]) / dtv;
 }
 
+// the last 2-D Jacobi solve of this thread: which path ran and its sweeps
+// per launch (cfd_get_last_jacobi2d_path, for the bench's per-launch roofline)
+thread_local int g_j2_last[2] = {0, 0};
+
 template <typename T>
 static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t *mask, int ny,
                           int nx, T dx2, T dtv, int iters, int resid_every, T *resid_out,
@@ -346,6 +350,8 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
             const int tk = timing_begin(s);
             if (jacobi2d_persist_solve(phi, div, false, mask, ny, nx, dx2, dtv, iters, s, &prc)) {
                 if (prc) return prc;
+                g_j2_last[0] = 1;
+                g_j2_last[1] = iters;
                 timing_end(tk, s, iters);
                 return CFD_OK;
             }
@@ -379,6 +385,8 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
         // wave (1 or 2), cells per lane (1 or 16 B) -- Tuning, cfd_set_small2d_shape
         const int ks = tuning().j2s_k, srw = tuning().j2s_rw, svec = tuning().j2s_vec;
         const int K = small ? ks : tuning().j2_blocking >= 2 ? tuning().j2_blocking : auto_levels2d<T>(ny, nx);
+        g_j2_last[0] = 0;
+        g_j2_last[1] = K < iters ? K : iters;
         int done = 0;
         while (done < iters) {
             int k = iters - done < K ? iters - done : K;
@@ -396,6 +404,8 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
         if (a != phi) CFD_CHECK_HIP(hipMemcpyAsync(phi, a, sizeof(T) * (size_t)ny * nx, hipMemcpyDeviceToDevice, s));
         return CFD_OK;
     }
+    g_j2_last[0] = 0;
+    g_j2_last[1] = 1;
     for (int it = 0; it < iters; ++it) {
         T *r = (resid_every > 0 && (it + 1) % resid_every == 0) ? resid_out + ((it + 1) / resid_every - 1)
                                                                  : nullptr;
@@ -1198,6 +1208,11 @@ int cfd_set_jacobi2d_staging(int rows_ahead) {
                 "2-D staging depth must be 0 (register prefetch), 4 or 6 rows");
     tuning().j2_dma = rows_ahead;
     return CFD_OK;
+}
+
+int cfd_get_last_jacobi2d_path(int *sweeps_per_launch) {
+    if (sweeps_per_launch) *sweeps_per_launch = g_j2_last[1];
+    return g_j2_last[0];
 }
 
 int cfd_set_jacobi2d_workgroup_march(int waves) {

@@ -92,6 +92,10 @@ int cfd_set_jacobi2d_staging(int rows_ahead);
  * (default).  Bit-identical either way.  Per host thread, like the other
  * tuning setters; env CFD_J2_WGM sets the process default. */
 int cfd_set_jacobi2d_workgroup_march(int waves);
+/* The calling thread's last 2-D Jacobi solve: returns 1 if it ran as one
+ * persistent launch (small grids), else 0; *sweeps_per_launch (may be NULL)
+ * = the sweeps one launch fused (the iterations, for the persistent solve). */
+int cfd_get_last_jacobi2d_path(int *sweeps_per_launch);
 int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, double *resid_out, void *stream);

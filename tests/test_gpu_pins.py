@@ -443,6 +443,25 @@ def test_persistent_cooperative_and_plain_launch_bitexact(cooperative):
     assert K.persistent_failures() == 0
 
 
+def test_last_jacobi2d_path_reports_the_persistent_solve():
+    """cfd_get_last_jacobi2d_path (the bench's per-launch roofline): the small
+    grid's solve is one persistent launch of all its sweeps, a forced
+    launch-per-pass solve reports its depth."""
+    import ctypes
+    shape = (128, 128)
+    div = dev(np.random.default_rng(5).standard_normal(shape).astype(np.float32))
+    phi = torch.zeros(shape, dtype=torch.float32, device=DEV)
+    spl = ctypes.c_int(0)
+    K.solve_pressure_jacobi(phi, div, 1 / 127, np.float32(1e-3), None, 500)
+    assert lib().cfd_get_last_jacobi2d_path(ctypes.byref(spl)) == 1 and spl.value == 500
+    call("cfd_set_small2d_jacobi_persistent", 1, 0)
+    try:
+        K.solve_pressure_jacobi(phi, div, 1 / 127, np.float32(1e-3), None, 500)
+        assert lib().cfd_get_last_jacobi2d_path(ctypes.byref(spl)) == 0 and 1 <= spl.value <= 8
+    finally:
+        call("cfd_set_small2d_jacobi_persistent", 0, 0)
+
+
 def test_persistent_forced_expiry_fails_loudly():
     """A neighbour wait that expires (forced by a 1-tick poll bound) must not
     pass silently: the persistent Jacobi leaves phi all NaN, the persistent
