@@ -1,6 +1,5 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
-for r in 1 2; do for b in base cur; do
-  if [ $b = base ]; then d=build_base; else d=.; fi
-  timeout -k 10 300 python $d/bench.py --workload cavity2d_128 --no-cpu-baseline > gpurun_out/cav.json || exit 1
-  echo "$b $(grep -o '"ms_per_step": [0-9.]*\|avg_launch_ms": [0-9.]*' gpurun_out/cav.json | tr '\n' ' ')"
-done; done
+timeout -k 10 300 python -u -m pytest -q -x --timeout 120 --timeout-method thread tests -m gpu -k "jacobi3d" > gpurun_out/t1.log 2>&1; rc=$?
+tail -2 gpurun_out/t1.log; grep -E "^FAILED" gpurun_out/t1.log | head -5
+[ $rc -eq 0 ] || exit 1
+bash scripts/ab.sh 3 "--steps 10 --warmup 2" cfd-simulations_amd/libcfdsim.so build_rotr0/libcfdsim.so || exit 1
