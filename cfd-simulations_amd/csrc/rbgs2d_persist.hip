@@ -59,9 +59,13 @@ namespace cfd {
 namespace {
 
 constexpr int kPW = 16, kPRW = 2, kPT0 = kPW * kPRW;  // waves, rows per wave, tile rows
-constexpr int kPLag = 3;                               // the stop test looks kPLag blocks back
+#ifndef CFD_GS_LAG
+#define CFD_GS_LAG 3
+#endif
+constexpr int kPLag = CFD_GS_LAG;                      // the stop test looks kPLag blocks back
 constexpr int kPGSlots = kPLag + 1;                    // granule planes (block outputs)
 constexpr int kPMSlots = 8;                            // per-block flag ring (>= kPLag + 2)
+static_assert(kPMSlots >= kPLag + 2, "flag ring too short for the lag");
 constexpr int kPMaxTiles = 256;                        // one tile per CU at most
 constexpr int kPMaxNI = 4;
 
