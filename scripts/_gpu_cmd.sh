@@ -1,10 +1,8 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
-for v in lag5 lag6; do
-  CFDSIM_LIB=$PWD/build_$v/libcfdsim.so timeout -k 10 300 python -u -m pytest -q -x --timeout 120 --timeout-method thread tests -m gpu -k "rbgs2d or time_step or persistent" > gpurun_out/t_$v.log 2>&1; rc=$?
-  echo "$v tests: $(tail -1 gpurun_out/t_$v.log)"; [ $rc -eq 0 ] || exit 1
-done
-for r in 1 2; do for v in "" lag5 lag6; do
-  if [ -z "$v" ]; then L=$PWD/cfd-simulations_amd/libcfdsim.so; else L=$PWD/build_$v/libcfdsim.so; fi
-  CFDSIM_LIB=$L timeout -k 10 300 python scripts/cylinder_bench.py --steps 40 --cpu-steps 0 > gpurun_out/cyl.json || exit 1
-  echo "${v:-lag3} $(python3 -c "import json; d=json.load(open('gpurun_out/cyl.json')); print(d['ms_per_step'], d['pressure_ms'], d['pressure_us_per_iteration'])")"
-done; done
+B="python3 bench.py --workload rbgs3d_1024 --steps 1 --warmup 0 --iters 40 --no-cpu-baseline"
+timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gs -o run --output-format csv -- $B > /dev/null || exit 1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_gs -o run --output-format csv -- $B > /dev/null || exit 1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_gs -o run --output-format csv -- $B > /dev/null || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES -d gpurun_out/sq_gs_a -o run --output-format csv -- $B > /dev/null || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_WAVES -d gpurun_out/sq_gs_b -o run --output-format csv -- $B > /dev/null || exit 1
+echo done
