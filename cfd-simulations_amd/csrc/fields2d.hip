@@ -251,7 +251,10 @@ __device__ inline Cells<VEC> pldv(__amdgpu_buffer_rsrc_t r, uint32_t ofs) {
 }
 template <int VEC>
 __device__ inline void pstv(const Cells<VEC> &c, __amdgpu_buffer_rsrc_t r, uint32_t ofs) {
-    constexpr int kNt = 2;  // streaming store policy
+#ifndef CFD_PRED_NT
+#define CFD_PRED_NT 2
+#endif
+    constexpr int kNt = CFD_PRED_NT;  // store cache policy (2: streaming)
     // (the builtins take unsigned words: pass the float bits, not a conversion)
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
