@@ -317,9 +317,18 @@ __device__ inline float supg_tau_fast(float vm, float nu, float rnu, float dt, c
 // divisions), its inputs re-read from global memory (L2: the march read them
 // a few rows ago)
 template <bool NUA>
+#ifndef CFD_PRED_ABL
+#define CFD_PRED_ABL 0
+#endif
 __device__ inline void pred_cell_exact(const PredRowArgs &a, uint32_t c, const libm::PowfTables &T) {
+#if CFD_PRED_ABL & 64  // measurement aid: the stencil from a tiny fixed window (L2-resident)
+    // u[c] below reads a.u[(c & 1023) + 2 nx]: rows 1..3, every offset in range
+    const float *__restrict__ u = a.u + (size_t)((c & 1023) + 2 * a.nx) - c;
+    const float *__restrict__ v = a.v + (size_t)((c & 1023) + 2 * a.nx) - c;
+#else
     const float *__restrict__ u = a.u;
     const float *__restrict__ v = a.v;
+#endif
     const int nx = a.nx;
     const float uc = u[c], vc = v[c];
     const float nu = NUA ? a.nu[c] : a.nu_s;
@@ -330,9 +339,14 @@ __device__ inline void pred_cell_exact(const PredRowArgs &a, uint32_t c, const l
     const float cv = conv_supg(uc, vc, vc, vE, vW, vN, vS, t, a.k);
     const float lu = laplacian(nu, uc, uE, uW, uN, uS, a.k);
     const float lv = laplacian(nu, vc, vE, vW, vN, vS, a.k);
+#if CFD_PRED_ABL & 32  // measurement aid: results computed, not stored
+    float r0 = uc + a.dt * (-cu + lu), r1 = vc + a.dt * (-cv + lv);
+    asm volatile("" ::"v"(r0), "v"(r1), "v"(t));
+#else
     a.us[c] = uc + a.dt * (-cu + lu);
     a.vs[c] = vc + a.dt * (-cv + lv);
     if (a.tau) a.tau[c] = t;
+#endif
 }
 
 #ifdef CFD_PRED_COUNT
@@ -340,9 +354,6 @@ __device__ unsigned long long g_pred_count;
 #endif
 #ifndef CFD_PRED_WPE
 #define CFD_PRED_WPE 1
-#endif
-#ifndef CFD_PRED_ABL
-#define CFD_PRED_ABL 0
 #endif
 template <bool SUPG, bool NUA, int VEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WPE, 8))) void k_predictor_rows(PredRowArgs a) {

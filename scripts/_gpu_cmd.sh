@@ -1,10 +1,6 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
-CFD_J2P_RW=4 timeout -k 10 400 python -u -m pytest -q -x --timeout 120 --timeout-method thread tests -m gpu -k "jacobi2d or persistent or cavity or time_step or golden" > gpurun_out/t1.log 2>&1; rc=$?
-tail -1 gpurun_out/t1.log; grep -E "^FAILED" gpurun_out/t1.log | head -5
-[ $rc -eq 0 ] || exit 1
-for r in 1 2; do for rw in 2 4; do
-  CFD_J2P_RW=$rw timeout -k 10 300 python scripts/cylinder_bench.py --steps 40 --cpu-steps 0 --jacobi > gpurun_out/cyl.json || exit 1
-  echo "rw=$rw cyl $(python3 -c "import json; d=json.load(open('gpurun_out/cyl.json')); print(d['ms_per_step'], d['pressure_ms'], d['pressure_us_per_iteration'])")"
-  CFD_J2P_RW=$rw timeout -k 10 300 python bench.py --workload cavity2d_128 --no-cpu-baseline > gpurun_out/cav.json || exit 1
-  echo "rw=$rw cav $(grep -o '"ms_per_step": [0-9.]*\|avg_launch_ms": [0-9.]*' gpurun_out/cav.json | tr '\n' ' ')"
-done; done
+for v in pabl32 pabl64; do
+  CFDSIM_LIB=$PWD/build_$v/libcfdsim.so timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pf_$v -o run --output-format csv -- python3 scripts/pred_fetch.py 1 > /dev/null || exit 1
+  CFDSIM_LIB=$PWD/build_$v/libcfdsim.so timeout -k 10 200 python bench.py --workload predictor2d_8192 --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/bp.json 2>/dev/null; echo "$v $(grep -o 'avg_launch_ms": [0-9.]*' gpurun_out/bp.json | head -1)"
+done
+echo ok
