@@ -214,14 +214,16 @@ __global__ __launch_bounds__(256) void k_predictor(const float *__restrict__ u,
 // / powf_sqrt_fast (libm_powf.hpp: float ops and an fma residual each, equal
 // to glibc's powf unless near a rounding midpoint, ~0.36 % / ~0.75 % per
 // call) and its two divisions through div_fast (v_rcp_f32 + one Newton step,
-// proven correctly rounded by the residual).  A cell none of whose checks can
-// be proven is NOT re-done in the march (one such lane would hold its whole
-// wave in the full powf at almost every row): its linear index goes to a
-// per-wave patch queue in LDS; whenever the queue holds 64 (and at the end of
-// the chunk) each lane recomputes one queued cell by the exact per-cell form
-// (pred_cell_exact: the full glibc powf, its tables in LDS, and IEEE
-// divisions) and overwrites the cell's three outputs.  Arithmetic per cell is
-// k_predictor's, operation for operation: the outputs are bit-identical.
+// proven correctly rounded by the residual).  An operation whose check fails
+// (~1.25 % of cells on O(1) data) is re-done exactly in the march by the lane
+// that needs it: the squares of a lane's cells, then their roots, each go
+// through a wave-uniform loop that runs one glibc powf (tables in LDS) per
+// pass for every lane with a job left, and a failed division takes the IEEE
+// divide.  Each output is written once.  (r04's first form queued such cells
+// in LDS and re-did them whole from a drain that reloaded their stencils and
+// overwrote the march's stores: the reloads missed L2 and made the kernel read
+// 1.9x its bytes; CFD_PRED_INLINE=0 keeps it for the record.)  Arithmetic per
+// cell is k_predictor's, operation for operation: the outputs are bit-identical.
 struct PredRowArgs {
     const float *u, *v, *nu;  // nu: the nu_eff array, or null (nu_s)
     float *us, *vs, *tau;     // tau: null = not written
@@ -280,20 +282,30 @@ __device__ inline float shl_old(float old, float src) {
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x130, 0xf, 0xf, false));
 }
 // a / b, correctly rounded, from rb ~ 1/b (v_rcp_f32) and one Newton step:
-// q1 = q0 + (a - q0 b) rb.  With the exact residual r = a - q1 b (one fma:
-// exact for q1 within an ulp of a/b, no underflow), a/b = q1 + r/b, so
-// |r| < (1/2 - 2^-10) |b| ulp(q1) proves q1 = RN(a/b) (the ulp taken below
-// q1's last bit, as in powf_sq_fast: the lower binade's for a power of two;
-// the 2^-10 margin covers the rounding of the threshold).  False otherwise
-// (near a midpoint, q1 tiny, inf, NaN): the caller takes the exact path.
-constexpr float kDivT = (float)((0.5 - 0x1p-10) * 0x1p-23);
+// q1 = q0 + (a - q0 b) rb.  With the exact residual r = a - q1 b (one fma),
+// a/b = q1 + r/b, so |r| < |b| ulp(q1) / 2 proves q1 = RN(a/b) (the ulp taken
+// below q1's last bit, as in powf_sq_fast: the lower binade's for a power of
+// two).  The test is |r| < RN(ub * kDivT) with ub = |b| 2^e exact (2^e: q1's
+// power of two below its last bit, so ulp = 2^(e - 23)):
+// kDivT = RN((1/2 - 2^-20) 2^-23) and the product's rounding add at most
+// (1 + 2^-24)^2 < 1 + 2^-21 to (1/2 - 2^-20), so the bound stays below
+// |b| ulp / 2.  The guards keep every quantity normal: |b|, |q1| >= 2^-100 and
+// ub (~ |a|) in [2^-100, 2^100] (the bound then >= 2^-124; the residual's
+// granularity ulp(q1) ulp(b) ~ ub 2^-46 is representable: r is exact whenever
+// q1 is within an ulp of a/b, and a q1 farther off leaves |r| above the bound).
+// False otherwise (near a midpoint, tiny or huge operands, inf, NaN): the
+// caller takes the IEEE division.  (r04 used a 2^-10 margin: 0.2 % of calls
+// left the fast path on the margin alone; now ~3e-6.)
+constexpr float kDivT = (float)((0.5 - 0x1p-20) * 0x1p-23);
 __device__ inline bool div_fast(float a, float b, float rb, float &q) {
     const float q0 = a * rb;
     const float q1 = __builtin_fmaf(__builtin_fmaf(-q0, b, a), rb, q0);
     const float r = __builtin_fmaf(-q1, b, a);
-    const float ul = __uint_as_float(((__float_as_uint(q1) & 0x7fffffffu) - 1u) & 0x7f800000u) * kDivT;
+    const float ab = __builtin_fabsf(b);
+    const float ub = ab * __uint_as_float(((__float_as_uint(q1) & 0x7fffffffu) - 1u) & 0x7f800000u);
     q = q1;
-    return __builtin_fabsf(q1) >= 0x1p-100f && __builtin_fabsf(r) < __builtin_fabsf(b) * ul;
+    return ab >= 0x1p-100f && __builtin_fabsf(q1) >= 0x1p-100f && ub >= 0x1p-100f && ub <= 0x1p100f &&
+           __builtin_fabsf(r) < ub * kDivT;
 }
 
 // supg_tau_vm on the fast division: tau, and whether it is proven exact
@@ -355,6 +367,9 @@ __device__ unsigned long long g_pred_count;
 #ifndef CFD_PRED_WPE
 #define CFD_PRED_WPE 1
 #endif
+#ifndef CFD_PRED_INLINE
+#define CFD_PRED_INLINE 1  // 0: the r04 LDS patch queue + drain instead of in-march fallbacks
+#endif
 template <bool SUPG, bool NUA, int VEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WPE, 8))) void k_predictor_rows(PredRowArgs a) {
     constexpr int SW = 64 * VEC;  // segment width (columns)
@@ -401,6 +416,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
     const float dt = a.dt;
     const float rnu_s = __builtin_amdgcn_rcpf(a.nu_s + a.k.eps);
 
+    // (CFD_PRED_INLINE=0 only; with the default in-march fallbacks nothing is
+    // queued and the compiler drops the queue.)
     // The wave's patch queue: a ring in LDS of the linear indices of the
     // interior cells whose tau the fast paths left unproven (~1.6 % of
     // cells).  The march stores every cell; once the queue holds a wave's
@@ -466,12 +483,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
                 vE[c] = c < VEC - 1 ? vc[c + 1] : shl_old(HVc, vc[0]);
                 vW[c] = c > 0 ? vc[c - 1] : shr_old(HVc, vc[VEC - 1]);
             }
+#if CFD_PRED_INLINE
+            // tau of the lane's cells with the exact fallbacks in the march
+            // itself: each failing powf is re-done by the lane that needs it,
+            // one job per pass of a wave-uniform loop (one powf body per
+            // exponent in the code; a pass runs when any lane has a job left)
+            float tq[VEC];
+            if (SUPG) {
+                float sq[2 * VEC];
+                uint32_t f = 0;
+#pragma unroll
+                for (int c = 0; c < VEC; ++c) {
+                    f |= (libm::powf_sq_fast(uc[c], sq[2 * c]) ? 0u : 1u) << (2 * c);
+                    f |= (libm::powf_sq_fast(vc[c], sq[2 * c + 1]) ? 0u : 1u) << (2 * c + 1);
+                }
+#if CFD_PRED_ABL & 128  // measurement aid: checks formed, fallbacks skipped
+                asm volatile("" ::"v"(f));
+                f = 0;
+#endif
+                while (__builtin_amdgcn_ballot_w64(f != 0)) {
+                    if (f) {
+                        const int j = __builtin_ctz(f);
+                        float x = uc[0];
+#pragma unroll
+                        for (int k = 1; k < 2 * VEC; ++k) x = j == k ? ((k & 1) ? vc[k >> 1] : uc[k >> 1]) : x;
+                        const float r = libm::powf(x, 2.0f, ptab);
+#pragma unroll
+                        for (int k = 0; k < 2 * VEC; ++k) sq[k] = j == k ? r : sq[k];
+                        f &= f - 1;
+                    }
+                }
+                float vmq[VEC], ss[VEC];
+                uint32_t g = 0;
+#pragma unroll
+                for (int c = 0; c < VEC; ++c) {
+                    ss[c] = sq[2 * c] + sq[2 * c + 1];
+                    g |= (libm::powf_sqrt_fast(ss[c], vmq[c]) ? 0u : 1u) << c;
+                }
+#if CFD_PRED_ABL & 128
+                asm volatile("" ::"v"(g));
+                g = 0;
+#endif
+                while (__builtin_amdgcn_ballot_w64(g != 0)) {
+                    if (g) {
+                        const int j = __builtin_ctz(g);
+                        float x = ss[0];
+#pragma unroll
+                        for (int k = 1; k < VEC; ++k) x = j == k ? ss[k] : x;
+                        const float r = libm::powf(x, 0.5f, ptab);
+#pragma unroll
+                        for (int k = 0; k < VEC; ++k) vmq[k] = j == k ? r : vmq[k];
+                        g &= g - 1;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < VEC; ++c) {
+                    const float nu = NUA ? NUc.x[c] : a.nu_s;
+                    bool od;
+                    tq[c] = supg_tau_fast(vmq[c], nu, NUA ? __builtin_amdgcn_rcpf(nu + a.k.eps) : rnu_s, dt, a.k, od);
+#if CFD_PRED_ABL & 128
+                    asm volatile("" ::"v"(od));
+                    od = true;
+#endif
+                    if (__builtin_amdgcn_ballot_w64(!od)) {
+                        if (!od) tq[c] = supg_tau_vm(vmq[c], nu, dt, a.k);
+                    }
+                }
+            }
+#endif
 #pragma unroll
             for (int c = 0; c < VEC; ++c) {
                 const float nu = NUA ? NUc.x[c] : a.nu_s;
                 float cu, cv, t = 0.0f;
                 bool ok = true;
                 if (SUPG) {
+#if CFD_PRED_INLINE
+                    t = tq[c];
+#else
                     // |V| (v5.py:155) and tau (v5.py:156-161) on the fast paths
                     float p, q, vm;
 #if CFD_PRED_ABL & 1  // ablation (timing aid only): no checks on the squares / root
@@ -495,6 +583,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
 #if CFD_PRED_ABL & 4  // ablation: no patch queue
                     ok = true;
 #endif
+#endif  // CFD_PRED_INLINE
                     cu = conv_supg_sel(uc[c], vc[c], uc[c], uE[c], uW[c], Up.x[c], Um.x[c], t, a.k);
                     cv = conv_supg_sel(uc[c], vc[c], vc[c], vE[c], vW[c], Vp.x[c], Vm.x[c], t, a.k);
                 } else {
@@ -1674,8 +1763,9 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
         // rows per chunk: every workgroup resident at once (one round at the
         // kernel's occupancy), chunks of at least 8 rows (2 halo rows each)
         // (r04 sweep, 8192^2 SUPG: 16-row chunks -- several rounds -- beat one
-        // resident round of 64-row chunks by 8-15 %: the patch queue drains
-        // at chunk ends, and short chunks spread those drains over the run)
+        // resident round of 64-row chunks by 8-15 % with the patch queue, whose
+        // drains short chunks spread over the run; with the in-march fallbacks
+        // 16 rows still beat 32 / 64 by 2-7 %)
         a.rows = tuning().pred_rows;
         if (a.rows <= 0) {
             const int resident = pred_rows_resident(f);

@@ -222,8 +222,9 @@ CFD_HDF bool powf_sq_fast(float x, float &p) {
     p = x * x;
     const float e = CFD_FMAF(x, x, -p);
     const float t = asf32u((asu32f(p) - 1u) & 0x7f800000u) * kPowfSqT;
-    // p >= 2^-100 keeps e exact (no underflow); inf / NaN fail the compare
-    return p >= 0x1p-100f && CFD_FABSF(e) < t;
+    // p >= 2^-100 keeps e exact (no underflow); inf / NaN fail the compare.
+    // x = +-0: glibc returns x * x = +0 (its zero branch), as p is
+    return (p >= 0x1p-100f && CFD_FABSF(e) < t) || x == 0.0f;
 }
 // r = sqrt(s) rounded; true when r is glibc's powf(s, 0.5) (the window in
 // the ulp below r's last bit, as above)
@@ -231,8 +232,10 @@ CFD_HDF bool powf_sqrt_fast(float s, float &r) {
     r = CFD_SQRTF(s);
     const float e = CFD_FMAF(-r, r, s);
     const float t = r * (asf32u((asu32f(r) - 1u) & 0x7f800000u) * kPowfSqrtT);
-    // s >= 2^-100 keeps e exact; s < 0, inf or NaN fail the compare
-    return s >= 0x1p-100f && CFD_FABSF(e) < t;
+    // s >= 2^-100 keeps e exact; s < 0, inf or NaN fail the compare.
+    // s = +0: glibc returns +0 (its zero branch: x * x), as r is (not s = -0:
+    // sqrtf(-0) = -0)
+    return (s >= 0x1p-100f && CFD_FABSF(e) < t) || asu32f(s) == 0u;
 }
 
 // NumPy float32 scalar x**2, bit for bit (glibc powf(x, 2.0f))
