@@ -304,8 +304,9 @@ __device__ inline bool div_fast(float a, float b, float rb, float &q) {
     const float ab = __builtin_fabsf(b);
     const float ub = ab * __uint_as_float(((__float_as_uint(q1) & 0x7fffffffu) - 1u) & 0x7f800000u);
     q = q1;
-    return ab >= 0x1p-100f && __builtin_fabsf(q1) >= 0x1p-100f && ub >= 0x1p-100f && ub <= 0x1p100f &&
-           __builtin_fabsf(r) < ub * kDivT;
+    // (bitwise, not short-circuit: the compiler keeps the test branch-free)
+    return (ab >= 0x1p-100f) & (__builtin_fabsf(q1) >= 0x1p-100f) & (ub >= 0x1p-100f) & (ub <= 0x1p100f) &
+           (__builtin_fabsf(r) < ub * kDivT);
 }
 
 // supg_tau_vm on the fast division: tau, and whether it is proven exact
@@ -320,7 +321,7 @@ __device__ inline float supg_tau_fast(float vm, float nu, float rnu, float dt, c
     float t = q * lim;
     asm volatile("" : "+v"(t));  // formed unconditionally (no branch on vm > eps)
     const bool big = vm > k.eps;
-    ok = !big || (o1 && o2);
+    ok = !big | (o1 & o2);
     return big ? t : dt / 2.0f;
 }
 

@@ -208,6 +208,9 @@ CFD_HDF float powf(float x, float y, const PowfTables &T = kPowfTables) {
 // powf.  A call leaves the fast path with probability ~2w =
 // 0.36 % on O(1) inputs.  powf_window.cpp checks powf_sq / powf_sqrt against
 // libm's powf for all 2^32 float inputs, bit for bit.
+#ifndef CFD_POWF_VSQRT
+#define CFD_POWF_VSQRT 1  // device root candidate from v_sqrt_f32 (0: IEEE sqrtf)
+#endif
 constexpr uint32_t kPowfSqWin = CFD_POWF_SQ_WIN;
 constexpr uint32_t kPowfSqrtWin = CFD_POWF_SQRT_WIN;
 // (1/2 - w) 2^-23 and (1 - 2w) 2^-23 with w = window / 2^29
@@ -224,18 +227,32 @@ CFD_HDF bool powf_sq_fast(float x, float &p) {
     const float t = asf32u((asu32f(p) - 1u) & 0x7f800000u) * kPowfSqT;
     // p >= 2^-100 keeps e exact (no underflow); inf / NaN fail the compare.
     // x = +-0: glibc returns x * x = +0 (its zero branch), as p is
-    return (p >= 0x1p-100f && CFD_FABSF(e) < t) || x == 0.0f;
+    // (bitwise, not short-circuit: the compiler keeps the test branch-free)
+    return ((p >= 0x1p-100f) & (CFD_FABSF(e) < t)) | (x == 0.0f);
 }
 // r = sqrt(s) rounded; true when r is glibc's powf(s, 0.5) (the window in
 // the ulp below r's last bit, as above)
 CFD_HDF bool powf_sqrt_fast(float s, float &r) {
+#if CFD_POWF_VSQRT && defined(__HIP_DEVICE_COMPILE__)
+    // the raw v_sqrt_f32 (within an ulp; not the IEEE root on ~15 % of
+    // inputs) moved to the nearest float by its residual: ~12 instructions
+    // against the IEEE sqrtf expansion's ~17; the proof test below decides,
+    // whatever this candidate is (r04: 0.397 against 0.41 ms per 8192^2
+    // predictor launch)
+    const float r0 = __builtin_amdgcn_sqrtf(s);
+    const float e0 = CFD_FMAF(-r0, r0, s);
+    const float h = r0 * (asf32u((asu32f(r0) - 1u) & 0x7f800000u) * 0x1p-23f);  // r0 ulp(r0)
+    const uint32_t b0 = asu32f(r0);
+    r = asf32u(e0 > h ? b0 + 1u : (e0 < -h ? b0 - 1u : b0));
+#else
     r = CFD_SQRTF(s);
+#endif
     const float e = CFD_FMAF(-r, r, s);
     const float t = r * (asf32u((asu32f(r) - 1u) & 0x7f800000u) * kPowfSqrtT);
     // s >= 2^-100 keeps e exact; s < 0, inf or NaN fail the compare.
     // s = +0: glibc returns +0 (its zero branch: x * x), as r is (not s = -0:
     // sqrtf(-0) = -0)
-    return (s >= 0x1p-100f && CFD_FABSF(e) < t) || asu32f(s) == 0u;
+    return ((s >= 0x1p-100f) & (CFD_FABSF(e) < t)) | (asu32f(s) == 0u);
 }
 
 // NumPy float32 scalar x**2, bit for bit (glibc powf(x, 2.0f))
