@@ -304,9 +304,12 @@ __device__ inline bool div_fast(float a, float b, float rb, float &q) {
     const float ab = __builtin_fabsf(b);
     const float ub = ab * __uint_as_float(((__float_as_uint(q1) & 0x7fffffffu) - 1u) & 0x7f800000u);
     q = q1;
-    // (bitwise, not short-circuit: the compiler keeps the test branch-free)
-    return (ab >= 0x1p-100f) & (__builtin_fabsf(q1) >= 0x1p-100f) & (ub >= 0x1p-100f) & (ub <= 0x1p100f) &
-           (__builtin_fabsf(r) < ub * kDivT);
+    // the guards select the bound (-1: refuse) and one compare decides: the
+    // guard masks stay scalar masks feeding a single select (combining the
+    // five compares as bools let the vectoriser pack them through VGPRs)
+    const bool g = (ab >= 0x1p-100f) & (__builtin_fabsf(q1) >= 0x1p-100f) & (ub >= 0x1p-100f) & (ub <= 0x1p100f);
+    const float thr = g ? ub * kDivT : -1.0f;
+    return __builtin_fabsf(r) < thr;
 }
 
 // supg_tau_vm on the fast division: tau, and whether it is proven exact
@@ -406,13 +409,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WP
     const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(a.tau ? a.tau : a.us, 0, a.tau ? bytes : 0, 0x00020000);
     // byte offset of this lane's cells in row i (kOob outside the grid: reads 0, stores dropped)
     auto rofs = [&](int i) -> uint32_t {
-        return (i >= 0 && i < ny && lane_in) ? (uint32_t)(((size_t)i * nx + x0) * sizeof(float)) : kOob;
+        return ((i >= 0) & (i < ny) & lane_in) ? (uint32_t)(((size_t)i * nx + x0) * sizeof(float)) : kOob;
     };
     // the segment's x-halo cells of row i: lane 0 column xs - 1, lane 63 column xs + SW
     const int hx = lane == 0 ? xs - 1 : (lane == kWave - 1 ? xs + SW : -1);
     const bool h_in = hx >= 0 && hx < nx;
     auto hofs = [&](int i) -> uint32_t {
-        return (i >= 0 && i < ny && h_in) ? (uint32_t)(((size_t)i * nx + hx) * sizeof(float)) : kOob;
+        return ((i >= 0) & (i < ny) & h_in) ? (uint32_t)(((size_t)i * nx + hx) * sizeof(float)) : kOob;
     };
     const float dt = a.dt;
     const float rnu_s = __builtin_amdgcn_rcpf(a.nu_s + a.k.eps);
