@@ -252,6 +252,26 @@ struct P4 {
 };
 __device__ inline v2f_t pick2(const P4 &f, int h) { return h ? f.o : f.e; }
 __device__ inline P4 split4(float4 f) { return P4{v2f_t{f.x, f.z}, v2f_t{f.y, f.w}}; }
+
+// Jacobi register-queue entry as two 64-bit values (CFD_TBR_Q64): a float4
+// held this way is copied by two v_mov_b64 when its queue shifts, where the
+// float4's four 32-bit components were copied one v_mov_b32 at a time
+#ifndef CFD_TBR_Q64
+#define CFD_TBR_Q64 1
+#endif
+struct Q4 {
+    unsigned long long lo, hi;
+};
+__device__ inline Q4 q4_of(float4 f) {
+    return Q4{__builtin_bit_cast(unsigned long long, v2f_t{f.x, f.y}),
+              __builtin_bit_cast(unsigned long long, v2f_t{f.z, f.w})};
+}
+__device__ inline float4 f4_of(const Q4 &q) {
+    const v2f_t a = __builtin_bit_cast(v2f_t, q.lo), b = __builtin_bit_cast(v2f_t, q.hi);
+    return make_float4(a.x, a.y, b.x, b.y);
+}
+[[maybe_unused]] __device__ inline float4 f4_of(float4 f) { return f; }
+__device__ inline const P4 &f4_of(const P4 &p) { return p; }
 // from LDS: two ds_read2_b32 (words 0, 2 and 1, 3) straight into the pairs
 __device__ inline P4 ldsp(const float *p) { return P4{v2f_t{p[0], p[2]}, v2f_t{p[1], p[3]}}; }
 // GS tiles (SPLIT): the 256 cells of a tile row are stored by colour pair,
@@ -652,21 +672,26 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             // cells keep the previous level's values, which the level below
             // holds): half the registers of the level queues
             using QT = std::conditional_t<MODE == kRbgs, v2f_t, float4>;
+            // Jacobi queue entries: Q4 (64-bit halves) or float4
+            using JQ = std::conditional_t<CFD_TBR_Q64 != 0, Q4, float4>;
             // GS: V and Rq hold colour pairs (P4)
-            using VT = std::conditional_t<MODE == kRbgs, P4, float4>;
+            using VT = std::conditional_t<MODE == kRbgs, P4, JQ>;
+            using QQ = std::conditional_t<MODE == kRbgs, v2f_t, JQ>;
             auto toV = [](float4 f) -> VT {
                 if constexpr (MODE == kRbgs)
                     return split4(f);
+                else if constexpr (CFD_TBR_Q64 != 0)
+                    return q4_of(f);
                 else
                     return f;
             };
             VT V[RPW][3], Rq[RPW][K];
-            QT Q[RPW][K][3];
+            QQ Q[RPW][K][3];
             float4 Rn[RPW];  // !RDMA: the rhs row of the next step's plane, in flight
 #pragma unroll
             for (int j = 0; j < RPW; ++j) {
 #pragma unroll
-                for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = QT{};
+                for (int l = 0; l < K; ++l) Q[j][l][0] = Q[j][l][1] = Q[j][l][2] = QQ{};
                 // planes zs - 1 and zs in slots 2 and 0 (slot (q - zs) mod 3), or 0
                 // and 1 (shifted queues)
                 V[j][ROT ? 2 : 0] = toV(ZERO ? z4 : ldb4(plane_rsrc(a.in, zs - 1, nz, plane), bo[j]));
@@ -749,9 +774,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 for (int j = 0; j < RPW; ++j) {
                     if (xin) {
                         if constexpr (SPLIT)
-                            sts4s(T(0, rr[j]), lane, V[j][vs(0)]);
+                            sts4s(T(0, rr[j]), lane, f4_of(V[j][vs(0)]));
                         else
-                            sts4(T(0, rr[j]) + 4 + 4 * lane, V[j][vs(0)]);
+                            sts4(T(0, rr[j]) + 4 + 4 * lane, f4_of(V[j][vs(0)]));
                     }
 #pragma unroll
                     for (int l = 1; l < K; ++l)
@@ -775,7 +800,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                         sts4(T(l, rr[j]) + 4 + 4 * lane, f);
                                 }
                             } else {
-                                sts4(T(l, rr[j]) + 4 + 4 * lane, Q[j][l][ROT ? sl3(R - l) : 2]);
+                                sts4(T(l, rr[j]) + 4 + 4 * lane, f4_of(Q[j][l][ROT ? sl3(R - l) : 2]));
                             }
                         }
                 }
@@ -798,7 +823,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     if constexpr (MODE == kRbgs)
                         V[j][vs(1)] = ldsp(pr + (rr[j] - 1) * 256 + 4 * lane);
                     else
-                        V[j][vs(1)] = ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane);
+                        V[j][vs(1)] = toV(ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane));
                     constexpr int RS0 = ROTR ? slk(R, K) : 0;  // slot of this step's rhs
                     if constexpr (!ROTR) {
 #pragma unroll
@@ -822,7 +847,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                         const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
                             a.rhs_out + (size_t)(own ? z : 0) * plane, (short)0,
                             own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
-                        const gv4f rv = {Rq[j][RS0].x, Rq[j][RS0].y, Rq[j][RS0].z, Rq[j][RS0].w};
+                        const float4 rq = f4_of(Rq[j][RS0]);
+                        const gv4f rv = {rq.x, rq.y, rq.z, rq.w};
                         __builtin_amdgcn_raw_buffer_store_b128(rv, ro, (int)so[j], 0, kStoreNt);
                     }
                 }
@@ -929,9 +955,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                           }
                         } else if (r >= l && r < NR - l) {
                             // level l-1 at planes p (c), p + 1 (U), p - 1 (D)
-                            const float4 c = l == 1 ? V[j][vs(0)] : Q[j][l - 1][qs(l - 1, 1)];
-                            const float4 U = l == 1 ? V[j][vs(1)] : Q[j][l - 1][qs(l - 1, 2)];
-                            const float4 D = l == 1 ? V[j][vs(-1)] : Q[j][l - 1][qs(l - 1, 0)];
+                            const float4 c = f4_of(l == 1 ? V[j][vs(0)] : Q[j][l - 1][qs(l - 1, 1)]);
+                            const float4 U = f4_of(l == 1 ? V[j][vs(1)] : Q[j][l - 1][qs(l - 1, 2)]);
+                            const float4 D = f4_of(l == 1 ? V[j][vs(-1)] : Q[j][l - 1][qs(l - 1, 0)]);
                             const LdsIn in = fetch(l, j);
                             float wl = dpp_from_lower(c.w);
                             float er = dpp_from_upper(c.x);
@@ -940,17 +966,17 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             float lm = 0.f;
                             // every lane (see the GS branch)
                             const float4 v = level4<MODE, PREL, K == 4>(c, wl, er, in.N, in.S, U, D,
-                                                                Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], x, nx,
+                                                                f4_of(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1]), x, nx,
                                                                 irow[j] && !fx, a, (BPv ^ E ^ (j * NWR)) & 1,
                                                                 orow[j] && p >= z0 && p < z1, lm);
                             fold(l, lm);
                             if (l < K) {
                                 if constexpr (ROT) {
-                                    Q[j][l][sl3(R - l + 1)] = v;  // over plane p - 3, dead
+                                    Q[j][l][sl3(R - l + 1)] = toV(v);  // over plane p - 3, dead
                                 } else {
                                     Q[j][l][0] = Q[j][l][1];
                                     Q[j][l][1] = Q[j][l][2];
-                                    Q[j][l][2] = v;
+                                    Q[j][l][2] = toV(v);
                                 }
                             } else {
                                 // unconditional buffer store: rows, lanes and planes this
