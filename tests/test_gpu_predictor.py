@@ -137,8 +137,8 @@ def test_predictor_slow_path_and_special_values(density, vec):
     """u, v drawn from values whose squares sit near a rounding midpoint (the
     full glibc powf must run), values whose u^2 + v^2 root does, and zeros,
     subnormals, huge values, inf and NaN scattered over the grid.  density
-    1: nearly every cell leaves the fast paths (the row march's patch queue
-    overflows and the chunk is redone per cell); 0.03: the queue path."""
+    1: nearly every cell leaves the fast paths (every pass of the march's
+    fallback loops has jobs in most lanes); 0.03: sparse fallbacks."""
     ny, nx = 64, 512
     c, nu = _cfg(ny, nx)
     rng = np.random.default_rng(5)
@@ -166,3 +166,25 @@ def test_predictor_slow_path_and_special_values(density, vec):
             for rows in (0, 2):
                 call("cfd_set_predictor2d_config", 2, rows, vec)
                 _check(u, v, nu, c, np.float32(2e-5), supg, False)
+
+
+@pytest.mark.parametrize("vec", [1, 2, 4])
+def test_predictor_quiescent_fields_bitexact(vec):
+    """Fields at rest or in uniform flow (v5's initial state: u = inflow, v = 0;
+    a cavity at rest: u = v = 0) and a quiescent patch inside a moving one:
+    the zero inputs go through the fast paths (glibc powf returns +0 for a
+    zero base) and must give the oracle's bits, tau = dt / 2 where |V| <= eps."""
+    ny, nx = 96, 520
+    c, nu = _cfg(ny, nx)
+    rng = np.random.default_rng(17)
+    dt = np.float32(2e-5)
+    zero = np.zeros((ny, nx), np.float32)
+    inflow = np.full((ny, nx), np.float32(c.V_inf), np.float32)
+    moving = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+    patch = moving.copy()
+    patch[20:60, 100:300] = 0.0
+    patch[30:40, 150:160] = -0.0
+    call("cfd_set_predictor2d_config", 2, 0, vec)
+    for u, v in ((zero, zero), (inflow, zero), (patch, zero), (patch, patch[::-1].copy()), (zero, moving)):
+        for supg in (True, False):
+            _check(u, v, nu, c, dt, supg, False)
