@@ -11,6 +11,11 @@ send/recv); strong scaling (the grid is fixed, each rank owns 1024/N planes).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment) starts
+the N ranks itself: a child `torch.distributed.run --nproc-per-node N` of the
+same arguments, launched before anything touches the GPU; its exit code is
+forwarded (spawn_ranks).
+
 Rank 0 prints ONE JSON line.  `value` = all ranks' interior cell-updates / the
 max-over-ranks wall time of the K timed steps.  `roofline` prices one launch
 of the dominant kernel -- a temporally blocked pass that fuses several sweeps
@@ -338,9 +343,50 @@ def predictor_bench():
     print(json.dumps(out), flush=True)
 
 
+SINGLE_GPU_WORKLOADS = ("cavity2d_128", "jacobi2d_8192_f64", "predictor2d_8192", "predictor2d_8192_f64")
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def rank_launch_cmd(argv, n, port):
+    """The child command that starts N ranks of this script on one node (one
+    process per GPU, rendezvous on 127.0.0.1): the same bench.py arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py")] + list(argv)
+
+
+def spawn_ranks(args, argv, run=None, device_count=None):
+    """`bench.py --gpus N` (N > 1) started as a plain process: start the N
+    ranks ourselves as a child `torch.distributed.run` and return its exit
+    code.  Nothing here touches the GPU (counting devices does not initialise
+    HIP on this image); the child is a fresh process, never an exec."""
+    import subprocess
+    n = args.gpus
+    if args.workload in SINGLE_GPU_WORKLOADS:
+        raise SystemExit(f"--workload {args.workload} is single-GPU; --gpus {n} applies to the 3-D slab workloads")
+    if device_count is None:
+        import torch
+        device_count = torch.cuda.device_count()
+    if device_count < n:
+        raise SystemExit(f"--gpus {n}: only {device_count} GPU(s) visible on this node")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = rank_launch_cmd(argv, n, _free_port())
+    print(f"bench.py: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return (run or subprocess.run)(cmd, env=env).returncode
+
+
 def main():
     global ARGS
     ARGS = parse()
+    if ARGS.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(ARGS, sys.argv[1:]))
     if ARGS.workload == "cavity2d_128":
         return cavity_bench()
     if ARGS.workload.startswith("predictor2d"):
@@ -357,8 +403,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != ARGS.gpus:
-        if world == 1 and ARGS.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+        print(f"WARNING: --gpus {ARGS.gpus} but WORLD_SIZE={world}: running {world} rank(s)", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_slab = world > 1 or ARGS.force_slab
