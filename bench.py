@@ -101,6 +101,9 @@ def parse():
                     help="use the RCCL slab path even on one rank (launch under torch.distributed.run)")
     ap.add_argument("--cpu-sample-planes", type=int, default=256)
     ap.add_argument("--sweep-tiles", action="store_true", help="print a tile-size sweep (N=1, 3-D)")
+    ap.add_argument("--tau-mode", default="exact", choices=["exact", "fast"],
+                    help="predictor workloads: SUPG tau arithmetic (exact: bit-exact glibc powf/pow; "
+                         "fast: the compiled reference's fastmath form)")
     return ap.parse_args()
 
 
@@ -269,12 +272,15 @@ def predictor_bench():
     OptimizedTurbulentConfig's domain: u, v ~ U(-1, 1) (seeded), SUPG, nu_eff =
     nu + art_visc as a scalar (nu_t == 0 with LES off, v5.py:386-388), tau
     written.  value = cells / s; roofline = algorithmic bytes (20 B per f32
-    cell, 40 B per f64) / the launch's HIP-event duration."""
+    cell, 40 B per f64) / the launch's HIP-event duration (the library's
+    predictor timing channel).  --tau-mode exact|fast picks the SUPG tau
+    arithmetic; the CPU-baseline leg also measures the launch's relative
+    L-inf against the oracle (exact arithmetic) on the sampled rows."""
     import torch
     import _pkgpath
     _pkgpath.load()
     from cfd_simulations_amd import kernels as K
-    from cfd_simulations_amd._lib import call
+    from cfd_simulations_amd._lib import call, lib
     from cfd_simulations_amd.solver import OptimizedTurbulentConfig
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("the predictor workload is single-GPU")
@@ -282,8 +288,9 @@ def predictor_bench():
     ny, nx = shape
     f64 = dt_name == "f64"
     tdt = torch.float64 if f64 else torch.float32
-    cfg = OptimizedTurbulentConfig(nx=nx, ny=ny)
-    nu_eff = (np.float64 if f64 else np.float32)(cfg.nu) + (np.float64 if f64 else np.float32)(cfg.artificial_viscosity)
+    npt = np.float64 if f64 else np.float32
+    cfg = OptimizedTurbulentConfig(nx=nx, ny=ny, memory_efficient=not f64)
+    nu_eff = npt(cfg.nu) + npt(cfg.artificial_viscosity)
     dt = np.float32(2e-5)
     g = torch.Generator(device="cuda").manual_seed(3)
     u = torch.rand(shape, generator=g, device="cuda", dtype=tdt) * 2 - 1
@@ -291,7 +298,7 @@ def predictor_bench():
     us, vs, tau = torch.empty_like(u), torch.empty_like(u), torch.empty_like(u)
 
     def step():
-        K.predictor_fused(u, v, cfg.dx, cfg.dy, dt, float(nu_eff), True, us, vs, tau)
+        K.predictor_fused(u, v, cfg.dx, cfg.dy, dt, float(nu_eff), True, us, vs, tau, tau_mode=ARGS.tau_mode)
     for _ in range(max(ARGS.warmup, 1)):
         step()
     torch.cuda.synchronize()
@@ -303,14 +310,19 @@ def predictor_bench():
     elapsed = time.perf_counter() - t0
     ms = ctypes.c_double()
     nl = ctypes.c_longlong()
-    call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(nl), 1)
+    call("cfd_timing_read_channel", 1, ctypes.byref(ms), ctypes.byref(nl), 1)
     call("cfd_timing_enable", 0)
     launch_ms = ms.value / max(nl.value, 1)
     cells = ny * nx
     alg = cells * bpc
     achieved = alg / (launch_ms * 1e-3) / 1e9
-    kern = ("k_predictor64<SUPG> (one thread per cell)" if f64 else
-            "k_predictor_rows<SUPG, scalar nu, 2 cells per lane> (row march, 16-row chunks)")
+    # the kernel that ran, as the library reports it
+    mode_c, vec_c = ctypes.c_int(), ctypes.c_int()
+    path = int(lib().cfd_get_last_predictor2d_path(ctypes.byref(mode_c), ctypes.byref(vec_c)))
+    mode = {0: "exact", 1: "fast"}[mode_c.value]
+    T = "double" if f64 else "float"
+    kern = (f"k_predictor_rows<{T}, tau {mode}, SUPG, scalar nu, {vec_c.value} cells per lane> (row march)"
+            if path == 1 else ("k_predictor64<SUPG>" if f64 else "k_predictor<SUPG>") + " (one thread per cell)")
     out = {
         "metric": "Gcell-updates/s of the fused advection-diffusion predictor; achieved HBM GB/s vs peak",
         "value": round(cells * ARGS.steps / elapsed / 1e9, 3), "unit": "Gcell-updates/s", "n_gpus": 1,
@@ -318,28 +330,42 @@ def predictor_bench():
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": dt_name,
         "data": "synthetic: u, v ~ U(-1, 1) seeded, on OptimizedTurbulentConfig's 20 x 4 domain (no dataset)",
         "config": {"workload": f"predictor2d_supg_{ny}x{nx}_{dt_name}", "grid": [ny, nx], "use_supg": True,
-                   "nu_eff": "scalar (LES off)", "tau_written": True},
+                   "nu_eff": "scalar (LES off)", "tau_written": True, "tau_mode": mode,
+                   "tau_arithmetic": ("glibc powf/pow restated on device (the reference's NumPy scalar **), "
+                                      "bit-exact" if mode == "exact" else
+                                      "fastmath: x*x, correctly rounded sqrt, rcp+Newton divisions")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(ARGS.workload, 1),
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": load_traffic(ARGS.workload + ("" if mode == "exact" else "_fast"), 1),
                      "kernel": kern, "bytes_per_cell": bpc, "cells_per_launch": cells,
                      "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(launch_ms, 5)},
         "cpu_baseline": None,
     }
-    if not ARGS.no_cpu_baseline and not f64:
+    if not ARGS.no_cpu_baseline:
         import oracle
-        rows = 1024
+        rows = 512 if f64 else 1024
         hu, hv = u[:rows].cpu().numpy(), v[:rows].cpu().numpy()
         n = 0
         t0 = time.perf_counter()
         while n < 1 or (time.perf_counter() - t0 < 10.0 and n < 20):
-            oracle.predictor2d(hu, hv, nu_eff, dx=cfg.dx, dy=cfg.dy, dt=dt, use_supg=True)
+            ref = oracle.predictor2d(hu, hv, nu_eff, dx=cfg.dx, dy=cfg.dy, dt=dt, use_supg=True, dtype=npt)
             n += 1
         t = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": rows * nx * n / t / 1e9, "unit": "Gcell-updates/s", "cores": 1,
                                "kind": "port",
                                "sample": f"{rows}x{nx} rows of the grid, {n} calls of oracle.predictor2d (C "
-                                         f"restatement of v5.py:127-176, :388-403 with libm powf, serial); "
-                                         f"{t:.2f} s; host has {os.cpu_count()} logical CPUs, 1 used"}
+                                         f"restatement of v5.py:127-176, :388-403 with libm "
+                                         f"{'pow' if f64 else 'powf'}, {dt_name}, serial); {t:.2f} s; host has "
+                                         f"{os.cpu_count()} logical CPUs, 1 used"}
+        # accuracy of the timed launch on the sampled rows (their interior:
+        # row rows-1 is a boundary row of the sample), vs the exact oracle
+        torch.cuda.synchronize()
+        err = {}
+        for k, t_ in (("u_star", us), ("v_star", vs), ("tau", tau)):
+            a_ = t_[1:rows - 1].cpu().numpy().astype(np.float64)
+            b_ = ref[k][1:rows - 1].astype(np.float64)
+            err[k] = float(np.abs(a_ - b_).max() / max(np.abs(b_).max(), 1e-300))
+        out["config"]["rel_linf_vs_exact_oracle"] = err
     print(json.dumps(out), flush=True)
 
 

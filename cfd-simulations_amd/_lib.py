@@ -48,6 +48,8 @@ PROTOTYPES = {
     "cfd_predictor2d_f32": (c_int, [P, P, P, c_float, P, P, P, c_int, c_int, c_double, c_double,
                                     c_float, c_int, P]),
     "cfd_set_predictor2d_config": (c_int, [c_int, c_int, c_int]),
+    "cfd_set_predictor2d_tau_mode": (c_int, [c_int]),
+    "cfd_get_last_predictor2d_path": (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "cfd_set_persistent_launch": (c_int, [c_int, ctypes.c_longlong]),
     "cfd_persistent_status": (c_int, [P]),
     "cfd_release_thread_resources": (c_int, []),
@@ -135,6 +137,7 @@ PROTOTYPES = {
     "cfd_set_small2d_shape": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "cfd_timing_enable": (c_int, [c_int]),
     "cfd_timing_read": (c_int, [ctypes.POINTER(c_double), ctypes.POINTER(ctypes.c_longlong), c_int]),
+    "cfd_timing_read_channel": (c_int, [c_int, ctypes.POINTER(c_double), ctypes.POINTER(ctypes.c_longlong), c_int]),
 }
 
 

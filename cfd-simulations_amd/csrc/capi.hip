@@ -25,6 +25,7 @@ struct Timing {
     bool on = false, overflow = false;
     std::vector<hipEvent_t> start, stop;
     std::vector<long long> sweeps;
+    std::vector<int> channel;
     size_t used = 0;
     ~Timing() {
         // return codes ignored: at process exit the runtime may already be gone
@@ -78,7 +79,7 @@ Tuning &tuning() {
     return t;
 }
 
-int timing_begin(hipStream_t s) {
+int timing_begin(hipStream_t s, int channel) {
     if (!g_timing.on) return -1;
     if (g_timing.used >= Timing::kMaxPairs) {
         g_timing.overflow = true;
@@ -90,8 +91,10 @@ int timing_begin(hipStream_t s) {
         g_timing.start.push_back(a);
         g_timing.stop.push_back(b);
         g_timing.sweeps.push_back(0);
+        g_timing.channel.push_back(0);
     }
     const int k = (int)g_timing.used++;
+    g_timing.channel[k] = channel;
     if (hipEventRecord(g_timing.start[k], s) != hipSuccess) return -1;
     return k;
 }
@@ -258,12 +261,18 @@ int cfd_timing_enable(int enable) {
 }
 
 int cfd_timing_read(double *ms, long long *sweeps, int reset) {
+    return cfd_timing_read_channel(kTimingSolve, ms, sweeps, reset);
+}
+
+int cfd_timing_read_channel(int channel, double *ms, long long *sweeps, int reset) {
     CFD_REQUIRE(ms && sweeps, "timing_read: null pointer");
+    CFD_REQUIRE(channel == kTimingSolve || channel == kTimingPredictor, "timing_read: channel 0 or 1");
     CFD_REQUIRE(!g_timing.overflow, "timing_read: more than %zu solves were timed without a read",
                 Timing::kMaxPairs);
     double total = 0.0;
     long long n = 0;
     for (size_t k = 0; k < g_timing.used; ++k) {
+        if (g_timing.channel[k] != channel) continue;
         CFD_CHECK_HIP(hipEventSynchronize(g_timing.stop[k]));
         float t = 0.f;
         CFD_CHECK_HIP(hipEventElapsedTime(&t, g_timing.start[k], g_timing.stop[k]));

@@ -22,7 +22,10 @@ constexpr int kNumXcd = 8; // MI355X: 8 XCDs, blocks dealt round-robin
 
 void set_error(const char *fmt, ...);
 // bench timing hooks (capi.hip): event pair around a solve's sweep launches
-int timing_begin(hipStream_t s);
+// (channel: kTimingSolve -- the pressure solves, what cfd_timing_read sums --
+// or kTimingPredictor, read by cfd_timing_read_channel)
+constexpr int kTimingSolve = 0, kTimingPredictor = 1;
+int timing_begin(hipStream_t s, int channel = kTimingSolve);
 void timing_end(int k, hipStream_t s, long long sweeps);
 void timing_cancel(int k);
 

@@ -11,36 +11,18 @@
 //
 // These kernels are one-pass per cell and HBM-bound; the fused predictor
 // reads u, v once (5-point neighbourhoods from L1/L2) and writes u*, v*, tau.
+#include <map>
+#include <mutex>
+
 #include "common.hpp"
 #include "internal.hpp"
 #include "libm_powf.hpp"
+#include "pred_rows.hpp"
 
 namespace cfd {
 
-struct PredConst {
-    float c1x, c1y;  // SUPG first derivative: 0.5 * (0.5/dx)   (v5.py:131,137)
-    float c2x, c2y;  // SUPG second derivative: (0.5/dx)^2       (v5.py:141)
-    float ux, uy;    // upwind: 1/dx                              (v5.py:116)
-    float lx, ly;    // laplacian: 1/(dx*dx)                      (v5.py:168)
-    float h;         // min(dx, dy) as float32                    (v5.py:156)
-    float eps;       // float32(1e-10)
-};
-
-static PredConst make_pred_const(double dx, double dy) {
-    PredConst k;
-    const double sdx = 0.5 / dx, sdy = 0.5 / dy;
-    k.c1x = (float)(0.5 * sdx);
-    k.c1y = (float)(0.5 * sdy);
-    k.c2x = (float)(sdx * sdx);
-    k.c2y = (float)(sdy * sdy);
-    k.ux = (float)(1.0 / dx);
-    k.uy = (float)(1.0 / dy);
-    k.lx = (float)(1.0 / (dx * dx));
-    k.ly = (float)(1.0 / (dy * dy));
-    k.h = (float)(dx < dy ? dx : dy);
-    k.eps = (float)1e-10;
-    return k;
-}
+using PredConst = PredK<float>;
+static PredConst make_pred_const(double dx, double dy) { return make_pred_k<float>(dx, dy); }
 
 // compute_supg_stabilization_fast body, v5.py:155-161: vel_mag =
 // (u**2 + v**2) ** 0.5 on float32 scalars, i.e. libm powf three times
@@ -57,64 +39,6 @@ __device__ inline float supg_tau(float u, float v, float nu, float dt, const Pre
     }
     return dt / 2.0f;
 }
-// the same from |V|^2 = u**2 + v**2 already formed (the row-march predictor
-// forms the squares and roots of a lane's four cells in batches)
-// (branch-free: both sides formed, one selected, so the row march can
-// interleave its four cells' division chains)
-__device__ inline float supg_tau_vm(float vm, float nu, float dt, const PredConst &k) {
-    const float pe = (vm * k.h) / (nu + k.eps);
-    const float half = pe / 2.0f;
-    const float lim = half < 1.0f ? half : 1.0f;
-    float t = (k.h / (2.0f * vm)) * lim;
-    asm volatile("" : "+v"(t));  // keeps the divisions out of a branch on vm > eps
-    return vm > k.eps ? t : dt / 2.0f;
-}
-
-// compute_convection_supg_fast body, v5.py:135-146
-__device__ inline float conv_supg(float uc, float vc, float C, float E, float W, float N, float S,
-                                  float t, const PredConst &k) {
-    const float ddx = (E - W) * k.c1x;
-    const float ddy = (N - S) * k.c1y;
-    const float cs = uc * ddx + vc * ddy;
-    if (t > 0.0f) {
-        const float d2x = ((E - 2.0f * C) + W) * k.c2x;
-        const float d2y = ((N - 2.0f * C) + S) * k.c2y;
-        return cs - t * (uc * d2x + vc * d2y);
-    }
-    return cs;
-}
-
-// conv_supg without the branch on t > 0 (both forms, one selected; the asm
-// keeps the compiler from sinking the second-derivative part into a branch):
-// the row march interleaves its four cells
-__device__ inline float conv_supg_sel(float uc, float vc, float C, float E, float W, float N, float S,
-                                      float t, const PredConst &k) {
-    const float ddx = (E - W) * k.c1x;
-    const float ddy = (N - S) * k.c1y;
-    const float cs = uc * ddx + vc * ddy;
-    const float d2x = ((E - 2.0f * C) + W) * k.c2x;
-    const float d2y = ((N - 2.0f * C) + S) * k.c2y;
-    float cd = cs - t * (uc * d2x + vc * d2y);
-    asm volatile("" : "+v"(cd));
-    return t > 0.0f ? cd : cs;
-}
-
-// compute_convection_fast body (first-order upwind), v5.py:120-124
-__device__ inline float conv_upwind(float uc, float vc, float C, float E, float W, float N,
-                                    float S, const PredConst &k) {
-    const float ddx = uc > 0.0f ? (C - W) * k.ux : (E - C) * k.ux;
-    const float ddy = vc > 0.0f ? (C - S) * k.uy : (N - C) * k.uy;
-    return uc * ddx + vc * ddy;
-}
-
-// compute_laplacian_fast body, v5.py:172-175
-__device__ inline float laplacian(float nu, float C, float E, float W, float N, float S,
-                                  const PredConst &k) {
-    const float l1 = ((E - 2.0f * C) + W) * k.lx;
-    const float l2 = ((N - 2.0f * C) + S) * k.ly;
-    return nu * (l1 + l2);
-}
-
 __device__ inline bool interior(int i, int j, int ny, int nx) {
     return i >= 1 && i < ny - 1 && j >= 1 && j < nx - 1;
 }
@@ -192,466 +116,6 @@ __global__ __launch_bounds__(256) void k_predictor(const float *__restrict__ u,
     us[c] = uc + dt * (-cu + lu);
     vs[c] = vc + dt * (-cv + lv);
     if (SUPG && tau_out) tau_out[c] = t;
-}
-
-// ---- row-march predictor (r04): the fused predictor as a tiled stencil ------
-// One wave owns a segment of 64 * VEC columns (64 lanes x VEC adjacent cells:
-// one float, float2 or float4 per lane) and marches down a chunk of rows.
-// Rows i-1, i, i+1 of u and v sit in registers (row i+2 is in flight: each row
-// is loaded once, one coalesced 64 * VEC * 4 B load per field, two steps
-// ahead), rotated by moves at the end of a step.  y-neighbours are the other
-// rows, x-neighbours the lane's own cells plus DPP wave shifts (wave_shr /
-// wave_shl) for its first and last cell; the two columns just outside the
-// segment arrive as one dword load per row and field (lane 0: column xs - 1,
-// lane 63: column xs + 64 VEC) and enter the shifts as their `old` operand.
-// The four waves of a workgroup take four adjacent segments; workgroups are
-// dealt chunk by chunk, XCD-swizzled, so the two halo rows a chunk shares with
-// its neighbours are read from the same L2.  u*, v* and tau leave as
-// streaming stores.  HBM: u, v read once (+2 halo rows per chunk), u*, v*,
-// tau written once: 20 B per cell (16 without tau).
-//
-// tau runs on proven fast paths: |V| = (u**2 + v**2)**0.5 through powf_sq_fast
-// / powf_sqrt_fast (libm_powf.hpp: float ops and an fma residual each, equal
-// to glibc's powf unless near a rounding midpoint, ~0.36 % / ~0.75 % per
-// call) and its two divisions through div_fast (v_rcp_f32 + one Newton step,
-// proven correctly rounded by the residual).  An operation whose check fails
-// (~1.25 % of cells on O(1) data) is re-done exactly in the march by the lane
-// that needs it: the squares of a lane's cells, then their roots, each go
-// through a wave-uniform loop that runs one glibc powf (tables in LDS) per
-// pass for every lane with a job left, and a failed division takes the IEEE
-// divide.  Each output is written once.  (r04's first form queued such cells
-// in LDS and re-did them whole from a drain that reloaded their stencils and
-// overwrote the march's stores: the reloads missed L2 and made the kernel read
-// 1.9x its bytes; CFD_PRED_INLINE=0 keeps it for the record.)  Arithmetic per
-// cell is k_predictor's, operation for operation: the outputs are bit-identical.
-struct PredRowArgs {
-    const float *u, *v, *nu;  // nu: the nu_eff array, or null (nu_s)
-    float *us, *vs, *tau;     // tau: null = not written
-    float nu_s, dt;
-    int ny, nx, rows, nseg, groups;
-    PredConst k;
-};
-
-// a lane's VEC cells of one row through a buffer resource (kOob: zeros / dropped)
-template <int VEC>
-struct Cells {
-    float x[VEC];
-};
-template <int VEC>
-__device__ inline Cells<VEC> pldv(__amdgpu_buffer_rsrc_t r, uint32_t ofs) {
-    Cells<VEC> c;
-    if constexpr (VEC == 4) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)ofs, 0, 0);
-        for (int k = 0; k < 4; ++k) c.x[k] = __uint_as_float(v[k]);
-    } else if constexpr (VEC == 2) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)ofs, 0, 0);
-        for (int k = 0; k < 2; ++k) c.x[k] = __uint_as_float(v[k]);
-    } else {
-        c.x[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)ofs, 0, 0));
-    }
-    return c;
-}
-template <int VEC>
-__device__ inline void pstv(const Cells<VEC> &c, __amdgpu_buffer_rsrc_t r, uint32_t ofs) {
-#ifndef CFD_PRED_NT
-#define CFD_PRED_NT 2
-#endif
-    constexpr int kNt = CFD_PRED_NT;  // store cache policy (2: streaming)
-    // (the builtins take unsigned words: pass the float bits, not a conversion)
-    typedef unsigned u4 __attribute__((ext_vector_type(4)));
-    typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    if constexpr (VEC == 4) {
-        __builtin_amdgcn_raw_buffer_store_b128(
-            u4{__float_as_uint(c.x[0]), __float_as_uint(c.x[1]), __float_as_uint(c.x[2]), __float_as_uint(c.x[3])}, r,
-            (int)ofs, 0, kNt);
-    } else if constexpr (VEC == 2) {
-        __builtin_amdgcn_raw_buffer_store_b64(u2{__float_as_uint(c.x[0]), __float_as_uint(c.x[1])}, r, (int)ofs, 0,
-                                              kNt);
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(c.x[0]), r, (int)ofs, 0, kNt);
-    }
-}
-__device__ inline float pld1(__amdgpu_buffer_rsrc_t r, uint32_t ofs) {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)ofs, 0, 0));
-}
-// DPP wave shifts whose out-of-wave lane keeps `old` (bound_ctrl off)
-__device__ inline float shr_old(float old, float src) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x138, 0xf, 0xf, false));
-}
-__device__ inline float shl_old(float old, float src) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x130, 0xf, 0xf, false));
-}
-// a / b, correctly rounded, from rb ~ 1/b (v_rcp_f32) and one Newton step:
-// q1 = q0 + (a - q0 b) rb.  With the exact residual r = a - q1 b (one fma),
-// a/b = q1 + r/b, so |r| < |b| ulp(q1) / 2 proves q1 = RN(a/b) (the ulp taken
-// below q1's last bit, as in powf_sq_fast: the lower binade's for a power of
-// two).  The test is |r| < RN(ub * kDivT) with ub = |b| 2^e exact (2^e: q1's
-// power of two below its last bit, so ulp = 2^(e - 23)):
-// kDivT = RN((1/2 - 2^-20) 2^-23) and the product's rounding add at most
-// (1 + 2^-24)^2 < 1 + 2^-21 to (1/2 - 2^-20), so the bound stays below
-// |b| ulp / 2.  The guards keep every quantity normal: |b|, |q1| >= 2^-100 and
-// ub (~ |a|) in [2^-100, 2^100] (the bound then >= 2^-124; the residual's
-// granularity ulp(q1) ulp(b) ~ ub 2^-46 is representable: r is exact whenever
-// q1 is within an ulp of a/b, and a q1 farther off leaves |r| above the bound).
-// False otherwise (near a midpoint, tiny or huge operands, inf, NaN): the
-// caller takes the IEEE division.  (r04 used a 2^-10 margin: 0.2 % of calls
-// left the fast path on the margin alone; now ~3e-6.)
-constexpr float kDivT = (float)((0.5 - 0x1p-20) * 0x1p-23);
-__device__ inline bool div_fast(float a, float b, float rb, float &q) {
-    const float q0 = a * rb;
-    const float q1 = __builtin_fmaf(__builtin_fmaf(-q0, b, a), rb, q0);
-    const float r = __builtin_fmaf(-q1, b, a);
-    const float ab = __builtin_fabsf(b);
-    const float ub = ab * __uint_as_float(((__float_as_uint(q1) & 0x7fffffffu) - 1u) & 0x7f800000u);
-    q = q1;
-    // the guards select the bound (-1: refuse) and one compare decides: the
-    // guard masks stay scalar masks feeding a single select (combining the
-    // five compares as bools let the vectoriser pack them through VGPRs)
-    const bool g = (ab >= 0x1p-100f) & (__builtin_fabsf(q1) >= 0x1p-100f) & (ub >= 0x1p-100f) & (ub <= 0x1p100f);
-    const float thr = g ? ub * kDivT : -1.0f;
-    return __builtin_fabsf(r) < thr;
-}
-
-// supg_tau_vm on the fast division: tau, and whether it is proven exact
-// (rnu = an approximate 1 / (nu + eps))
-__device__ inline float supg_tau_fast(float vm, float nu, float rnu, float dt, const PredConst &k, bool &ok) {
-    float pe, q;
-    const bool o1 = div_fast(vm * k.h, nu + k.eps, rnu, pe);
-    const float half = pe / 2.0f;
-    const float lim = half < 1.0f ? half : 1.0f;
-    const float d = 2.0f * vm;
-    const bool o2 = div_fast(k.h, d, __builtin_amdgcn_rcpf(d), q);
-    float t = q * lim;
-    asm volatile("" : "+v"(t));  // formed unconditionally (no branch on vm > eps)
-    const bool big = vm > k.eps;
-    ok = !big | (o1 & o2);
-    return big ? t : dt / 2.0f;
-}
-
-// one interior cell of the fused SUPG predictor, exactly (k_predictor's
-// body: the full glibc powf wherever the fast paths do not apply, IEEE
-// divisions), its inputs re-read from global memory (L2: the march read them
-// a few rows ago)
-template <bool NUA>
-#ifndef CFD_PRED_ABL
-#define CFD_PRED_ABL 0
-#endif
-__device__ inline void pred_cell_exact(const PredRowArgs &a, uint32_t c, const libm::PowfTables &T) {
-#if CFD_PRED_ABL & 64  // measurement aid: the stencil from a tiny fixed window (L2-resident)
-    // u[c] below reads a.u[(c & 1023) + 2 nx]: rows 1..3, every offset in range
-    const float *__restrict__ u = a.u + (size_t)((c & 1023) + 2 * a.nx) - c;
-    const float *__restrict__ v = a.v + (size_t)((c & 1023) + 2 * a.nx) - c;
-#else
-    const float *__restrict__ u = a.u;
-    const float *__restrict__ v = a.v;
-#endif
-    const int nx = a.nx;
-    const float uc = u[c], vc = v[c];
-    const float nu = NUA ? a.nu[c] : a.nu_s;
-    const float uE = u[c + 1], uW = u[c - 1], uN = u[c + nx], uS = u[c - nx];
-    const float vE = v[c + 1], vW = v[c - 1], vN = v[c + nx], vS = v[c - nx];
-    const float t = supg_tau(uc, vc, nu, a.dt, a.k, T);
-    const float cu = conv_supg(uc, vc, uc, uE, uW, uN, uS, t, a.k);
-    const float cv = conv_supg(uc, vc, vc, vE, vW, vN, vS, t, a.k);
-    const float lu = laplacian(nu, uc, uE, uW, uN, uS, a.k);
-    const float lv = laplacian(nu, vc, vE, vW, vN, vS, a.k);
-#if CFD_PRED_ABL & 32  // measurement aid: results computed, not stored
-    float r0 = uc + a.dt * (-cu + lu), r1 = vc + a.dt * (-cv + lv);
-    asm volatile("" ::"v"(r0), "v"(r1), "v"(t));
-#else
-    a.us[c] = uc + a.dt * (-cu + lu);
-    a.vs[c] = vc + a.dt * (-cv + lv);
-    if (a.tau) a.tau[c] = t;
-#endif
-}
-
-#ifdef CFD_PRED_COUNT
-__device__ unsigned long long g_pred_count;
-#endif
-#ifndef CFD_PRED_WPE
-#define CFD_PRED_WPE 1
-#endif
-#ifndef CFD_PRED_INLINE
-#define CFD_PRED_INLINE 1  // 0: the r04 LDS patch queue + drain instead of in-march fallbacks
-#endif
-template <bool SUPG, bool NUA, int VEC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFD_PRED_WPE, 8))) void k_predictor_rows(PredRowArgs a) {
-    constexpr int SW = 64 * VEC;  // segment width (columns)
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    // the glibc powf tables of the queue drain's slow paths, in LDS: a table
-    // load from global memory would wait (vmcnt) for every row load and store
-    // in flight (copied before any wave of the workgroup can leave)
-    __shared__ libm::PowfTables ptab;
-    if (SUPG) {
-        const unsigned long long *src = reinterpret_cast<const unsigned long long *>(&libm::kPowfTables);
-        unsigned long long *dst = reinterpret_cast<unsigned long long *>(&ptab);
-        for (int k = threadIdx.x; k < (int)(sizeof(libm::PowfTables) / 8); k += blockDim.x) dst[k] = src[k];
-        __syncthreads();
-    }
-    const int b = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
-    const int chunk = b / a.groups;
-    const int seg = (b - chunk * a.groups) * 4 + wv;
-    if (seg >= a.nseg) return;
-    const int ny = a.ny, nx = a.nx;
-    const int r0 = chunk * a.rows;
-    const int r1 = min(r0 + a.rows, ny);
-    const int xs = seg * SW;
-    const int x0 = xs + lane * VEC;
-    const bool lane_in = x0 < nx;  // nx % VEC == 0: a lane's cells are all in or all out
-    const int bytes = (int)((size_t)ny * nx * sizeof(float));
-    const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.u), 0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.v), 0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rn =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(NUA ? a.nu : a.u), 0, NUA ? bytes : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rus = __builtin_amdgcn_make_buffer_rsrc(a.us, 0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rvs = __builtin_amdgcn_make_buffer_rsrc(a.vs, 0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(a.tau ? a.tau : a.us, 0, a.tau ? bytes : 0, 0x00020000);
-    // byte offset of this lane's cells in row i (kOob outside the grid: reads 0, stores dropped)
-    auto rofs = [&](int i) -> uint32_t {
-        return ((i >= 0) & (i < ny) & lane_in) ? (uint32_t)(((size_t)i * nx + x0) * sizeof(float)) : kOob;
-    };
-    // the segment's x-halo cells of row i: lane 0 column xs - 1, lane 63 column xs + SW
-    const int hx = lane == 0 ? xs - 1 : (lane == kWave - 1 ? xs + SW : -1);
-    const bool h_in = hx >= 0 && hx < nx;
-    auto hofs = [&](int i) -> uint32_t {
-        return ((i >= 0) & (i < ny) & h_in) ? (uint32_t)(((size_t)i * nx + hx) * sizeof(float)) : kOob;
-    };
-    const float dt = a.dt;
-    const float rnu_s = __builtin_amdgcn_rcpf(a.nu_s + a.k.eps);
-
-    // (CFD_PRED_INLINE=0 only; with the default in-march fallbacks nothing is
-    // queued and the compiler drops the queue.)
-    // The wave's patch queue: a ring in LDS of the linear indices of the
-    // interior cells whose tau the fast paths left unproven (~1.6 % of
-    // cells).  The march stores every cell; once the queue holds a wave's
-    // worth (64), and at the end of the chunk, each lane recomputes one queued
-    // cell by the exact per-cell form (pred_cell_exact) and overwrites its
-    // three outputs, after the march's own stores of it have completed
-    // (vmcnt(0)).  (Queueing the cells' stencil inputs in LDS instead and
-    // skipping their march stores measured 25 % slower: more live registers
-    // and a drain per 64 cells of the same cost.)
-#ifndef CFD_PRED_DTH
-#define CFD_PRED_DTH 64  // queued cells that trigger a drain (1..64)
-#endif
-    constexpr int kPQ = 512;  // >= 63 + the 64 VEC cells one row appends
-    __shared__ uint32_t pq_idx_all[4][kPQ];
-    uint32_t *const pq_idx = pq_idx_all[wv];
-    int qh = 0, qn = 0;  // head and count, wave-uniform
-#ifdef CFD_PRED_COUNT
-    int qtot = 0;
-#endif
-    auto drain = [&](int n) {
-#if CFD_PRED_ABL & 8  // ablation (timing aid only): no wait before the patch stores
-#else
-        wait_vmcnt<0>();
-#endif
-#if CFD_PRED_ABL & 16  // ablation: queued cells dropped, not recomputed
-#else
-        if (lane < n) pred_cell_exact<NUA>(a, pq_idx[(qh + lane) & (kPQ - 1)], ptab);
-#endif
-        qh = (qh + n) & (kPQ - 1);
-        qn -= n;
-#ifdef CFD_PRED_COUNT
-        qtot += n;
-#endif
-    };
-
-    // rows i-1 (m), i (c), i+1 (p) and i+2 (n, in flight) of u and v; the
-    // segment's x-halo cells and the nu_eff row of rows i, i+1, i+2
-    Cells<VEC> Um = pldv<VEC>(ru, rofs(r0 - 1)), Vm = pldv<VEC>(rv, rofs(r0 - 1));
-    Cells<VEC> Uc = pldv<VEC>(ru, rofs(r0)), Vc = pldv<VEC>(rv, rofs(r0));
-    float HUc = pld1(ru, hofs(r0)), HVc = pld1(rv, hofs(r0));
-    Cells<VEC> Up = pldv<VEC>(ru, rofs(r0 + 1)), Vp = pldv<VEC>(rv, rofs(r0 + 1));
-    float HUp = pld1(ru, hofs(r0 + 1)), HVp = pld1(rv, hofs(r0 + 1));
-    Cells<VEC> NUc = {}, NUp = {};
-    if (NUA) {
-        NUc = pldv<VEC>(rn, rofs(r0));
-        NUp = pldv<VEC>(rn, rofs(r0 + 1));
-    }
-    for (int i = r0; i < r1; ++i) {
-        // two rows ahead: row i+2 (and its halo cells / nu row)
-        const Cells<VEC> Un = pldv<VEC>(ru, rofs(i + 2)), Vn = pldv<VEC>(rv, rofs(i + 2));
-        const float HUn = pld1(ru, hofs(i + 2)), HVn = pld1(rv, hofs(i + 2));
-        Cells<VEC> NUn = {};
-        if (NUA) NUn = pldv<VEC>(rn, rofs(i + 2));
-        Cells<VEC> uo = Uc, vo = Vc, to = {};
-        uint32_t slow = 0;  // this lane's cells whose tau is unproven
-        if (i >= 1 && i <= ny - 2) {  // wave-uniform: boundary rows keep u* = u + dt*(-0 + 0)
-            const float *uc = Uc.x, *vc = Vc.x;
-            float uE[VEC], uW[VEC], vE[VEC], vW[VEC];
-#pragma unroll
-            for (int c = 0; c < VEC; ++c) {
-                uE[c] = c < VEC - 1 ? uc[c + 1] : shl_old(HUc, uc[0]);
-                uW[c] = c > 0 ? uc[c - 1] : shr_old(HUc, uc[VEC - 1]);
-                vE[c] = c < VEC - 1 ? vc[c + 1] : shl_old(HVc, vc[0]);
-                vW[c] = c > 0 ? vc[c - 1] : shr_old(HVc, vc[VEC - 1]);
-            }
-#if CFD_PRED_INLINE
-            // tau of the lane's cells with the exact fallbacks in the march
-            // itself: each failing powf is re-done by the lane that needs it,
-            // one job per pass of a wave-uniform loop (one powf body per
-            // exponent in the code; a pass runs when any lane has a job left)
-            float tq[VEC];
-            if (SUPG) {
-                float sq[2 * VEC];
-                uint32_t f = 0;
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) {
-                    f |= (libm::powf_sq_fast(uc[c], sq[2 * c]) ? 0u : 1u) << (2 * c);
-                    f |= (libm::powf_sq_fast(vc[c], sq[2 * c + 1]) ? 0u : 1u) << (2 * c + 1);
-                }
-#if CFD_PRED_ABL & 128  // measurement aid: checks formed, fallbacks skipped
-                asm volatile("" ::"v"(f));
-                f = 0;
-#endif
-                while (__builtin_amdgcn_ballot_w64(f != 0)) {
-                    if (f) {
-                        const int j = __builtin_ctz(f);
-                        float x = uc[0];
-#pragma unroll
-                        for (int k = 1; k < 2 * VEC; ++k) x = j == k ? ((k & 1) ? vc[k >> 1] : uc[k >> 1]) : x;
-                        const float r = libm::powf(x, 2.0f, ptab);
-#pragma unroll
-                        for (int k = 0; k < 2 * VEC; ++k) sq[k] = j == k ? r : sq[k];
-                        f &= f - 1;
-                    }
-                }
-                float vmq[VEC], ss[VEC];
-                uint32_t g = 0;
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) {
-                    ss[c] = sq[2 * c] + sq[2 * c + 1];
-                    g |= (libm::powf_sqrt_fast(ss[c], vmq[c]) ? 0u : 1u) << c;
-                }
-#if CFD_PRED_ABL & 128
-                asm volatile("" ::"v"(g));
-                g = 0;
-#endif
-                while (__builtin_amdgcn_ballot_w64(g != 0)) {
-                    if (g) {
-                        const int j = __builtin_ctz(g);
-                        float x = ss[0];
-#pragma unroll
-                        for (int k = 1; k < VEC; ++k) x = j == k ? ss[k] : x;
-                        const float r = libm::powf(x, 0.5f, ptab);
-#pragma unroll
-                        for (int k = 0; k < VEC; ++k) vmq[k] = j == k ? r : vmq[k];
-                        g &= g - 1;
-                    }
-                }
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) {
-                    const float nu = NUA ? NUc.x[c] : a.nu_s;
-                    bool od;
-                    tq[c] = supg_tau_fast(vmq[c], nu, NUA ? __builtin_amdgcn_rcpf(nu + a.k.eps) : rnu_s, dt, a.k, od);
-#if CFD_PRED_ABL & 128
-                    asm volatile("" ::"v"(od));
-                    od = true;
-#endif
-                    if (__builtin_amdgcn_ballot_w64(!od)) {
-                        if (!od) tq[c] = supg_tau_vm(vmq[c], nu, dt, a.k);
-                    }
-                }
-            }
-#endif
-#pragma unroll
-            for (int c = 0; c < VEC; ++c) {
-                const float nu = NUA ? NUc.x[c] : a.nu_s;
-                float cu, cv, t = 0.0f;
-                bool ok = true;
-                if (SUPG) {
-#if CFD_PRED_INLINE
-                    t = tq[c];
-#else
-                    // |V| (v5.py:155) and tau (v5.py:156-161) on the fast paths
-                    float p, q, vm;
-#if CFD_PRED_ABL & 1  // ablation (timing aid only): no checks on the squares / root
-                    p = uc[c] * uc[c];
-                    q = vc[c] * vc[c];
-                    vm = __builtin_amdgcn_sqrtf(p + q);
-                    const bool oa = true, ob = true, os = true;
-#else
-                    const bool oa = libm::powf_sq_fast(uc[c], p);
-                    const bool ob = libm::powf_sq_fast(vc[c], q);
-                    const bool os = libm::powf_sqrt_fast(p + q, vm);
-#endif
-                    bool od;
-#if CFD_PRED_ABL & 2  // ablation: no divisions
-                    t = vm > a.k.eps ? vm * a.k.h * rnu_s : dt;
-                    od = true;
-#else
-                    t = supg_tau_fast(vm, nu, NUA ? __builtin_amdgcn_rcpf(nu + a.k.eps) : rnu_s, dt, a.k, od);
-#endif
-                    ok = oa && ob && os && od;
-#if CFD_PRED_ABL & 4  // ablation: no patch queue
-                    ok = true;
-#endif
-#endif  // CFD_PRED_INLINE
-                    cu = conv_supg_sel(uc[c], vc[c], uc[c], uE[c], uW[c], Up.x[c], Um.x[c], t, a.k);
-                    cv = conv_supg_sel(uc[c], vc[c], vc[c], vE[c], vW[c], Vp.x[c], Vm.x[c], t, a.k);
-                } else {
-                    cu = conv_upwind(uc[c], vc[c], uc[c], uE[c], uW[c], Up.x[c], Um.x[c], a.k);
-                    cv = conv_upwind(uc[c], vc[c], vc[c], vE[c], vW[c], Vp.x[c], Vm.x[c], a.k);
-                }
-                const float lu = laplacian(nu, uc[c], uE[c], uW[c], Up.x[c], Um.x[c], a.k);
-                const float lv = laplacian(nu, vc[c], vE[c], vW[c], Vp.x[c], Vm.x[c], a.k);
-                const bool in = x0 + c >= 1 && x0 + c <= nx - 2;
-                // a face cell: conv = lap = tau = 0 (np.zeros_like rings)
-                uo.x[c] = uc[c] + dt * (-(in ? cu : 0.0f) + (in ? lu : 0.0f));
-                vo.x[c] = vc[c] + dt * (-(in ? cv : 0.0f) + (in ? lv : 0.0f));
-                to.x[c] = in ? t : 0.0f;
-                if (SUPG) slow |= (in && lane_in && !ok ? 1u : 0u) << c;
-            }
-            if (SUPG && __builtin_amdgcn_ballot_w64(slow != 0)) {
-                // queue the unproven cells, cell slot by cell slot: positions
-                // by a ballot and mbcnt (no LDS round trips)
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) {
-                    const uint64_t m = __builtin_amdgcn_ballot_w64((slow >> c) & 1u);
-                    if (m) {
-                        if ((slow >> c) & 1u) {
-                            const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            pq_idx[(qh + qn + r) & (kPQ - 1)] = (uint32_t)((size_t)i * nx + x0 + c);
-                        }
-                        qn += __builtin_popcountll(m);
-                    }
-                }
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < VEC; ++c) {
-                uo.x[c] = Uc.x[c] + dt * (-0.0f + 0.0f);
-                vo.x[c] = Vc.x[c] + dt * (-0.0f + 0.0f);
-            }
-        }
-        const uint32_t o = rofs(i);
-        pstv<VEC>(uo, rus, o);
-        pstv<VEC>(vo, rvs, o);
-        if (SUPG && a.tau) pstv<VEC>(to, rt, o);
-        // (after the row's stores; at CFD_PRED_DTH queued cells: their
-        // stencil rows are still in L2 when few rows have passed)
-        while (SUPG && qn >= CFD_PRED_DTH) drain(qn < kWave ? qn : kWave);
-        Um = Uc;
-        Vm = Vc;
-        Uc = Up;
-        Vc = Vp;
-        Up = Un;
-        Vp = Vn;
-        HUc = HUp;
-        HVc = HVp;
-        HUp = HUn;
-        HVp = HVn;
-        if (NUA) {
-            NUc = NUp;
-            NUp = NUn;
-        }
-    }
-    if (SUPG && qn) drain(qn);
-#ifdef CFD_PRED_COUNT  // measurement aid only: cells drained
-    if (SUPG && lane == 0) atomicAdd(&g_pred_count, (unsigned long long)qtot);
-#endif
 }
 
 // compute_divergence_fast, v5.py:178-187 (+ max|div| diagnostic, v5.py:410)
@@ -1656,22 +1120,25 @@ __global__ void k_numpy_powf(const float *__restrict__ x, float y, float *__rest
 
 static dim3 grid2d(int ny, int nx) { return dim3(ceil_div(nx, 256), ny); }
 
-// the row-march kernel for (SUPG, array nu, cells per lane)
-static const void *pred_rows_kernel(bool supg, bool nua, int vec) {
-#define CFD_PRK(V_)                                                                                         \
-    return supg ? (nua ? (const void *)k_predictor_rows<true, true, V_> : (const void *)k_predictor_rows<true, false, V_>) \
-                : (nua ? (const void *)k_predictor_rows<false, true, V_> : (const void *)k_predictor_rows<false, false, V_>)
-    if (vec == 4) CFD_PRK(4);
-    if (vec == 2) CFD_PRK(2);
-    CFD_PRK(1);
-#undef CFD_PRK
+static thread_local int g_last_pred[3] = {-1, 0, 0};
+void set_last_predictor(int path, int tau, int vec) {
+    g_last_pred[0] = path;
+    g_last_pred[1] = tau;
+    g_last_pred[2] = vec;
 }
-// workgroups of that kernel resident on the device at once
-static int pred_rows_resident(const void *f) {
-    int dev = 0, cus = 256, per = 0;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+int pred_rows_resident(const void *f) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(dev, f);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int cus = 256, per = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per < 1) per = 1;
-    return per * cus;
+    return cache[key] = per * cus;
 }
 static int grid1d(size_t n) {
     long b = (long)((n + 255) / 256);
@@ -1737,8 +1204,8 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
     CFD_SHAPE2D(ny, nx);
     const PredConst k = make_pred_const(dx, dy);
     hipStream_t s = as_stream(stream);
-    // cells per lane of the row march: the preferred count (tuning; auto 4),
-    // lowered until nx and every array's alignment allow it
+    // cells per lane of the row march: the preferred count (tuning; default
+    // 2), halved until nx and every array's alignment allow it (1 always does)
     int vec = tuning().pred_vec ? tuning().pred_vec : 2;
     auto fits = [&](int w) {
         const uintptr_t m = (uintptr_t)(4 * w - 1);
@@ -1746,10 +1213,11 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
         return nx % w == 0 && al(u) && al(v) && al(u_star) && al(v_star) && al(tau) && al(nu_eff);
     };
     while (vec > 1 && !fits(vec)) vec /= 2;
-    const bool rows_ok = (size_t)ny * nx * sizeof(float) < ((size_t)1 << 31) && fits(vec);
-    const int tk = timing_begin(s);
+    const bool rows_ok = (size_t)ny * nx * sizeof(float) < ((size_t)1 << 31);
+    const int tau_mode = use_supg ? tuning().pred_tau : kTauExact;
+    const int tk = timing_begin(s, kTimingPredictor);
     if (tuning().pred_variant != 1 && rows_ok) {
-        PredRowArgs a;
+        PredRowArgs<float> a;
         a.u = u;
         a.v = v;
         a.nu = nu_eff;
@@ -1760,33 +1228,17 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
         a.dt = dt;
         a.ny = ny;
         a.nx = nx;
-        a.nseg = ceil_div(nx, 64 * vec);
-        a.groups = ceil_div(a.nseg, 4);
         a.k = k;
-        const void *f = pred_rows_kernel(use_supg != 0, nu_eff != nullptr, vec);
-        // rows per chunk: every workgroup resident at once (one round at the
-        // kernel's occupancy), chunks of at least 8 rows (2 halo rows each)
-        // (r04 sweep, 8192^2 SUPG: 16-row chunks -- several rounds -- beat one
-        // resident round of 64-row chunks by 8-15 % with the patch queue, whose
-        // drains short chunks spread over the run; with the in-march fallbacks
-        // 16 rows still beat 32 / 64 by 2-7 %)
-        a.rows = tuning().pred_rows;
-        if (a.rows <= 0) {
-            const int resident = pred_rows_resident(f);
-            const int chunks = resident / a.groups > 0 ? resident / a.groups : 1;
-            a.rows = ceil_div(ny, chunks);
-            if (a.rows > 16) a.rows = 16;
-            if (a.rows < 8) a.rows = 8;
-        }
-        const int nblk = a.groups * ceil_div(ny, a.rows);
-        void *args[] = {&a};
-        CFD_CHECK_HIP(hipLaunchKernel(f, dim3(nblk), dim3(256), args, 0, s));
+        CFD_CHECK_HIP(pred_rows_launch<float>(a, use_supg != 0, tau_mode, vec, tuning().pred_rows, s));
+        set_last_predictor(1, tau_mode, vec);
     } else if (use_supg) {
         hipLaunchKernelGGL(k_predictor<true>, grid2d(ny, nx), dim3(256), 0, s, u, v, nu_eff, nu_eff_scalar, u_star,
                            v_star, tau, ny, nx, dt, k);
+        set_last_predictor(0, kTauExact, 1);
     } else {
         hipLaunchKernelGGL(k_predictor<false>, grid2d(ny, nx), dim3(256), 0, s, u, v, nu_eff, nu_eff_scalar, u_star,
                            v_star, tau, ny, nx, dt, k);
+        set_last_predictor(0, kTauExact, 1);
     }
     timing_end(tk, s, 1);
     CFD_LAUNCH_CHECK();
@@ -1796,6 +1248,18 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
 // 0: auto (row march when the shape allows it), 1: one thread per cell
 // (k_predictor), 2: row march; rows per chunk (0: auto); cells per lane
 // (0: auto, 1, 2, 4)
+int cfd_set_predictor2d_tau_mode(int mode) {
+    CFD_REQUIRE(mode == kTauExact || mode == kTauFast, "predictor2d tau mode: 0 (exact) or 1 (fast)");
+    tuning().pred_tau = mode;
+    return CFD_OK;
+}
+
+int cfd_get_last_predictor2d_path(int *tau_mode, int *cells_per_lane) {
+    if (tau_mode) *tau_mode = g_last_pred[1];
+    if (cells_per_lane) *cells_per_lane = g_last_pred[2];
+    return g_last_pred[0];
+}
+
 int cfd_set_predictor2d_config(int variant, int rows, int cells_per_lane) {
     CFD_REQUIRE(variant >= 0 && variant <= 2 && rows >= 0, "predictor2d config: variant 0..2, rows >= 0");
     CFD_REQUIRE(cells_per_lane == 0 || cells_per_lane == 1 || cells_per_lane == 2 || cells_per_lane == 4,

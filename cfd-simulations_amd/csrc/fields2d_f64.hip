@@ -22,7 +22,9 @@
 // v5.py:633); the red-black GS runs as in-place colour passes, two launches
 // per iteration, with the device-side stop rule of the float32 path.
 #include "common.hpp"
+#include "internal.hpp"
 #include "libm_pow.hpp"
+#include "pred_rows.hpp"
 
 namespace cfd {
 namespace {
@@ -503,15 +505,45 @@ int cfd_predictor2d_f64(const double *u, const double *v, const double *nu_eff, 
     CFD_REQUIRE(u_star != u && v_star != v && u_star != v && v_star != u,
                 "predictor2d_f64: outputs must not alias inputs");
     CFD_SHAPE2D64(ny, nx);
-    const Pred64 k = make_pred64(dx, dy);
-    const int tk = timing_begin(as_stream(stream));
-    if (use_supg)
-        hipLaunchKernelGGL(k_predictor64<true>, grid2d64(ny, nx), dim3(256), 0, as_stream(stream), u, v, nu_eff,
-                           nu_eff_scalar, u_star, v_star, tau, ny, nx, dt, k);
-    else
-        hipLaunchKernelGGL(k_predictor64<false>, grid2d64(ny, nx), dim3(256), 0, as_stream(stream), u, v, nu_eff,
-                           nu_eff_scalar, u_star, v_star, tau, ny, nx, dt, k);
-    timing_end(tk, as_stream(stream), 1);
+    hipStream_t s = as_stream(stream);
+    // the row march (pred_rows.hpp): cells per lane 2 (16 B) or 1, halved
+    // until nx and every array's alignment allow it
+    int vec = tuning().pred_vec == 1 ? 1 : 2;
+    auto fits = [&](int w) {
+        const uintptr_t m = (uintptr_t)(8 * w - 1);
+        auto al = [&](const void *p_) { return !p_ || ((uintptr_t)p_ & m) == 0; };
+        return nx % w == 0 && al(u) && al(v) && al(u_star) && al(v_star) && al(tau) && al(nu_eff);
+    };
+    while (vec > 1 && !fits(vec)) vec /= 2;
+    const bool rows_ok = (size_t)ny * nx * sizeof(double) < ((size_t)1 << 31) && fits(vec);
+    const int tau_mode = use_supg ? tuning().pred_tau : kTauExact;
+    const int tk = timing_begin(s, kTimingPredictor);
+    if (tuning().pred_variant != 1 && rows_ok) {
+        PredRowArgs<double> a;
+        a.u = u;
+        a.v = v;
+        a.nu = nu_eff;
+        a.us = u_star;
+        a.vs = v_star;
+        a.tau = use_supg ? tau : nullptr;
+        a.nu_s = nu_eff_scalar;
+        a.dt = dt;
+        a.ny = ny;
+        a.nx = nx;
+        a.k = make_pred_k<double>(dx, dy);
+        CFD_CHECK_HIP(pred_rows_launch<double>(a, use_supg != 0, tau_mode, vec, tuning().pred_rows, s));
+        set_last_predictor(1, tau_mode, vec);
+    } else {
+        const Pred64 k = make_pred64(dx, dy);
+        if (use_supg)
+            hipLaunchKernelGGL(k_predictor64<true>, grid2d64(ny, nx), dim3(256), 0, s, u, v, nu_eff, nu_eff_scalar,
+                               u_star, v_star, tau, ny, nx, dt, k);
+        else
+            hipLaunchKernelGGL(k_predictor64<false>, grid2d64(ny, nx), dim3(256), 0, s, u, v, nu_eff, nu_eff_scalar,
+                               u_star, v_star, tau, ny, nx, dt, k);
+        set_last_predictor(0, kTauExact, 1);
+    }
+    timing_end(tk, s, 1);
     CFD_LAUNCH_CHECK();
     return CFD_OK;
 }

@@ -52,12 +52,17 @@ struct Tuning {
     // diagnostics: the tall-tile kernels' per-wave step timestamps (workgroup
     // 0, 64 steps, 5 marks each, 16 waves' worth: 40 KiB) into this buffer
     void *tbr_trace = nullptr;
-    // fused 2-D predictor (cfd_predictor2d_f32): 0 auto (the row march when
-    // nx % 4 == 0 and the arrays are 16-byte aligned), 1 one thread per cell,
-    // 2 row march; rows per chunk of the row march (0: one resident round)
+    // fused 2-D predictor (cfd_predictor2d_f32 / _f64): 0 auto (the row march
+    // whenever the arrays are below 2^31 bytes), 1 one thread per cell, 2 row
+    // march; rows per chunk of the row march (0: one resident round, 8..16)
     int pred_variant = 0, pred_rows = 0;
-    // row march: cells per lane (0 auto, 1, 2, 4)
+    // row march: preferred cells per lane (0: 2; f32 1, 2, 4; f64 1, 2),
+    // halved until nx and every pointer's alignment fit
     int pred_vec = 0;
+    // SUPG tau: 0 exact (glibc powf / pow, bit-exact with the reference's
+    // NumPy scalars), 1 fast (x*x, correctly rounded sqrt, rcp + Newton
+    // divisions: the compiled reference's fastmath arithmetic, within 1e-6)
+    int pred_tau = 0;
     // persistent small-grid solves (jacobi2d_persist, rbgs2d_persist): launch
     // cooperatively (the runtime guarantees every tile co-resident or refuses
     // the launch, which then takes the launch-per-pass path); the bound of a

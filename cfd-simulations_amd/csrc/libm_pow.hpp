@@ -68,7 +68,7 @@ CFD_HD int checkint64(uint64_t iy) {
 CFD_HD bool zeroinfnan64(uint64_t i) { return 2 * i - 1 >= 2 * asu64(INFINITY) - 1; }
 
 // log(x) as hi + *tail for the bits ix of a positive normal x
-CFD_HD double pow_log_inline(uint64_t ix, double *tail) {
+CFD_HD double pow_log_inline(uint64_t ix, double *tail, const double (*tab)[3] = kPowTab) {
     constexpr uint64_t OFF = 0x3fe6955500000000ULL;
     const uint64_t tmp = ix - OFF;
     const int i = (int)((tmp >> (52 - 7)) % 128);
@@ -76,7 +76,7 @@ CFD_HD double pow_log_inline(uint64_t ix, double *tail) {
     const uint64_t iz = ix - (tmp & 0xfffULL << 52);
     const double z = asf64(iz);
     const double kd = (double)k;
-    const double invc = kPowTab[i][0], logc = kPowTab[i][1], logctail = kPowTab[i][2];
+    const double invc = tab[i][0], logc = tab[i][1], logctail = tab[i][2];
     const double r = CFD_FMA(z, invc, -1.0);
     const double t1 = CFD_FMA(kd, kPowLn2hi, logc);      // kd * Ln2hi + logc
     const double t2 = t1 + r;
@@ -121,7 +121,7 @@ CFD_HD double pow_exp_specialcase(double tmp, uint64_t sbits, uint64_t ki) {
     return 0x1p-1022 * y;
 }
 
-CFD_HD double pow_exp_inline(double x, double xtail, uint32_t sign_bias) {
+CFD_HD double pow_exp_inline(double x, double xtail, uint32_t sign_bias, const unsigned long long *etab = kExpTab) {
     uint32_t abstop = top12(x) & 0x7ff;
     if (abstop - top12(0x1p-54) >= top12(512.0) - top12(0x1p-54)) {
         if (abstop - top12(0x1p-54) >= 0x80000000u) {
@@ -141,8 +141,8 @@ CFD_HD double pow_exp_inline(double x, double xtail, uint32_t sign_bias) {
     r += xtail;
     const uint64_t idx = 2 * (ki % 128);
     const uint64_t top = (ki + sign_bias) << (52 - 7);
-    const double tail = asf64(kExpTab[idx]);
-    const uint64_t sbits = kExpTab[idx + 1] + top;
+    const double tail = asf64(etab[idx]);
+    const uint64_t sbits = etab[idx + 1] + top;
     const double r2 = r * r;
     // tail + r + r2 (C2 + r C3) + r2 r2 (C4 + r C5), both products contracted
     const double t = CFD_FMA(r2, CFD_FMA(r, kExpC[1], kExpC[0]), tail + r);
@@ -152,7 +152,9 @@ CFD_HD double pow_exp_inline(double x, double xtail, uint32_t sign_bias) {
     return CFD_FMA(scale, tmp, scale);
 }
 
-CFD_HD double pow(double x, double y) {
+// (tab / etab: the log and exp tables -- a kernel may pass copies in LDS, so
+// that a table read does not wait on its global loads in flight)
+CFD_HD double pow(double x, double y, const double (*tab)[3] = kPowTab, const unsigned long long *etab = kExpTab) {
     constexpr uint32_t SIGN_BIAS = 0x800 << 7;
     uint32_t sign_bias = 0;
     uint64_t ix = asu64(x), iy = asu64(y);
@@ -190,10 +192,10 @@ CFD_HD double pow(double x, double y) {
         }
     }
     double lo;
-    const double hi = pow_log_inline(ix, &lo);
+    const double hi = pow_log_inline(ix, &lo, tab);
     const double ehi = y * hi;
     const double elo = CFD_FMA(y, lo, CFD_FMA(y, hi, -ehi));  // y * lo + fma(y, hi, -ehi)
-    return pow_exp_inline(ehi, elo, sign_bias);
+    return pow_exp_inline(ehi, elo, sign_bias, etab);
 }
 
 }  // namespace libm

@@ -273,9 +273,21 @@ def clean_divergence_fast(u, v, dx, dy, iterations=2, workspace=None):
     return u, v
 
 
-def predictor_fused(u, v, dx, dy, dt, nu_eff, use_supg=True, u_star=None, v_star=None, tau=None):
-    """v5.py:388-403 in one pass: returns (u_star, v_star, tau)."""
+TAU_MODES = {"exact": 0, "fast": 1}
+
+
+def predictor_fused(u, v, dx, dy, dt, nu_eff, use_supg=True, u_star=None, v_star=None, tau=None, tau_mode=None):
+    """v5.py:388-403 in one pass: returns (u_star, v_star, tau).
+
+    tau_mode: "exact" (the reference's NumPy scalar `**`: glibc powf / pow,
+    bit-exact), "fast" (the compiled reference's fastmath x*x / sqrt, within
+    1e-6 relative L-inf), or None (the calling thread's current setting,
+    cfd_set_predictor2d_tau_mode; "exact" unless changed)."""
     ny, nx = _shape2d(u)
+    if tau_mode is not None:
+        if tau_mode not in TAU_MODES:
+            raise ValueError(f"tau_mode must be one of {sorted(TAU_MODES)}, not {tau_mode!r}")
+        call("cfd_set_predictor2d_tau_mode", TAU_MODES[tau_mode])
     us = torch.empty_like(u) if u_star is None else u_star
     vs = torch.empty_like(v) if v_star is None else v_star
     if tau is None and use_supg:

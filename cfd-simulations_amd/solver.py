@@ -66,6 +66,10 @@ class OptimizedTurbulentConfig:
     dpi: int = 200
     # build-only knobs (not in the reference)
     log_diagnostics: bool = False   # compute the v5.py:410-435 log values on device
+    # SUPG tau arithmetic: "exact" = the reference's NumPy scalar `**` (glibc
+    # powf / pow; bit-exact time_step), "fast" = the compiled reference's
+    # fastmath form (x*x, correctly rounded sqrt; within 1e-6 relative L-inf)
+    supg_tau: str = "exact"
     device: str = "cuda"
 
     def __post_init__(self):
@@ -75,6 +79,8 @@ class OptimizedTurbulentConfig:
         self.dt = np.float32(self.dt_base)
         self.artificial_viscosity = np.float32(self.artificial_viscosity)
         self.parallel_threads = min(self.parallel_threads, os.cpu_count() or 1)
+        if self.supg_tau not in ("exact", "fast"):
+            raise ValueError(f"supg_tau must be 'exact' or 'fast', not {self.supg_tau!r}")
 
 
 # ------------------------------------------------------------ host setup
@@ -310,7 +316,7 @@ class OptimizedTurbulentSolver:
         # nu_eff = nu + nu_t + art_visc with nu_t == 0 in the fields' dtype (v5.py:388)
         nu_eff = self._np(self._np(cfg.nu) + self._np(0.0)) + self._np(cfg.artificial_viscosity)
         K.predictor_fused(self.u, self.v, cfg.dx, cfg.dy, dt, nu_eff, cfg.use_supg,
-                          u_star=self.u_star, v_star=self.v_star, tau=self.tau_supg)
+                          u_star=self.u_star, v_star=self.v_star, tau=self.tau_supg, tau_mode=cfg.supg_tau)
         if not cfg.use_supg:
             self.tau_supg.zero_()
         force_strength = min(1.0, self.step / cfg.initial_steps)

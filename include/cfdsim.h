@@ -175,14 +175,30 @@ int cfd_laplacian2d_f32(const float *phi, const float *nu_eff, float nu_eff_scal
 int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, float nu_eff_scalar,
                         float *u_star, float *v_star, float *tau, int ny, int nx,
                         double dx, double dy, float dt, int use_supg, void *stream);
-/* Kernel of cfd_predictor2d_f32 (tuning, per host thread; same bits either
- * way): variant 0 = auto (the row-march tile kernel when ny*nx < 2^29; else
- * one thread per cell), 1 = one thread per cell, 2 = row march where it
- * applies; rows = rows per row-march chunk (0 = auto: every workgroup resident
- * in one round); cells_per_lane = adjacent cells per lane of the row march (0 =
- * auto, 1, 2, 4), lowered until nx % it == 0 and every array is aligned to
- * 4 * it bytes. */
+/* Kernel of cfd_predictor2d_f32 / _f64 (tuning, per host thread; same bits
+ * either way): variant 0 = auto (the row-march tile kernel when the arrays are
+ * below 2^31 bytes; else one thread per cell), 1 = one thread per cell, 2 =
+ * row march where it applies; rows = rows per row-march chunk (0 = auto: every
+ * workgroup resident in one round, 8..16 rows); cells_per_lane = adjacent
+ * cells per lane of the row march (0 = auto: 2; f32 1, 2, 4; f64 1, 2),
+ * halved until nx % it == 0 and every array is aligned to it elements. */
 int cfd_set_predictor2d_config(int variant, int rows, int cells_per_lane);
+/* SUPG tau arithmetic of cfd_predictor2d_f32 / _f64 (per host thread):
+ * 0 = exact (default): |V| = (u**2 + v**2)**0.5 through device copies of
+ *     glibc's powf / pow, as the reference's NumPy scalar `**` runs it
+ *     (v5.py:155): bit-exact with the reference's time_step;
+ * 1 = fast: the compiled reference's fastmath arithmetic (v5.py:149 is
+ *     @njit(fastmath=True): x**2 -> x*x, **0.5 -> sqrt): sqrt(u*u + v*v)
+ *     correctly rounded, tau's two divisions on the hardware reciprocal plus
+ *     one Newton step (f32; IEEE in f64).  Within 1e-6 relative L-infinity of
+ *     mode 0 on u*, v*, tau (tests/test_gpu_predictor.py).
+ * The one-thread-per-cell kernel (variant 1, or arrays past 2^31 bytes)
+ * always computes mode 0. */
+int cfd_set_predictor2d_tau_mode(int mode);
+/* The calling thread's last predictor launch: returns 1 = row march, 0 = one
+ * thread per cell, -1 = none yet; *tau_mode (0 exact / 1 fast) and
+ * *cells_per_lane of that launch (either pointer may be NULL). */
+int cfd_get_last_predictor2d_path(int *tau_mode, int *cells_per_lane);
 
 /* compute_divergence_fast, v5.py:178-187.  absmax (device float*, optional):
  * receives max|div| (the v5.py:410 diagnostic); must be zeroed by the caller. */
@@ -532,6 +548,11 @@ int cfd_get_last_tbr_shape(int *levels, int *row_waves, int *rows_per_wave, int 
  * cover.  Not for use under graph capture. */
 int cfd_timing_enable(int enable);
 int cfd_timing_read(double *ms, long long *sweeps, int reset);
+/* The same for one channel: 0 = the pressure solves (cfd_timing_read), 1 =
+ * the predictor launches (cfd_predictor2d_f32 / _f64, one count per launch),
+ * so a timed time_step reports the solve's sweeps without the predictor in
+ * them.  reset clears both channels. */
+int cfd_timing_read_channel(int channel, double *ms, long long *sweeps, int reset);
 
 #ifdef __cplusplus
 }

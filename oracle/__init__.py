@@ -68,6 +68,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_rbgs2d_f32_mt.restype = _i
         L.oracle_threads.restype = _i
         L.oracle_predictor2d_f32.argtypes = [_f32p, _f32p, _f32p, _i, _i, _d, _d, _f, _i] + [_f32p] * 7
+        L.oracle_predictor2d_f32_mode.argtypes = [_f32p, _f32p, _f32p, _i, _i, _d, _d, _f, _i, _i] + [_f32p] * 7
+        L.oracle_predictor2d_f64.argtypes = [_f64p, _f64p, _f64p, _i, _i, _d, _d, _d, _i, _i] + [_f64p] * 7
         L.oracle_divergence2d_f32.argtypes = [_f32p, _f32p, _f32p, _i, _i, _d, _d]
         L.oracle_gradient2d_f32.argtypes = [_f32p, _f32p, _f32p, _i, _i, _d, _d]
         L.oracle_powf_f32.argtypes = [_f32p, _f, _f32p, ctypes.c_size_t]
@@ -185,15 +187,27 @@ def jacobi3d_numpy(div, *, h, dt, iters):
 
 
 # ---------------------------------------------------------------- predictor
-def predictor2d(u, v, nu_eff, *, dx, dy, dt, use_supg=True):
-    """a6-a10 (v5.py:112-176, :388-403).  Returns a dict of every array."""
-    u = np.ascontiguousarray(u, np.float32)
-    v = np.ascontiguousarray(v, np.float32)
-    nu = np.ascontiguousarray(np.broadcast_to(np.asarray(nu_eff, np.float32), u.shape))
+def predictor2d(u, v, nu_eff, *, dx, dy, dt, use_supg=True, fastmath=False, dtype=np.float32):
+    """a6-a10 (v5.py:112-176, :388-403).  Returns a dict of every array.
+
+    dtype float32 (memory_efficient=True) or float64 (False, v5.py:287-296:
+    float64 scalars, libm pow, Python constants unrounded).  fastmath: |V| as
+    the compiled reference computes it (@njit(fastmath=True), v5.py:149:
+    x**2 -> x*x, **0.5 -> a correctly rounded sqrt) instead of NumPy's scalar
+    `**` (libm powf / pow) -- the checker of the build's tau mode 1."""
+    dtype = np.dtype(dtype)
+    u = np.ascontiguousarray(u, dtype)
+    v = np.ascontiguousarray(v, dtype)
+    nu = np.ascontiguousarray(np.broadcast_to(np.asarray(nu_eff, dtype), u.shape))
     out = {k: np.empty_like(u) for k in ("tau", "conv_u", "conv_v", "lap_u", "lap_v", "u_star", "v_star")}
-    lib().oracle_predictor2d_f32(u, v, nu, u.shape[0], u.shape[1], float(dx), float(dy), np.float32(dt),
-                                 int(bool(use_supg)), out["tau"], out["conv_u"], out["conv_v"],
-                                 out["lap_u"], out["lap_v"], out["u_star"], out["v_star"])
+    if dtype == np.float64:
+        lib().oracle_predictor2d_f64(u, v, nu, u.shape[0], u.shape[1], float(dx), float(dy), float(dt),
+                                     int(bool(use_supg)), int(bool(fastmath)), out["tau"], out["conv_u"],
+                                     out["conv_v"], out["lap_u"], out["lap_v"], out["u_star"], out["v_star"])
+    else:
+        lib().oracle_predictor2d_f32_mode(u, v, nu, u.shape[0], u.shape[1], float(dx), float(dy), np.float32(dt),
+                                          int(bool(use_supg)), int(bool(fastmath)), out["tau"], out["conv_u"],
+                                          out["conv_v"], out["lap_u"], out["lap_v"], out["u_star"], out["v_star"])
     return out
 
 

@@ -335,10 +335,12 @@ int oracle_rbgs2d_f32_mt(float *phi, const float *div, const uint8_t *mask,
 }
 
 /* ---- a6: compute_supg_stabilization_fast, v5.py:149-162 --------------- */
-static float supg_tau(float u, float v, float nu, double h, float dt) {
+static float supg_tau(float u, float v, float nu, double h, float dt, int fastmath) {
     /* NumPy float32 scalar `u**2` and `** 0.5` both go through libm powf,
-     * which is not always the correctly rounded u*u or sqrt: keep powf. */
-    float vm = powf(powf(u, 2.0f) + powf(v, 2.0f), 0.5f);
+     * which is not always the correctly rounded u*u or sqrt: keep powf.
+     * fastmath: the compiled form (@njit(fastmath=True), v5.py:149): x*x and
+     * a correctly rounded sqrt (the build's tau mode 1). */
+    float vm = fastmath ? sqrtf(u * u + v * v) : powf(powf(u, 2.0f) + powf(v, 2.0f), 0.5f);
     if (vm > (float)1e-10) {
         float pe = (vm * (float)h) / (nu + (float)1e-10);
         float half = pe / 2.0f;
@@ -346,6 +348,19 @@ static float supg_tau(float u, float v, float nu, double h, float dt) {
         return ((float)h / (2.0f * vm)) * lim;
     }
     return dt / 2.0f;
+}
+
+/* the same on float64 scalars (memory_efficient=False): libm pow, Python
+ * float constants unrounded (NEP 50) */
+static double supg_tau64(double u, double v, double nu, double h, double dt, int fastmath) {
+    double vm = fastmath ? sqrt(u * u + v * v) : pow(pow(u, 2.0) + pow(v, 2.0), 0.5);
+    if (vm > 1e-10) {
+        double pe = (vm * h) / (nu + 1e-10);
+        double half = pe / 2.0;
+        double lim = (half < 1.0) ? half : 1.0;
+        return (h / (2.0 * vm)) * lim;
+    }
+    return dt / 2.0;
 }
 
 /* libm powf elementwise (NumPy float32 scalar `**`): the checker for the
@@ -365,8 +380,8 @@ void oracle_pow_f64(const double *x, double y, double *out, size_t n) {
  * Writes tau (SUPG only), conv_u/conv_v, lap_u/lap_v and u_star/v_star.
  * Boundary rings of tau/conv/lap are 0 (np.zeros_like), so
  * u_star = u + dt*(-0 + 0) there.                                            */
-void oracle_predictor2d_f32(const float *u, const float *v, const float *nu_eff,
-                            int ny, int nx, double dx, double dy, float dt, int use_supg,
+void oracle_predictor2d_f32_mode(const float *u, const float *v, const float *nu_eff,
+                            int ny, int nx, double dx, double dy, float dt, int use_supg, int fastmath,
                             float *tau, float *conv_u, float *conv_v, float *lap_u,
                             float *lap_v, float *u_star, float *v_star) {
     size_t n = (size_t)ny * nx;
@@ -384,7 +399,7 @@ void oracle_predictor2d_f32(const float *u, const float *v, const float *nu_eff,
     if (use_supg)
         for (int i = 1; i < ny - 1; ++i)
             for (int j = 1; j < nx - 1; ++j)
-                tau[IDX(i, j)] = supg_tau(u[IDX(i, j)], v[IDX(i, j)], nu_eff[IDX(i, j)], h, dt);
+                tau[IDX(i, j)] = supg_tau(u[IDX(i, j)], v[IDX(i, j)], nu_eff[IDX(i, j)], h, dt, fastmath);
     for (int pass = 0; pass < 2; ++pass) {
         const float *f = pass ? v : u;
         float *conv = pass ? conv_v : conv_u;
@@ -412,6 +427,71 @@ void oracle_predictor2d_f32(const float *u, const float *v, const float *nu_eff,
                 }
                 float l1 = ((E - 2.0f * C) + W) * lx;
                 float l2 = ((N - 2.0f * C) + S) * ly;
+                lap[IDX(i, j)] = nu_eff[IDX(i, j)] * (l1 + l2);
+            }
+    }
+    for (size_t k = 0; k < n; ++k) {
+        u_star[k] = u[k] + dt * (-conv_u[k] + lap_u[k]);
+        v_star[k] = v[k] + dt * (-conv_v[k] + lap_v[k]);
+    }
+}
+
+void oracle_predictor2d_f32(const float *u, const float *v, const float *nu_eff,
+                            int ny, int nx, double dx, double dy, float dt, int use_supg,
+                            float *tau, float *conv_u, float *conv_v, float *lap_u,
+                            float *lap_v, float *u_star, float *v_star) {
+    oracle_predictor2d_f32_mode(u, v, nu_eff, ny, nx, dx, dy, dt, use_supg, 0, tau, conv_u, conv_v, lap_u, lap_v,
+                                u_star, v_star);
+}
+
+/* a6-a10 in float64 (memory_efficient=False, v5.py:287-296) */
+void oracle_predictor2d_f64(const double *u, const double *v, const double *nu_eff,
+                            int ny, int nx, double dx, double dy, double dt, int use_supg, int fastmath,
+                            double *tau, double *conv_u, double *conv_v, double *lap_u,
+                            double *lap_v, double *u_star, double *v_star) {
+    size_t n = (size_t)ny * nx;
+    memset(tau, 0, n * sizeof(double));
+    memset(conv_u, 0, n * sizeof(double));
+    memset(conv_v, 0, n * sizeof(double));
+    memset(lap_u, 0, n * sizeof(double));
+    memset(lap_v, 0, n * sizeof(double));
+    const double h = dx < dy ? dx : dy;
+    const double sdx = 0.5 / dx, sdy = 0.5 / dy;               /* supg dx_inv (quirk) */
+    const double c1x = 0.5 * sdx, c1y = 0.5 * sdy;
+    const double c2x = sdx * sdx, c2y = sdy * sdy;
+    const double ux = 1.0 / dx, uy = 1.0 / dy; /* upwind dx_inv */
+    const double lx = 1.0 / (dx * dx), ly = 1.0 / (dy * dy);
+    if (use_supg)
+        for (int i = 1; i < ny - 1; ++i)
+            for (int j = 1; j < nx - 1; ++j)
+                tau[IDX(i, j)] = supg_tau64(u[IDX(i, j)], v[IDX(i, j)], nu_eff[IDX(i, j)], h, dt, fastmath);
+    for (int pass = 0; pass < 2; ++pass) {
+        const double *f = pass ? v : u;
+        double *conv = pass ? conv_v : conv_u;
+        double *lap = pass ? lap_v : lap_u;
+        for (int i = 1; i < ny - 1; ++i)
+            for (int j = 1; j < nx - 1; ++j) {
+                const double uc = u[IDX(i, j)], vc = v[IDX(i, j)];
+                const double C = f[IDX(i, j)], E = f[IDX(i, j + 1)], W = f[IDX(i, j - 1)];
+                const double N = f[IDX(i + 1, j)], S = f[IDX(i - 1, j)];
+                if (use_supg) {
+                    double ddx = (E - W) * c1x, ddy = (N - S) * c1y;
+                    double cs = uc * ddx + vc * ddy;
+                    double t = tau[IDX(i, j)];
+                    if (t > 0.0) {
+                        double d2x = ((E - 2.0 * C) + W) * c2x;
+                        double d2y = ((N - 2.0 * C) + S) * c2y;
+                        conv[IDX(i, j)] = cs - t * (uc * d2x + vc * d2y);
+                    } else {
+                        conv[IDX(i, j)] = cs;
+                    }
+                } else {
+                    double ddx = uc > 0.0 ? (C - W) * ux : (E - C) * ux;
+                    double ddy = vc > 0.0 ? (C - S) * uy : (N - C) * uy;
+                    conv[IDX(i, j)] = uc * ddx + vc * ddy;
+                }
+                double l1 = ((E - 2.0 * C) + W) * lx;
+                double l2 = ((N - 2.0 * C) + S) * ly;
                 lap[IDX(i, j)] = nu_eff[IDX(i, j)] * (l1 + l2);
             }
     }

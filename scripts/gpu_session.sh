@@ -43,6 +43,16 @@ for s in "$@"; do
     testspred) step pytest_pred 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "predictor or powf or time_step or golden or persistent" ;;
     benchpred) step benchpred 600 python bench.py --workload predictor2d_8192 --steps 20 --warmup 3 ;;
     benchpred64) step benchpred64 600 python bench.py --workload predictor2d_8192_f64 --steps 20 --warmup 3 ;;
+    benchpredf) step benchpredf 600 python bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --tau-mode fast ;;
+    benchpred64f) step benchpred64f 600 python bench.py --workload predictor2d_8192_f64 --steps 20 --warmup 3 --tau-mode fast ;;
+    profpredf) step profpredf 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profpredf -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --no-cpu-baseline --tau-mode fast ;;
+    profpred64f) step profpred64f 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profpred64f -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 20 --warmup 3 --no-cpu-baseline --tau-mode fast ;;
+    pmc_fetch_predf) step pmc_fetch_predf 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_predf -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline --tau-mode fast ;;
+    pmc_write_predf) step pmc_write_predf 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_predf -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline --tau-mode fast ;;
+    pmc_fetch_pred64) step pmc_fetch_pred64 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_pred64 -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 12 --warmup 0 --no-cpu-baseline ;;
+    pmc_write_pred64) step pmc_write_pred64 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_pred64 -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 12 --warmup 0 --no-cpu-baseline ;;
+    sq_predf) step sq_predf 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES -d gpurun_out/sq_predf -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline --tau-mode fast ;;
+    testspred2) step pytest_pred2 900 python -u -m pytest tests/test_gpu_predictor.py -q -x --timeout 300 --timeout-method thread ;;
     benchpredv1) step benchpredv1 600 env CFD_PRED_VARIANT=1 python bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --no-cpu-baseline ;;
     profpred) step profpred 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profpred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --no-cpu-baseline ;;
     profpred64) step profpred64 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profpred64 -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 20 --warmup 3 --no-cpu-baseline ;;
