@@ -129,9 +129,7 @@ PROTOTYPES = {
     "cfd_set_jacobi3d_prefetch": (c_int, [c_int]),
     "cfd_set_jacobi2d_blocking": (c_int, [c_int]),
     "cfd_set_jacobi2d_staging": (c_int, [c_int]),
-    "cfd_set_jacobi2d_workgroup_march": (c_int, [c_int]),
     "cfd_get_last_jacobi2d_path": (c_int, [ctypes.POINTER(c_int)]),
-    "cfd_set_clean_divergence_pipeline": (c_int, [c_int]),
     "cfd_reset_tuning": (c_int, []),
     "cfd_get_last_tbr_shape": (c_int, [ctypes.POINTER(c_int)] * 4),
     "cfd_set_small2d_shape": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),

@@ -50,9 +50,6 @@ static Tuning process_defaults() {
         t.j2s_vec = env_int("CFD_J2_SMALL_VEC", 1) == 1 ? 1 : 0;  // 0: 16 bytes per lane
         const int dd = env_int("CFD_J2_DMA", t.j2_dma);
         t.j2_dma = dd == 0 || dd == 4 || dd == 6 ? dd : t.j2_dma;
-        t.clean_pipe = env_int("CFD_CLEAN_PIPE", t.clean_pipe) != 0;
-        const int wg = env_int("CFD_J2_WGM", t.j2_wgm);
-        t.j2_wgm = wg == 0 || wg == 2 || wg == 4 || wg == 8 ? wg : t.j2_wgm;
         t.gs_rw = env_int("CFD_GS_SMALL_RW", 2) == 1 ? 1 : 2;
         t.gs_vec = env_int("CFD_GS_SMALL_VEC", 1) == 4 ? 4 : 1;
         t.gs_wpb = env_int("CFD_GS_SMALL_WPB", 4) == 16 ? 16 : 4;
@@ -244,12 +241,6 @@ int cfd_set_small2d_jacobi_persistent(int on, int sweeps_per_block) {
     const Tuning d = process_defaults();
     tuning().j2_persist = on ? on == 2 : d.j2_persist;
     tuning().j2p_ni = sweeps_per_block ? sweeps_per_block : d.j2p_ni;
-    return CFD_OK;
-}
-
-int cfd_set_clean_divergence_pipeline(int on) {
-    CFD_REQUIRE(on == 0 || on == 1, "clean_divergence pipeline: 0 (per iteration) or 1 (pipelined)");
-    tuning().clean_pipe = on;
     return CFD_OK;
 }
 

@@ -625,329 +625,6 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
     }
 }
 
-// ---------------------------------------------------------------------------
-// Both clean_divergence iterations (v5.py:239-257, iterations = 2) as ONE
-// launch of one workgroup: three groups of NW waves (one wave per 64 rows,
-// a single band of <= 5 * 64 interior rows), one barrier per 16-step chunk
-// for all of them.
-//  * A runs sweep 1 as k_lex_gs_sweep_reg does, from phi = 0: its old values
-//    E and N are the zeros of np.zeros_like (v5.py:242), so only div1 streams
-//    in (LDS-DMA); phi1 goes to the phi workspace.
-//  * B trails A by LB chunks and works on 16-column bands of the whole grid:
-//    at chunk T it forms u1 = u - grad_x(phi1), v1 = v - grad_y(phi1) (the
-//    first iteration's correction, v5.py:255-256, boundary cells unchanged)
-//    for band T - LB into scratch fields, and div2 = div(u1, v1) (v5.py:246)
-//    for band T - LB - 2, whose neighbour bands are then stored; it also copies
-//    phi1 of the rows just below A's / C's wave edges into LDS.
-//  * C runs sweep 2 on the same phi buffer (in place, as the serial loop), LC
-//    chunks behind A: E = phi1 and div2 by LDS-DMA, lane 63's N (the next
-//    wave's first row of phi1) from B's LDS copies.
-// The lags are the chunks each hand-off needs: A's stores of chunk c are
-// complete at the start of its chunk c + R (R = 2, the ring depth: in-order
-// vmcnt) and visible to B after that chunk's barrier; B waits for its own
-// stores every chunk; C's DMAs are issued R chunks early.  The u, v result
-// (u1 - grad_x(phi2), v1 - grad_y(phi2)) is k_sub_gradient2 afterwards.
-// Arithmetic and order are the serial loop's and the kernels' above, bit for
-// bit (test_clean_divergence_lexicographic_shapes).
-constexpr int kCpR = 2;  // DMA ring depth (chunks) of A and C
-// lex_dma_x4 with the device-scope (sc1) policy: misses the CU's L1, so a
-// line cached there before another wave of the workgroup stored into it is
-// never returned stale
-__device__ inline void lex_dma_x4_sc1(v4i32 rs, uint32_t ofs, uint32_t lds_addr) {
-    int saved;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %1\n\t"
-        "buffer_load_dwordx4 %2, %3, 0 offen sc1 lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(saved)
-        : "s"(lds_addr), "v"(ofs), "s"(rs)
-        : "memory");
-}
-// a float load with the device-scope policy (global_load sc1, L1 missed)
-__device__ inline float ld_sc1(const float *p) {
-    return __uint_as_float(
-        __hip_atomic_load(reinterpret_cast<const unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-struct Clean2Args {
-    float *phi;                // in: zeros; out: phi2 (phi1 in between)
-    const float *div1;         // div(u, v)
-    float *div2;               // div(u1, v1), formed here
-    const float *u, *v;        // the input velocity (read only here)
-    float *u1, *v1;            // u - grad_x(phi1), v - grad_y(phi1)
-    int ny, nx, nw, lb, lc, nchunks, nbands, ntot;
-    float cx2, cy2, cd, gx, gy;
-};
-size_t clean2_lds_bytes(int nw, int nx) {
-    return (size_t)kCpR * 4 * 64 * nw * sizeof(float4) + (size_t)kCpR * 8 * 64 * nw * sizeof(float4) +
-           (size_t)nw * (size_t)(nx + kLexPadL + kLexPadR) * sizeof(float);
-}
-__global__ __launch_bounds__(1024) void k_clean2_pipe(Clean2Args a) {
-    __shared__ __attribute__((aligned(16))) float belowA[5][4 * kLexC], belowC[5][4 * kLexC];
-    extern __shared__ float4 cp_lds[];
-    const int NW = a.nw, nt = 64 * NW;
-    const int lane = threadIdx.x & 63;
-    const int wall = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // waves [0, NW): A; [NW, 2 NW): C; the rest of the 16: B
-    const int grp = wall < NW ? 0 : wall < 2 * NW ? 2 : 1;
-    const int wv = grp == 0 ? wall : grp == 2 ? wall - NW : wall - 2 * NW;
-    const int NB = 16 - 2 * NW;
-    const int t = lane + 64 * wv;  // row index in the band (A, C); lane index in the group (B)
-    const int ny = a.ny, nx = a.nx, n = ny * nx;
-    const int nrows = ny - 2, jmax = nx - 2;
-    float4 *ringA = cp_lds;                                  // [R][4 quads][nt]: div1
-    float4 *ringC = cp_lds + (size_t)kCpR * 4 * nt;          // [R][2 fields][4 quads][nt]: phi1, div2
-    float *under = reinterpret_cast<float *>(cp_lds + (size_t)kCpR * 12 * nt);  // [NW][rs]
-    const int rs = nx + kLexPadL + kLexPadR;
-    for (int x = threadIdx.x; x < NW * rs; x += blockDim.x) under[x] = 0.f;
-    const v4i32 rp = buf_rsrc4(a.phi, (uint32_t)(n * 4)), rd1 = buf_rsrc4(a.div1, (uint32_t)(n * 4)),
-                rd2 = buf_rsrc4(a.div2, (uint32_t)(n * 4));
-    const int i = 1 + t;
-    const bool rowok = t < nrows;
-    const int lag = kLexC * wv;
-    const int jb = 1 - lag - t;
-    const int rowc = (i <= ny - 1 ? i : 0) * nx;
-    const uint32_t oE = i <= ny - 1 ? (uint32_t)(rowc + jb + 1) * 4u : kOob;
-    const uint32_t oD = rowok ? (uint32_t)(rowc + jb) * 4u : kOob;
-    const uint32_t qstride = (uint32_t)nt * 16u;
-    const uint32_t laA = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(ringA + wv * 64));
-    const uint32_t laC = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(ringC + wv * 64));
-    // A: chunk c's div1 windows; C: chunk c's phi1 and div2 windows
-    auto issueA = [&](int c, int slot) {
-        const uint32_t d = 64u * (uint32_t)c;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) lex_dma_x4(rd1, oD + d + 16u * q, laA + (uint32_t)(slot * 4 + q) * qstride);
-    };
-    auto issueC = [&](int c, int slot) {
-        const uint32_t d = 64u * (uint32_t)c;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            lex_dma_x4_sc1(rp, oE + d + 16u * q, laC + (uint32_t)((slot * 2 + 0) * 4 + q) * qstride);
-            lex_dma_x4_sc1(rd2, oD + d + 16u * q, laC + (uint32_t)((slot * 2 + 1) * 4 + q) * qstride);
-        }
-    };
-    __syncthreads();  // `under` zeroed
-    float w = 0.f, vprev = 0.f;  // phi(i, 0) = 0: W of column 1
-    if (grp == 0) {
-#pragma unroll
-        for (int r = 0; r < kCpR; ++r) {
-            issueA(r, r);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) buf_store_x1(0.f, kOob, rp);  // the loop's store slots
-        }
-    }
-    // one sweep chunk (A: sweep 1, C: sweep 2) from ring slot `slot`
-    auto sweep_chunk = [&](const bool sw2, const int c, const int slot) {
-        if (sw2)
-            wait_vmcnt<12 * (kCpR - 1)>();  // 4 stores + 8 DMAs were issued after this chunk's
-        else
-            wait_vmcnt<8 * (kCpR - 1)>();   // 4 stores + 4 DMAs
-        float Er[kLexC], Dr[kLexC];
-        const float4 *sl = sw2 ? ringC + (size_t)slot * 8 * nt + t : ringA + (size_t)slot * 4 * nt + t;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 d = sw2 ? sl[(4 + q) * nt] : sl[q * nt];
-            Dr[4 * q] = d.x; Dr[4 * q + 1] = d.y; Dr[4 * q + 2] = d.z; Dr[4 * q + 3] = d.w;
-            if (sw2) {
-                const float4 e = sl[q * nt];
-                Er[4 * q] = e.x; Er[4 * q + 1] = e.y; Er[4 * q + 2] = e.z; Er[4 * q + 3] = e.w;
-            } else {
-                Er[4 * q] = Er[4 * q + 1] = Er[4 * q + 2] = Er[4 * q + 3] = 0.f;
-            }
-        }
-        float S0[kLexC], N63[kLexC];
-        float(*below)[4 * kLexC] = sw2 ? belowC : belowA;
-        if (wv == 0) {
-#pragma unroll
-            for (int k = 0; k < kLexC; ++k) S0[k] = 0.f;  // row 0: phi = 0
-        } else {
-            const int base = (kLexC * c - lag) & (4 * kLexC - 1);
-            const float *ab = below[wv - 1];
-            S0[0] = ab[(base - 1) & (4 * kLexC - 1)];
-#pragma unroll
-            for (int q = 0; q < kLexC / 4; ++q) {
-                const float4 v4 = *reinterpret_cast<const float4 *>(ab + base + 4 * q);
-                if (4 * q + 1 < kLexC) S0[4 * q + 1] = v4.x;
-                if (4 * q + 2 < kLexC) S0[4 * q + 2] = v4.y;
-                if (4 * q + 3 < kLexC) S0[4 * q + 3] = v4.z;
-                if (4 * q + 4 < kLexC) S0[4 * q + 4] = v4.w;
-            }
-        }
-        if (sw2) {
-            const float *ur = under + wv * rs + kLexPadL;
-            const int j0 = min(max(1 - lag - (64 * wv + 63) + kLexC * c, -kLexPadL), nx);  // lane 63's column
-#pragma unroll
-            for (int k = 0; k < kLexC; ++k) N63[k] = ur[j0 + k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < kLexC; ++k) N63[k] = 0.f;
-        }
-        const int jc = jb + kLexC * c;
-        float out[kLexC];
-        bool act[kLexC];
-#pragma unroll
-        for (int k = 0; k < kLexC; ++k) {
-            const float E = Er[k];
-            // sweep 1: N is the old phi below, 0; sweep 2: lane t+1's E, lane 63 from LDS
-            const float N = sw2 ? __int_as_float(__builtin_amdgcn_update_dpp(
-                                      __float_as_int(N63[k]), __float_as_int(E), 0x130, 0xf, 0xf, false))
-                                : 0.f;
-            const float S = __int_as_float(__builtin_amdgcn_update_dpp(
-                __float_as_int(S0[k]), __float_as_int(vprev), 0x138, 0xf, 0xf, false));
-            const float aa = a.cx2 * (E + w);
-            const float bb = a.cy2 * (N + S);
-            const float v = ((aa + bb) - Dr[k]) * a.cd;
-            act[k] = rowok && (uint32_t)(jc + k - 1) < (uint32_t)jmax;
-            w = act[k] ? v : w;
-            vprev = v;
-            out[k] = v;
-        }
-        if (lane == 63) {
-            float *mine = below[wv] + ((kLexC * c - lag) & (4 * kLexC - 1));
-#pragma unroll
-            for (int q = 0; q < kLexC / 4; ++q)
-                *reinterpret_cast<float4 *>(mine + 4 * q) =
-                    make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
-        }
-        // results transposed through the slot's first field (see k_lex_gs_sweep_reg)
-        float4 *tw = (sw2 ? ringC + (size_t)slot * 8 * nt : ringA + (size_t)slot * 4 * nt) + 64 * wv;
-#pragma unroll
-        for (int q = 0; q < kLexC / 4; ++q)
-            tw[q * nt + lane] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
-        const int g = lane >> 4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rho = 16 * q + (lane & 15), tr = 64 * wv + rho;
-            const float4 v4 = tw[g * nt + rho];
-            const int j0 = 1 - lag - tr + kLexC * c + 4 * g;
-            const bool rok = tr < nrows;
-            bool ae[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) ae[e] = rok && (uint32_t)(j0 + e - 1) < (uint32_t)jmax;
-            const bool full = ae[0] && ae[3];
-            const uint32_t o = (uint32_t)((1 + tr) * nx + j0) * 4u;
-            buf_store_x4(v4, full ? o : kOob, rp);
-            const bool part = !full && (ae[0] || ae[1] || ae[2] || ae[3]);
-            if (__any(part)) {
-                buf_store_x1(v4.x, part && ae[0] ? o : kOob, rp);
-                buf_store_x1(v4.y, part && ae[1] ? o + 4u : kOob, rp);
-                buf_store_x1(v4.z, part && ae[2] ? o + 8u : kOob, rp);
-                buf_store_x1(v4.w, part && ae[3] ? o + 12u : kOob, rp);
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads before its refill
-    };
-    // B: u1, v1 of band b (every row, boundary cells copied) and div2 of band
-    // b2.  A lane takes column bcol of the band and rows rg, rg + nrg, ...,
-    // in batches of kCpB rows whose loads are all issued before any store (the
-    // stores could alias them for the compiler, which would serialise them)
-    constexpr int kCpB = 8;
-    const int bcol = lane & 15, rg = t >> 4, nrg = 4 * NB;
-    auto band_uv = [&](int b) {
-        const int j = 16 * b + bcol;
-        if (j >= nx) return;
-        for (int y0 = rg; y0 < ny; y0 += kCpB * nrg) {
-            float uu[kCpB], vv[kCpB], pe[kCpB], pw[kCpB], pn[kCpB], ps[kCpB];
-            bool in_[kCpB];
-#pragma unroll
-            for (int m = 0; m < kCpB; ++m) {
-                const int y = y0 + m * nrg;
-                const int c = min(y, ny - 1) * nx + j;
-                in_[m] = y >= 1 && y <= ny - 2 && j >= 1 && j <= nx - 2;
-                uu[m] = a.u[c];
-                vv[m] = a.v[c];
-                // phi1, written by A's waves: read past L1
-                pe[m] = in_[m] ? ld_sc1(a.phi + c + 1) : 0.f;
-                pw[m] = in_[m] ? ld_sc1(a.phi + c - 1) : 0.f;
-                pn[m] = in_[m] ? ld_sc1(a.phi + c + nx) : 0.f;
-                ps[m] = in_[m] ? ld_sc1(a.phi + c - nx) : 0.f;
-            }
-#pragma unroll
-            for (int m = 0; m < kCpB; ++m) {
-                const int y = y0 + m * nrg;
-                if (y >= ny) break;
-                const int c = y * nx + j;
-                float u1 = uu[m], v1 = vv[m];
-                if (in_[m]) {
-                    const float ga = (pe[m] - pw[m]) * a.gx;
-                    const float gb = (pn[m] - ps[m]) * a.gy;
-                    u1 = u1 - ga;
-                    v1 = v1 - gb;
-                }
-                a.u1[c] = u1;
-                a.v1[c] = v1;
-            }
-        }
-        // phi1 of the first row of each next wave, for C's lane 63
-        if (rg < NW - 1) under[rg * rs + kLexPadL + j] = ld_sc1(a.phi + (1 + 64 * (rg + 1)) * nx + j);
-    };
-    auto band_div = [&](int b) {
-        const int j = 16 * b + bcol;
-        if (j < 1 || j > nx - 2) return;
-        for (int y0 = 1 + rg; y0 <= ny - 2; y0 += kCpB * nrg) {
-            float ue[kCpB], uw[kCpB], vn[kCpB], vs[kCpB];
-#pragma unroll
-            for (int m = 0; m < kCpB; ++m) {
-                const int c = min(y0 + m * nrg, ny - 2) * nx + j;
-                // u1, v1 stored by other lanes of B in earlier chunks: past L1
-                ue[m] = ld_sc1(a.u1 + c + 1);
-                uw[m] = ld_sc1(a.u1 + c - 1);
-                vn[m] = ld_sc1(a.v1 + c + nx);
-                vs[m] = ld_sc1(a.v1 + c - nx);
-            }
-#pragma unroll
-            for (int m = 0; m < kCpB; ++m) {
-                const int y = y0 + m * nrg;
-                if (y > ny - 2) break;
-                a.div2[y * nx + j] = (ue[m] - uw[m]) * a.gx + (vn[m] - vs[m]) * a.gy;
-            }
-        }
-    };
-    for (int T0 = 0; T0 < a.ntot; T0 += kCpR) {
-#pragma unroll
-        for (int r = 0; r < kCpR; ++r) {
-            const int T = T0 + r;
-            if (grp == 0) {
-                sweep_chunk(false, T, r);
-                issueA(T + kCpR, r);
-            } else if (grp == 2) {
-                const int c = T - a.lc;  // C's chunk; slot = c mod R = r (lc is a multiple of R)
-                if (c >= 0) sweep_chunk(true, c, r);
-                if (c + kCpR >= 0) {
-                    issueC(c + kCpR, r);
-                    if (c < 0) {
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) buf_store_x1(0.f, kOob, rp);  // the store slots
-                    }
-                }
-            } else {
-                // the last chunk's stores drained while B waited at the barrier;
-                // they are visible to every wave after this chunk's barrier
-                wait_vmcnt<0>();
-                const int b = T - a.lb;
-                if (b >= 0 && b < a.nbands) band_uv(b);
-                if (b - 3 >= 0 && b - 3 < a.nbands) band_div(b - 3);
-            }
-            lex_lds_barrier();
-        }
-    }
-    wait_vmcnt<0>();  // no DMA lands in LDS after the workgroup is gone
-}
-
-// v5.py:255-256 for the second iteration: u = u1 - grad_x(phi2), v = v1 - grad_y(phi2)
-__global__ void k_sub_gradient2(const float *__restrict__ phi, const float *__restrict__ u1,
-                                const float *__restrict__ v1, float *__restrict__ u, float *__restrict__ v,
-                                int ny, int nx, float cx, float cy) {
-    CFD_2D_INDEX
-    if (!interior(i, j, ny, nx)) return;
-    const float a = (phi[c + 1] - phi[c - 1]) * cx;
-    const float b = (phi[c + nx] - phi[c - nx]) * cy;
-    u[c] = u1[c] - a;
-    v[c] = v1[c] - b;
-}
-
 size_t lex_dma_lds_bytes(int nt, int lx) {
     return (size_t)lx * 4 * nt * sizeof(float4) + (size_t)(nt / 64) * kLexRing * sizeof(float);
 }
@@ -1302,10 +979,9 @@ int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star
 }
 
 size_t cfd_clean_divergence_workspace_bytes(int ny, int nx) {
-    // phi and div scratch fields, sized for float64 (cfd_clean_divergence2d_f64);
-    // the f32 pipelined path takes five f32 fields (phi, div1, div2, u1, v1)
+    // phi and div scratch fields, sized for float64 (cfd_clean_divergence2d_f64)
     const size_t n = (size_t)(ny > 0 ? ny : 0) * (size_t)(nx > 0 ? nx : 0);
-    return 2 * sizeof(double) * n > 5 * sizeof(float) * n ? 2 * sizeof(double) * n : 5 * sizeof(float) * n;
+    return 2 * sizeof(double) * n;
 }
 
 int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, double dy,
@@ -1320,46 +996,6 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
     const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy);
     const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv));
     const float cx = (float)(0.5 / dx), cy = (float)(0.5 / dy);
-    // the solver's two iterations on a single band of rows: one pipelined
-    // launch (k_clean2_pipe) between div(u, v) and the final correction
-    const bool pipe_on = tuning().clean_pipe != 0;  // cfd_set_clean_divergence_pipeline
-    const int nw = ceil_div(ny - 2, 64);
-    if (pipe_on && iterations == 2 && ny >= 3 && nx >= 3 && nw <= 5 && n * 4 < ((size_t)1 << 31) &&
-        clean2_lds_bytes(nw, nx) + 4096 <= kLexRegLdsMax) {
-        float *div2 = div + n, *u1 = div + 2 * n, *v1 = div + 3 * n;
-        hipLaunchKernelGGL(k_divergence, grid2d(ny, nx), dim3(256), 0, s, u, v, div, ny, nx, cx, cy,
-                           (float *)nullptr);
-        Clean2Args a;
-        a.phi = phi; a.div1 = div; a.div2 = div2; a.u = u; a.v = v; a.u1 = u1; a.v1 = v1;
-        a.ny = ny; a.nx = nx; a.nw = nw;
-        const int nrows = ny - 2, jmax = nx - 2, wl = nw - 1;
-        // B's lag: phi1 of every row up to column 16 b + 16 is stored in A's
-        // chunk floor((16 b + 16 + nrows - 2 + 16 wl) / 16), complete R chunks
-        // later and visible after that chunk's barrier
-        a.lb = 4 + (nrows - 2 + 16 * wl) / 16;
-        // C's lag: its DMAs (issued R chunks early) need div2 of band c + 1,
-        // which B forms at T = c + 4 + lb; its stores complete at B's next
-        // chunk and are visible after that chunk's barrier
-        a.lc = a.lb + 6 + kCpR;
-        a.lc += a.lc % kCpR;
-        a.nchunks = (nrows - 2 + jmax + kLexC * wl) / kLexC + 1;
-        a.nbands = ceil_div(nx, 16);
-        int ntot = max(a.lc + a.nchunks, a.lb + a.nbands + 3);
-        a.ntot = ntot + ntot % kCpR;
-        a.cx2 = (float)dx2_inv; a.cy2 = (float)dy2_inv; a.cd = (float)denom_inv;
-        a.gx = cx; a.gy = cy;
-        static bool attr2 = false;
-        if (!attr2) {
-            CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_clean2_pipe),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)(kLexRegLdsMax - 4096)));
-            attr2 = true;
-        }
-        hipLaunchKernelGGL(k_clean2_pipe, dim3(1), dim3(1024), clean2_lds_bytes(nw, nx), s, a);
-        hipLaunchKernelGGL(k_sub_gradient2, grid2d(ny, nx), dim3(256), 0, s, phi, u1, v1, u, v, ny, nx, cx, cy);
-        CFD_LAUNCH_CHECK();
-        return CFD_OK;
-    }
     for (int it = 0; it < iterations; ++it) {
         hipLaunchKernelGGL(k_divergence, grid2d(ny, nx), dim3(256), 0, s, u, v, div, ny, nx, cx, cy,
                            (float *)nullptr);

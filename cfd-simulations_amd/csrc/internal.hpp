@@ -21,8 +21,6 @@ struct Tuning {
     // one row ahead, jacobi2d_tbk, the default: r03 8192^2 f64 0.337 ms per
     // pass against 0.355 (6 ahead) and 0.362 (4 ahead), same box)
     int j2_dma = 0;
-    int j2_wgm = 0;      // 2-D unmasked passes: workgroup-wide row march of this many waves (0: per-wave march)
-    int clean_pipe = 0;  // clean_divergence, 2 iterations, one band: the pipelined launch (1; measured slower, opt-in)
     // small-grid 2-D Jacobi: sweeps per launch (1..8), rows per wave, cells per lane
     int j2s_k = 4, j2s_rw = 1, j2s_vec = 1;
     // small-grid 2-D Jacobi (f32) as one persistent launch (jacobi2d_persist)

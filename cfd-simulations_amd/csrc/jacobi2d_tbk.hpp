@@ -267,156 +267,6 @@ __global__ __launch_bounds__(256) void jacobi2d_tbd(const T *__restrict__ in, T 
     wait_vmcnt<0>();  // no DMA may land in LDS after the workgroup is gone
 }
 
-// jacobi2d_tbk as a WORKGROUP-wide row march (unmasked passes, Tuning
-// j2_wgm = NW waves): the NW waves of a workgroup sit side by side in x
-// (NW * 64 lanes x VEC cells, 4 KB of f64 row at NW = 4, VEC = 2) and march
-// the same rows in lockstep.  Only the workgroup's two outer edges keep
-// HL = ceil(K / VEC) eroding halo lanes; between waves the x-neighbours of a
-// level's row come from the neighbouring wave through LDS.  Level l at step r
-// reads level l - 1's row r - l + 1, which level l - 1 produced in step r - 1
-// (level 0: the row loaded earlier), so one exchange per step serves every
-// level: at the start of step r each wave's lanes 0 and 63 publish their edge
-// cells of the K rows the levels will read (a [parity][level][wave][side]
-// table, double-buffered by step parity), one barrier, and each level's DPP
-// shift takes the neighbour wave's cell as its `old` operand at lane 0 / 63.
-// Per-wave halo recompute falls from 2 HL / 64 lanes (tbk) to 2 HL / (64 NW);
-// the levels, operation order and edge rules are jacobi2d_tbk's: bit-identical.
-template <typename T, int VEC, int K, bool PRE, int NW>
-__global__ __launch_bounds__(NW * 64) void jacobi2d_wgm(const T *__restrict__ in, T *__restrict__ out,
-                                                        const T *__restrict__ div, int ny, int nx, int nsegw,
-                                                        int rows_per_chunk, T dx2, T dtv) {
-    constexpr int HL = (K + VEC - 1) / VEC;
-    constexpr int SOUT = (NW * 64 - 2 * HL) * VEC;  // cells written per workgroup
-    // wave slots 1..NW; slots 0 and NW + 1 stay 0 (the workgroup's outer edges)
-    __shared__ T ex[2][K][NW + 2][2];
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int seg = bid % nsegw, chunk = bid / nsegw;
-    const int y0 = 1 + chunk * rows_per_chunk;
-    if (y0 >= ny - 1) return;  // uniform over the workgroup
-    const int y1 = min(y0 + rows_per_chunk, ny - 1);
-    const int gl = wv * 64 + lane;
-    const int x0 = seg * SOUT - HL * VEC + gl * VEC;
-    const bool valid = x0 >= 0 && x0 < nx;
-    const bool writer = gl >= HL && gl < NW * 64 - HL && valid;
-    auto row = [&](int y) { return (size_t)y * nx + (valid ? x0 : 0); };
-    auto inrow = [&](int y) { return valid && y >= 0 && y <= ny - 1; };
-    for (int q = threadIdx.x; q < 2 * K * 4; q += NW * 64) {
-        const int p = q / (K * 4), l = (q / 4) % K, w = (q / 2) % 2 ? NW + 1 : 0;
-        ex[p][l][w][q % 2] = T(0);
-    }
-    constexpr int U = kTbkUnroll<K>;
-    static_assert(U % 2 == 0, "the exchange parity is the step's slot parity");
-    T Q[K][3][VEC];
-    T R[K][VEC];
-#pragma unroll
-    for (int l = 0; l < K; ++l)
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) Q[l][0][k] = Q[l][1][k] = Q[l][2][k] = R[l][k] = T(0);
-    const int rs = y0 - K + 1;
-    const int rl = y1 + K - 2;
-    const int nsteps = U * ((rl - rs + U) / U);
-    if (inrow(rs - 1)) ld<T, VEC>(in + row(rs - 1), Q[0][2]);
-    if (inrow(rs)) ld<T, VEC>(in + row(rs), Q[0][0]);
-    if (inrow(rs + 1)) ld<T, VEC>(in + row(rs + 1), Q[0][1]);
-    if (inrow(rs)) ld<T, VEC>(div + row(rs), R[0]);
-    const bool edge_l = lane == 0, edge_r = lane == 63;
-    // the neighbour cell this lane reads: lane 0 the left wave's right edge,
-    // every other lane (only lane 63's is used) the right wave's left edge
-    const int nslot = edge_l ? wv : wv + 2, nside = edge_l ? 1 : 0;
-    auto step = [&](int r, auto rotc) {
-        constexpr int RT = decltype(rotc)::value;
-        constexpr int S2 = (RT + 2) % 3;
-        constexpr int PAR = RT & 1;
-        T nq[VEC], nd[VEC];
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) nq[k] = nd[k] = T(0);
-        if (inrow(r + 2)) ld<T, VEC>(in + row(r + 2), nq);
-        if (inrow(r + 1)) ld<T, VEC>(div + row(r + 1), nd);
-        // publish the edge cells of the rows levels 1..K read this step:
-        // level m's row r - m sits in slot (RT - m) mod 3
-        if (edge_l || edge_r) {
-#pragma unroll
-            for (int m = 0; m < K; ++m) {
-                const int sm = ((RT - m) % 3 + 3) % 3;
-                ex[PAR][m][wv + 1][edge_l ? 0 : 1] = edge_l ? Q[m][sm][0] : Q[m][sm][VEC - 1];
-            }
-        }
-        __syncthreads();
-        T nbs[K];  // all K neighbour cells in one batch: one LDS wait per step
-#pragma unroll
-        for (int m = 0; m < K; ++m) nbs[m] = ex[PAR][m][nslot][nside];
-#pragma unroll
-        for (int l = 1; l <= K; ++l) {
-            const int p = r - l + 1;
-            const bool fixed = p == 0 || p == ny - 1;
-            const int sc = ((RT - l + 1) % 3 + 3) % 3, sn = ((RT - l + 2) % 3 + 3) % 3,
-                      ss = ((RT - l) % 3 + 3) % 3, sr = ((RT - l + 1) % K + K) % K;
-            const T *C = Q[l - 1][sc];
-            const T *Nn = Q[l - 1][sn];
-            const T *Ss = Q[l - 1][ss];
-            const T nb = nbs[l - 1];
-            const T wl = dpp_from_lower_old(nb, C[VEC - 1]);
-            const T er = dpp_from_upper_old(nb, C[0]);
-            T v[VEC];
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const T E = (k + 1 < VEC) ? C[k + 1] : er;
-                const T W = (k > 0) ? C[k - 1] : wl;
-                const int x = x0 + k;
-                v[k] = (fixed || x <= 0 || x >= nx - 1) ? C[k] : jac5<T>(E, W, Nn[k], Ss[k], R[sr][k], dx2, dtv, PRE);
-            }
-            if (l < K) {
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) Q[l][sc][k] = v[k];
-            } else if (writer && p >= y0 && p < y1) {
-                st_out<T, VEC>(out + row(p), v);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            Q[0][S2][k] = nq[k];
-            R[(RT + 1) % K][k] = nd[k];
-        }
-    };
-    for (int rb = rs; rb < rs + nsteps; rb += U)
-        static_for(std::make_integer_sequence<int, U>{}, [&](auto i) { step(rb + decltype(i)::value, i); });
-}
-
-// the workgroup march's launch (jacobi2d_tbk_launch's chunk sizing per workgroup)
-template <typename T, int VEC, int K, bool PRE, int NW>
-static void jacobi2d_wgm_launch(const T *in, T *out, const T *div, int ny, int nx, T dx2, T dtv, hipStream_t s) {
-    constexpr int HL = (K + VEC - 1) / VEC;
-    constexpr int SOUT = (NW * 64 - 2 * HL) * VEC;
-    const int nsegw = ceil_div(nx, SOUT);
-    const int rows = ny - 2;
-    static int slots = 0;  // resident workgroups per chip
-    if (slots <= 0) {
-        int nb = 0, dev = 0, ncu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jacobi2d_wgm<T, VEC, K, PRE, NW>, NW * 64, 0) !=
-                hipSuccess ||
-            hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || nb <= 0 ||
-            ncu <= 0) {
-            (void)hipGetLastError();
-            nb = 2;
-            ncu = 256;
-        }
-        slots = nb * ncu;
-    }
-    int nchunk = slots / nsegw;
-    if (nchunk < 1) nchunk = 1;
-    int rpc = ceil_div(rows, nchunk);
-    const int rmin = 2 * (K - 1);
-    if (rpc < rmin) rpc = rmin;
-    constexpr int U = kTbkUnroll<K>;
-    rpc = U * ceil_div(rpc + 2 * K - 2, U) - (2 * K - 2);
-    nchunk = ceil_div(rows, rpc);
-    hipLaunchKernelGGL((jacobi2d_wgm<T, VEC, K, PRE, NW>), dim3(nsegw * nchunk), dim3(NW * 64), 0, s, in, out, div,
-                       ny, nx, nsegw, rpc, dx2, dtv);
-}
-
 template <typename T, int VEC, int K, bool PRE, bool MASK>
 static void jacobi2d_tbk_launch(const T *in, T *out, const T *div, const uint8_t *mask, int ny,
                                 int nx, T dx2, T dtv, hipStream_t s) {
@@ -427,14 +277,6 @@ static void jacobi2d_tbk_launch(const T *in, T *out, const T *div, const uint8_t
     const int rows = ny - 2;
     // the kernel: the LDS-ring march where it applies (jacobi2d_tbd), else the
     // register march
-    if constexpr (!MASK && K == 8) {
-        switch (tuning().j2_wgm) {
-            case 2: jacobi2d_wgm_launch<T, VEC, K, PRE, 2>(in, out, div, ny, nx, dx2, dtv, s); return;
-            case 4: jacobi2d_wgm_launch<T, VEC, K, PRE, 4>(in, out, div, ny, nx, dx2, dtv, s); return;
-            case 8: jacobi2d_wgm_launch<T, VEC, K, PRE, 8>(in, out, div, ny, nx, dx2, dtv, s); return;
-            default: break;
-        }
-    }
     constexpr bool DMA_OK = !MASK && VEC * sizeof(T) == 16 && (K == 4 || K == 6 || K == 8);
     const int dma = DMA_OK ? tuning().j2_dma : 0;
     static int slot_cache[3] = {0, 0, 0};  // resident waves per chip, by kernel (register, ring 4, ring 6)

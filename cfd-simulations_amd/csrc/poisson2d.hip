@@ -1215,13 +1215,6 @@ int cfd_get_last_jacobi2d_path(int *sweeps_per_launch) {
     return g_j2_last[0];
 }
 
-int cfd_set_jacobi2d_workgroup_march(int waves) {
-    CFD_REQUIRE(waves == 0 || waves == 2 || waves == 4 || waves == 8,
-                "workgroup march: 0 (per-wave march), 2, 4 or 8 waves");
-    tuning().j2_wgm = waves;
-    return CFD_OK;
-}
-
 size_t cfd_rbgs_workspace_bytes(int iterations) {
     // flags, maxc[iterations], then the small-grid kernel's kGsSlots slot rows
     static_assert(kGsSlots == kGsSlotRows, "one slot-row count");

@@ -86,12 +86,6 @@ int cfd_get_jacobi2d_levels(void);
  * the faster of the two on MI355X).  Same bits either way (a tuning knob, per
  * host thread like the others). */
 int cfd_set_jacobi2d_staging(int rows_ahead);
-/* Unmasked 8-sweep 2-D passes as a workgroup-wide row march of `waves` waves
- * side by side in x (2, 4 or 8; x-halos between the waves through LDS, halo
- * lanes only at the workgroup's outer edges); 0 = the per-wave march
- * (default).  Bit-identical either way.  Per host thread, like the other
- * tuning setters; env CFD_J2_WGM sets the process default. */
-int cfd_set_jacobi2d_workgroup_march(int waves);
 /* The calling thread's last 2-D Jacobi solve: returns 1 if it ran as one
  * persistent launch (small grids), else 0; *sweeps_per_launch (may be NULL)
  * = the sweeps one launch fused (the iterations, for the persistent solve). */
@@ -221,12 +215,6 @@ int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star
 size_t cfd_clean_divergence_workspace_bytes(int ny, int nx);
 int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, double dy,
                                int iterations, void *ws, void *stream);
-/* on = 1: two iterations on grids of at most 322 rows run as one pipelined
- * launch (sweep 2 trailing sweep 1; fields2d.hip k_clean2_pipe) between
- * div(u, v) and the final correction; 0 (default) = one iteration after the
- * other, measured faster on MI355X.  Same bits.  Per
- * host thread (env CFD_CLEAN_PIPE sets the process default). */
-int cfd_set_clean_divergence_pipeline(int on);
 /* OptimizedTurbulentSolver.apply_boundary_conditions, v5.py:349-360.
  * y: device float64 (ny) grid coordinates (np.linspace, v5.py:272). */
 int cfd_apply_bc2d_f32(float *u, float *v, const double *y, int ny, int nx, double y_max,

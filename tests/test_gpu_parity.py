@@ -101,31 +101,6 @@ def test_jacobi2d_staged_rows_bitexact(dtype, shape, iters, pre, blocking, stagi
         call("cfd_set_jacobi2d_blocking", 0)
 
 
-@pytest.mark.parametrize("waves", [2, 4, 8])
-@pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("shape,iters,pre", [((37, 53), 17, False), ((130, 260), 31, True), ((9, 124), 16, True),
-                                             ((71, 1000), 24, False), ((300, 1500), 9, True), ((517, 40), 8, False),
-                                             ((4, 600), 8, True), ((1030, 2044), 16, True)])
-def test_jacobi2d_workgroup_march_bitexact(dtype, shape, iters, pre, waves):
-    """The workgroup-wide row march (waves side by side, x-halos through LDS)
-    at 8 sweeps per pass: bit-exact against the oracle, ragged widths
-    included (a segment's last wave partly or wholly past the row end)."""
-    call("cfd_set_jacobi2d_blocking", 8)
-    call("cfd_set_jacobi2d_workgroup_march", waves)
-    try:
-        rng = np.random.default_rng(23)
-        div = rng.standard_normal(shape).astype(dtype)
-        phi0 = rng.standard_normal(shape).astype(dtype)
-        ref = oracle.jacobi2d(div, phi0, dx=0.017, dt=np.float32(2e-4), iters=iters)
-        phi = dev(phi0)
-        K.solve_pressure_jacobi(phi, dev(div), 0.017, np.float32(2e-4), None, iters,
-                                rhs_ws=torch.empty_like(phi) if pre else None)
-        assert np.array_equal(host(phi), ref)
-    finally:
-        call("cfd_set_jacobi2d_workgroup_march", 0)
-        call("cfd_set_jacobi2d_blocking", 0)
-
-
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_jacobi2d_rhs_workspace_bitexact(dtype):
     """The RHS prologue (rhs_ws) gives the same bits as the in-register RHS."""
@@ -476,32 +451,26 @@ def test_project_and_clean_divergence_bitexact(golden):
     assert np.array_equal(host(u), cu) and np.array_equal(host(v), cv)
 
 
-@pytest.mark.parametrize("pipe", [1, 0])
 @pytest.mark.parametrize("ny,nx", [(3, 3), (3, 50), (4, 7), (66, 30), (67, 30), (130, 17), (180, 600),
                                    (194, 33), (258, 70), (322, 51), (323, 20), (36, 1200),
                                    (514, 9), (515, 9), (1030, 40)])
-def test_clean_divergence_lexicographic_shapes(ny, nx, pipe):
+def test_clean_divergence_lexicographic_shapes(ny, nx):
     """The serial lexicographic phi sweep of clean_divergence_fast (v5.py:250-253)
     on ragged shapes: one and several waves per band, a band edge inside a wave,
     a single-row last band (row above and below both from memory), several bands;
-    both iterations pipelined in one launch (pipe, up to 322 rows) or one after
-    the other."""
-    call("cfd_set_clean_divergence_pipeline", pipe)
-    try:
-        rng = np.random.default_rng(ny * 1000 + nx)
-        u0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
-        v0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
-        dx, dy = 20.0 / (nx - 1), 6.0 / (ny - 1)
-        cu, cv = oracle.clean_divergence2d(u0, v0, dx=dx, dy=dy, iterations=2)
-        u, v = dev(u0), dev(v0)
-        K.clean_divergence_fast(u, v, dx, dy, iterations=2)
-        assert np.array_equal(host(u), cu) and np.array_equal(host(v), cv)
-        cu1, cv1 = oracle.clean_divergence2d(u0, v0, dx=dx, dy=dy, iterations=1)
-        u, v = dev(u0), dev(v0)
-        K.clean_divergence_fast(u, v, dx, dy, iterations=1)
-        assert np.array_equal(host(u), cu1) and np.array_equal(host(v), cv1)
-    finally:
-        call("cfd_set_clean_divergence_pipeline", 0)
+    one and two iterations."""
+    rng = np.random.default_rng(ny * 1000 + nx)
+    u0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+    v0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+    dx, dy = 20.0 / (nx - 1), 6.0 / (ny - 1)
+    cu, cv = oracle.clean_divergence2d(u0, v0, dx=dx, dy=dy, iterations=2)
+    u, v = dev(u0), dev(v0)
+    K.clean_divergence_fast(u, v, dx, dy, iterations=2)
+    assert np.array_equal(host(u), cu) and np.array_equal(host(v), cv)
+    cu1, cv1 = oracle.clean_divergence2d(u0, v0, dx=dx, dy=dy, iterations=1)
+    u, v = dev(u0), dev(v0)
+    K.clean_divergence_fast(u, v, dx, dy, iterations=1)
+    assert np.array_equal(host(u), cu1) and np.array_equal(host(v), cv1)
 
 
 def test_bc_ibm_clip_bitexact(golden):
