@@ -42,7 +42,7 @@ def test_library_identifies_itself():
     assert L.cfd_device_arch() == b"gfx950"
     assert L.cfd_rbgs_workspace_bytes(1500) >= 4 * 1500
     # sized for float64 (2 fields) and for the f32 pipelined path (phi, div1, div2, u1, v1)
-    assert L.cfd_clean_divergence_workspace_bytes(180, 600) == max(2 * 8, 5 * 4) * 180 * 600
+    assert L.cfd_clean_divergence_workspace_bytes(180, 600) == 2 * 8 * 180 * 600
 
 
 def test_invalid_arguments_report_errors_without_gpu():
