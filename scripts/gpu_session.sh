@@ -52,6 +52,8 @@ for s in "$@"; do
     pmc_fetch_pred64) step pmc_fetch_pred64 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_pred64 -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 12 --warmup 0 --no-cpu-baseline ;;
     pmc_write_pred64) step pmc_write_pred64 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_pred64 -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 12 --warmup 0 --no-cpu-baseline ;;
     sq_predf) step sq_predf 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES -d gpurun_out/sq_predf -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 12 --warmup 0 --no-cpu-baseline --tau-mode fast ;;
+    pmc_fetch_pred64f) step pmc_fetch_pred64f 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_pred64f -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 12 --warmup 0 --no-cpu-baseline --tau-mode fast ;;
+    pmc_write_pred64f) step pmc_write_pred64f 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_pred64f -o run --output-format csv -- python3 bench.py --workload predictor2d_8192_f64 --steps 12 --warmup 0 --no-cpu-baseline --tau-mode fast ;;
     testspred2) step pytest_pred2 900 python -u -m pytest tests/test_gpu_predictor.py -q -x --timeout 300 --timeout-method thread ;;
     benchpredv1) step benchpredv1 600 env CFD_PRED_VARIANT=1 python bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --no-cpu-baseline ;;
     profpred) step profpred 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profpred -o run --output-format csv -- python3 bench.py --workload predictor2d_8192 --steps 20 --warmup 3 --no-cpu-baseline ;;

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--bytes-per-update", type=float, default=12.0)
     ap.add_argument("--trace", help="run_kernel_trace.csv: keep one mid-run window of the timeline")
     ap.add_argument("--window", type=int, default=10, help="kernels in the --trace window")
+    ap.add_argument("--timeline", action="store_true", help="write the --trace window as <tag>_<workload>_timeline.json")
     ap.add_argument("--skip", type=int, default=0,
                     help="drop the first N launches of the kernel (the cold launches at process start)")
     a = ap.parse_args()
@@ -56,12 +57,27 @@ def main():
         summ = [{"kernel": short(r["Name"]), "calls": int(r["Calls"]),
                  "avg_ms": float(r["AverageNs"]) / 1e6, "total_ms": float(r["TotalDurationNs"]) / 1e6,
                  "pct": float(r["Percentage"])} for r in rows]
+        if a.trace:
+            # steady state: every kernel's launches after its first --skip
+            # (clock warm-up and cold caches at process start inflate the
+            # rocprof average; the bench times its steps after a warm-up)
+            durs = collections.defaultdict(list)
+            for r in sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"])):
+                durs[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+            for e in summ:
+                d = durs.get(e["kernel"], [])[a.skip:]
+                if d:
+                    e["steady_skip_first"] = a.skip
+                    e["steady_calls"] = len(d)
+                    e["steady_avg_ms"] = sum(d) / len(d)
+                    e["steady_median_ms"] = sorted(d)[len(d) // 2]
         p = out_dir / f"{a.tag}_{a.workload}_kernel_stats.json"
         p.write_text(json.dumps(summ, indent=1) + "\n")
         print("wrote", p)
         for s in summ[:6]:
-            print(f"  {s['kernel'][:70]:70s} calls={s['calls']:5d} avg={s['avg_ms']:.4f} ms {s['pct']:.2f}%")
-    if a.trace:
+            print(f"  {s['kernel'][:70]:70s} calls={s['calls']:5d} avg={s['avg_ms']:.4f} ms {s['pct']:.2f}%"
+                  + (f" steady={s['steady_avg_ms']:.4f} ms" if "steady_avg_ms" in s else ""))
+    if a.trace and a.timeline:
         # a slice of the kernel timeline (start offsets, durations, HW queue):
         # shows whether the exchange kernel runs beside the interior launch
         rows = [r for r in csv.DictReader(open(a.trace))
