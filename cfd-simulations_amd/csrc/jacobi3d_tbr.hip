@@ -53,6 +53,18 @@ __device__ inline void sts4(float *p, float4 v) { *reinterpret_cast<float4 *>(p)
 // array); a lane outside the grid passes kOob and reads 0, with no branch.
 typedef float gv4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
+// LDS float pointers (32-bit addresses) for the lane-based addressing of the
+// Jacobi row waves: a float4 at base + compile-time offset is one ds_read_b128
+// / ds_write_b128 with the offset in the instruction's immediate field
+typedef __attribute__((address_space(3))) float lfloat;
+typedef __attribute__((address_space(3))) gv4f lgv4f;
+__device__ inline uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)(const lds_void *)p; }
+__device__ inline lfloat *lds_ptr(uint32_t a) { return (lfloat *)(uintptr_t)a; }
+__device__ inline float4 lds4l(const lfloat *p) {
+    const gv4f v = *(const lgv4f *)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ inline void sts4l(lfloat *p, float4 v) { *(lgv4f *)p = gv4f{v.x, v.y, v.z, v.w}; }
 __device__ inline __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, int p, int nz, size_t plane) {
     const bool in = p >= 0 && p <= nz - 1;
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(in ? base + (size_t)p * plane : base),
@@ -65,6 +77,14 @@ __device__ inline __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, int p, in
 // as well: 2.97 ms at K = 3 -- the neighbouring tiles' halo re-reads then
 // miss L2.)
 constexpr int kStoreNt = 2;
+// lane-based LDS addressing and exact vmcnt waits in the Jacobi row waves
+// (A/B knobs; see the DMA row wave)
+#ifndef CFD_TBR_LB
+#define CFD_TBR_LB 1
+#endif
+#ifndef CFD_TBR_XW
+#define CFD_TBR_XW 1
+#endif
 #ifndef CFD_TBR_EARLY
 #define CFD_TBR_EARLY 1
 #endif
@@ -688,6 +708,30 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             VT V[RPW][3], Rq[RPW][K];
             QQ Q[RPW][K][3];
             float4 Rn[RPW];  // !RDMA: the rhs row of the next step's plane, in flight
+            // Lane-based LDS addressing (Jacobi): every tile and staging access
+            // of a row wave is one of a few per-wave base addresses (the lane's
+            // float4 in the wave's first row; the level tiles past T_1 from a
+            // second base, so offsets fit the 16-bit immediate) plus a
+            // compile-time offset, folded into the DS instruction.  The bases
+            // are made opaque once per step, so the compiler keeps 4 + 2 VGPRs
+            // instead of hoisting one address per (level, row) out of the
+            // z-loop -- which spilled 5 VGPRs at K = 4 whose scratch reloads
+            // each waited vmcnt(0), i.e. for the DMAs of the next planes.
+            constexpr bool LB = MODE == kJacobi && CFD_TBR_LB;
+            constexpr int kTb2 = [] {  // first float of tile T_2 (0 when K < 3)
+                int t = 0;
+                for (int m = 0; m < 2 && m < K; ++m) t += (NR - 2 * m) * RS;
+                return K >= 3 ? t : 0;
+            }();
+            auto tbase = [](int l) {
+                int t = 0;
+                for (int m = 0; m < l; ++m) t += (NR - 2 * m) * RS;
+                return t;
+            };
+            const uint32_t lbA0 = lds_addr(smem) + 4u * (uint32_t)(wv * RS + 4 + 4 * lane);
+            const uint32_t lbU0 = lds_addr(smem) + 4u * (uint32_t)(wv * RS);
+            const uint32_t lbP00 = lds_addr(st_p0) + 4u * (uint32_t)(wv * 256 + 4 * lane);
+            const uint32_t lbP10 = lds_addr(st_p1) + 4u * (uint32_t)(wv * 256 + 4 * lane);
 #pragma unroll
             for (int j = 0; j < RPW; ++j) {
 #pragma unroll
@@ -718,6 +762,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 }
                 wait_vmcnt<0>();
             }
+            // XW (Jacobi): the prologue's loads land before the march, so the
+            // waits the compiler places for them in the loop's first step are
+            // no-ops (it does not count the LDS-DMAs, so a wait of its own for
+            // an older load would wait for this step's DMAs as well)
+            constexpr bool XW = MODE == kJacobi && !EARLY && CFD_TBR_XW;
+            if constexpr (XW) wait_vmcnt<0>();
             // Register queues without moves: plane q of level 0 / level l lives
             // in slot (q - zs) mod 3 of V / Q[.][l], and (when the unroll
             // period 6 is a multiple of K) the rhs of plane q in slot
@@ -746,6 +796,28 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 float *const rw = E ? st_r1 : st_r0;
                 const float *const pr = E ? st_p0 : st_p1;
                 const float *const rdr = E ? st_r0 : st_r1;
+                // LB: this step's opaque bases; tp(l, d): the lane's float4 of
+                // level tile l in row rr[j] + d (d = j * NWR + delta); up(l, d):
+                // that row's first float (uniform)
+                uint32_t bA = lbA0, bU = lbU0, bP = E ? lbP00 : lbP10;
+                if constexpr (LB) asm volatile("" : "+v"(bA), "+v"(bU), "+v"(bP));
+                const uint32_t bB = bA + 4u * kTb2, bUB = bU + 4u * kTb2;
+                auto tp = [&](int l, int d) -> lfloat * {
+                    return l < 2 ? lds_ptr(bA) + (tbase(l) + (1 + d - l) * RS)
+                                 : lds_ptr(bB) + (tbase(l) - kTb2 + (1 + d - l) * RS);
+                };
+                auto up = [&](int l, int d) -> const lfloat * {
+                    return l < 2 ? lds_ptr(bU) + (tbase(l) + (1 + d - l) * RS)
+                                 : lds_ptr(bUB) + (tbase(l) - kTb2 + (1 + d - l) * RS);
+                };
+                (void)tp;
+                (void)up;
+                // !RDMA: this step's rhs row (loaded last step) and the next one's load
+                float4 Rc[RPW];
+                if constexpr (!RDMA && XW) {
+#pragma unroll
+                    for (int j = 0; j < RPW; ++j) Rc[j] = Rn[j];  // landed: see phase R
+                }
                 if constexpr (!EARLY) {
                     const v4i32 rp = plane_rsrc4(a.in, z + 2, nz, plane);
                     const v4i32 rd = plane_rsrc4(a.div, z + 1, nz, plane);
@@ -758,14 +830,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     (void)pw;
                     (void)rw;
                 }
-                // !RDMA: this step's rhs row (loaded last step) and the next one's load
-                float4 Rc[RPW];
                 if constexpr (!RDMA) {
                     (void)rw;
                     (void)rdr;
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
-                        Rc[j] = Rn[j];
+                        if constexpr (!XW) Rc[j] = Rn[j];
                         Rn[j] = ldb4(plane_rsrc(a.div, z + 1, nz, plane), bo[j]);
                     }
                 }
@@ -775,6 +845,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     if (xin) {
                         if constexpr (SPLIT)
                             sts4s(T(0, rr[j]), lane, f4_of(V[j][vs(0)]));
+                        else if constexpr (LB)
+                            sts4l(tp(0, j * NWR), f4_of(V[j][vs(0)]));
                         else
                             sts4(T(0, rr[j]) + 4 + 4 * lane, f4_of(V[j][vs(0)]));
                     }
@@ -799,6 +871,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                     else
                                         sts4(T(l, rr[j]) + 4 + 4 * lane, f);
                                 }
+                            } else if constexpr (LB) {
+                                sts4l(tp(l, j * NWR), f4_of(Q[j][l][ROT ? sl3(R - l) : 2]));
                             } else {
                                 sts4(T(l, rr[j]) + 4 + 4 * lane, f4_of(Q[j][l][ROT ? sl3(R - l) : 2]));
                             }
@@ -813,6 +887,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 // pass) and DMAs, and step z - 1's level-K stores
                 if constexpr (EARLY)
                     wait_vmcnt<2 * kNSK + 2 * kNR + kNSR + kND>();
+                else if constexpr (XW)
+                    // issued after step z - 1's DMAs: its rhs loads, rhs
+                    // stores (first pass), 0..RPW level-K stores, and this
+                    // step's DMAs and rhs loads -- so last step's level-K
+                    // stores may still be in flight
+                    wait_vmcnt<2 * kNR + kNSR + kND>();
                 else
                     wait_vmcnt<((ZERO ? 0 : 1) + 1) * RPW>();
                 trace_mark(a.trace, wv, z - zs, 1);
@@ -822,6 +902,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 for (int j = 0; j < RPW; ++j) {
                     if constexpr (MODE == kRbgs)
                         V[j][vs(1)] = ldsp(pr + (rr[j] - 1) * 256 + 4 * lane);
+                    else if constexpr (LB)
+                        V[j][vs(1)] = toV(ZERO ? z4 : lds4l(lds_ptr(bP) + j * NWR * 256));
                     else
                         V[j][vs(1)] = toV(ZERO ? z4 : lds4(pr + (rr[j] - 1) * 256 + 4 * lane));
                     constexpr int RS0 = ROTR ? slk(R, K) : 0;  // slot of this step's rhs
@@ -897,6 +979,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             o.N = pick2(lds4(T(l - 1, r + 1) + 4 + 4 * lane), h);
                             o.S = pick2(lds4(T(l - 1, r - 1) + 4 + 4 * lane), h);
                         }
+                    } else if constexpr (LB) {
+                        (void)row;
+                        o.wl = up(l - 1, j * NWR)[3];
+                        o.er = up(l - 1, j * NWR)[260];
+                        o.N = lds4l(tp(l - 1, j * NWR + 1));
+                        o.S = lds4l(tp(l - 1, j * NWR - 1));
                     } else {
                         o.wl = row[3];
                         o.er = row[260];
@@ -909,6 +997,21 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 for (int l = 1; l <= K; ++l) {
                     const int p = z - l + 1;
                     const bool fx = fixedp(p);
+                    if (!RDMA && XW && l == K) {
+                        // the next step's rhs rows (loaded at this step's
+                        // start) taken into registers here, as late as
+                        // possible but before this step's level-K stores: the
+                        // compiler's wait for them then counts only the first
+                        // pass's rhs stores after them and nothing it cannot
+                        // see (the LDS-DMAs); a wait counted from the next
+                        // step would also wait for that step's DMAs
+#pragma unroll
+                        for (int j = 0; j < RPW; ++j) {
+                            gv4f r4 = {Rn[j].x, Rn[j].y, Rn[j].z, Rn[j].w};
+                            asm volatile("" : "+v"(r4));
+                            Rn[j] = make_float4(r4.x, r4.y, r4.z, r4.w);
+                        }
+                    }
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
                         const int r = rr[j];
