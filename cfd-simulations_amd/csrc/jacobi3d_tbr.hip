@@ -85,6 +85,9 @@ constexpr int kStoreNt = 2;
 #ifndef CFD_TBR_XW
 #define CFD_TBR_XW 1
 #endif
+#ifndef CFD_TBR_T0S  // level-0 tile = the DMA staging slot (Jacobi; see jacobi3d_tbr)
+#define CFD_TBR_T0S 1
+#endif
 #ifndef CFD_TBR_EARLY
 #define CFD_TBR_EARLY 1
 #endif
@@ -346,15 +349,19 @@ __device__ inline v2f_t level2(v2f_t C, v2f_t O, float wl, float er, v2f_t N, v2
 // The halo wave of jacobi3d_tbr (see there): loads the two outermost level-0
 // rows and the 4-float x-halo chunks of every row, and computes levels
 // 1..K-1 of the chunks, in lock step (two barriers per step) with the row waves.
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT, bool PT>
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT, bool PT, bool T0S = false>
 __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int z0, int z1, int y0, int xs,
-                                              int zl) {
+                                              int zl, float *slots = nullptr) {
     constexpr int NR = NWR * RPW + 2;
     constexpr int RS = 264, RS2 = kPairRow;
+    // T0S: level 0 of plane z is slot (z - zs) mod 3 of `slots` (the row
+    // waves' LDS-DMA staging ring), the level tiles 1..K-1 start at smem
+    int t0 = 0;  // this step's slot offset (floats)
     auto T = [&](int l, int r) -> float * {
+        if (T0S && l == 0) return slots + t0 + r * RS;
         int base = 0;
 #pragma unroll
-        for (int m = 0; m < K; ++m)
+        for (int m = T0S ? 1 : 0; m < K; ++m)
             if (m < l) base += (NR - 2 * m) * (PT && m ? RS2 : RS);
         return smem + base + (r - l) * (PT && l ? RS2 : RS);
     };
@@ -408,6 +415,7 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
     }
     const int hw = threadIdx.x >> 6;
     for (int z = zs; z <= zl; ++z) {
+        if constexpr (T0S) t0 = ((z - zs) % 3) * (NR * RS);
         trace_mark(a.trace, hw, z - zs, 0);
         Lq[PD - 1] = ldlo(z + PD);
         Uq[PD - 1] = ldhi(z + PD);
@@ -494,10 +502,10 @@ __device__ __forceinline__ void tbr_halo_wave(const TbrArgs a, float *smem, int 
 // The halo wave as a called function (K <= 3: measured 1.5-2.5 % faster than
 // inlined there); K = 4 inlines it (as a call it takes the TbrArgs by value in
 // VGPRs and a call frame: 168-181 VGPRs, which spill).
-template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT, bool PT>
+template <int K, int NWR, int RPW, bool PRE, int PD, int MODE, int F, bool SPLIT, bool PT, bool T0S>
 __device__ __noinline__ void tbr_halo_wave_call(const TbrArgs a, float *smem, int z0, int z1, int y0,
-                                                int xs, int zl) {
-    tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F, SPLIT, PT>(a, smem, z0, z1, y0, xs, zl);
+                                                int xs, int zl, float *slots) {
+    tbr_halo_wave<K, NWR, RPW, PRE, PD, MODE, F, SPLIT, PT, T0S>(a, smem, z0, z1, y0, xs, zl, slots);
 }
 
 // (A double-buffered, one-barrier-per-step version of the (3, 11, 2) shape --
@@ -524,12 +532,22 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // come by LDS-DMA too at 4 levels
     constexpr bool PT = MODE == kRbgs && PD == 1 && K == 4;  // (at 3 levels: 16 VGPRs spill)
     constexpr int RS2 = kPairRow;
+    // T0S (Jacobi, LDS-DMA path): the level-0 tile of plane z IS the DMA
+    // staging slot that plane landed in -- a ring of 3 full tiles (planes z,
+    // z + 1 landed, z + 2 in flight), the rows DMA'd straight to their tile
+    // position and the halo wave adding the outer rows and x-halo chunks -- so
+    // phase W no longer copies level 0 into a tile: a quarter of the K = 4
+    // pass's LDS stores, the slow direction of the LDS (ds_write_b128 ~79
+    // B/clk/CU against 256 for reads)
+    constexpr bool T0S = MODE == kJacobi && PD == 1 && CFD_TBR_LB && CFD_TBR_T0S;
+    constexpr int SLOT = NR * RS;
     constexpr int TOTAL = [] {
         int t = 0;
-        for (int l = 0; l < K; ++l) t += (NR - 2 * l) * (PT && l ? RS2 : RS);
+        for (int l = T0S ? 1 : 0; l < K; ++l) t += (NR - 2 * l) * (PT && l ? RS2 : RS);
         return t;
     }();
-    __shared__ __attribute__((aligned(16))) float smem[TOTAL];
+    __shared__ __attribute__((aligned(16))) float smem[TOTAL > 0 ? TOTAL : 4];
+    __shared__ __attribute__((aligned(16))) float slots[T0S ? 3 * SLOT : 4];
     // DMA staging (row waves, when it fits in LDS with the level tiles): the
     // level-0 row of plane z + 2 and the rhs row of plane z + 1 are fetched by
     // LDS-DMA at the start of step z into the even/odd buffers and read at
@@ -540,8 +558,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // DMA: the phi rows by LDS-DMA; RDMA: the rhs rows too when both staging
     // pairs fit beside the level tiles, else the rhs row of plane z + 1 is a
     // register load issued a step ahead (4 VGPRs per row)
-    constexpr bool DMA = PD == 1 && (TOTAL + 2 * SR_ * 256) * 4 <= 160 * 1024;
-    constexpr bool RDMA = DMA && (TOTAL + 4 * SR_ * 256) * 4 <= 160 * 1024;
+    constexpr int STG = T0S ? 3 * SLOT : 2 * SR_ * 256;  // the phi staging floats
+    constexpr bool DMA = PD == 1 && (TOTAL + STG) * 4 <= 160 * 1024;
+    constexpr bool RDMA = DMA && (TOTAL + STG + 2 * SR_ * 256) * 4 <= 160 * 1024;
+    static_assert(!T0S || DMA, "T0S: the LDS-DMA path");
     // GS level-0 tile by colour pair (sts4s; at 3 levels every tile): +1.2 %
     // at K = 3
     constexpr bool SPLIT = MODE == kRbgs && DMA;
@@ -549,14 +569,14 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // in phase R right after the wave read its rows of the same buffer,
     // instead of one step ahead at the start of phase W
     constexpr bool EARLY = DMA && MODE == kRbgs && CFD_TBR_EARLY;
-    constexpr int SST = DMA ? SR_ * 256 : 4;
+    constexpr int SST = DMA && !T0S ? SR_ * 256 : 4;
     constexpr int SSR = RDMA ? SR_ * 256 : 4;
     __shared__ __attribute__((aligned(16))) float st_p0[SST], st_p1[SST], st_r0[SSR], st_r1[SSR];
-    // level l keeps rows [l, NR - l)
+    // level l keeps rows [l, NR - l) (T0S: l >= 1 only; level 0 is a slot)
     auto T = [&](int l, int r) -> float * {
         int base = 0;
 #pragma unroll
-        for (int m = 0; m < K; ++m)
+        for (int m = T0S ? 1 : 0; m < K; ++m)
             if (m < l) base += (NR - 2 * m) * (PT && m ? RS2 : RS);
         return smem + base + (r - l) * (PT && l ? RS2 : RS);
     };
@@ -669,6 +689,11 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         if constexpr (MODE == kRbgs) chgl[slot(l)] = fmaxf(chgl[slot(l)], lm);
     };
 
+    if constexpr (T0S && ZERO) {
+        // level 0 = 0 (no DMA fills the slots): zero them once
+        for (int k = threadIdx.x; k < 3 * SLOT / 4; k += blockDim.x) sts4(slots + 4 * k, z4);
+        __syncthreads();
+    }
     if (wv < NWR) {
         if constexpr (DMA) {
             // --------------------------------------------- row wave, DMA-staged
@@ -718,20 +743,26 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             // z-loop -- which spilled 5 VGPRs at K = 4 whose scratch reloads
             // each waited vmcnt(0), i.e. for the DMAs of the next planes.
             constexpr bool LB = MODE == kJacobi && CFD_TBR_LB;
+            // (T0S: tiles 1..K-1 all within the 16-bit offset of one base)
             constexpr int kTb2 = [] {  // first float of tile T_2 (0 when K < 3)
                 int t = 0;
                 for (int m = 0; m < 2 && m < K; ++m) t += (NR - 2 * m) * RS;
-                return K >= 3 ? t : 0;
+                return K >= 3 && !T0S ? t : 0;
             }();
             auto tbase = [](int l) {
                 int t = 0;
-                for (int m = 0; m < l; ++m) t += (NR - 2 * m) * RS;
+                for (int m = T0S ? 1 : 0; m < l; ++m) t += (NR - 2 * m) * RS;
                 return t;
             };
             const uint32_t lbA0 = lds_addr(smem) + 4u * (uint32_t)(wv * RS + 4 + 4 * lane);
             const uint32_t lbU0 = lds_addr(smem) + 4u * (uint32_t)(wv * RS);
             const uint32_t lbP00 = lds_addr(st_p0) + 4u * (uint32_t)(wv * 256 + 4 * lane);
             const uint32_t lbP10 = lds_addr(st_p1) + 4u * (uint32_t)(wv * 256 + 4 * lane);
+            // T0S: the lane's float4 in row wv of slot 0, and row wv's first float
+            const uint32_t lbS0 = lds_addr(slots) + 4u * (uint32_t)(wv * RS + 4 + 4 * lane);
+            const uint32_t lbUS0 = lds_addr(slots) + 4u * (uint32_t)(wv * RS);
+            // a row's DMA destination in slot q: row rr[j], column 4
+            auto slot_row = [&](int q, int j) { return slots + q * SLOT + rr[j] * RS + 4; };
 #pragma unroll
             for (int j = 0; j < RPW; ++j) {
 #pragma unroll
@@ -746,7 +777,15 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
 #pragma unroll
                 for (int i = 0; i < K; ++i) Rq[j][i] = toV(z4);
                 // read at step zs (even): plane zs + 1 and rhs zs in the odd buffers
-                if (!ZERO) dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], st_p1 + (rr[j] - 1) * 256);
+                // (T0S: planes zs and zs + 1 into slots 0 and 1)
+                if constexpr (T0S) {
+                    if (!ZERO) {
+                        dma_row(plane_rsrc4(a.in, zs, nz, plane), bo[j], slot_row(0, j));
+                        dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], slot_row(1, j));
+                    }
+                } else if (!ZERO) {
+                    dma_row(plane_rsrc4(a.in, zs + 1, nz, plane), bo[j], st_p1 + (rr[j] - 1) * 256);
+                }
                 if constexpr (RDMA)
                     dma_row(plane_rsrc4(a.div, zs, nz, plane), bo[j], st_r1 + (rr[j] - 1) * 256);
                 else
@@ -799,17 +838,29 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 // LB: this step's opaque bases; tp(l, d): the lane's float4 of
                 // level tile l in row rr[j] + d (d = j * NWR + delta); up(l, d):
                 // that row's first float (uniform)
+                // T0S: slot sz holds plane z (this step's level 0), sn plane
+                // z + 1 (landed), sd receives plane z + 2
+                const int sz = T0S ? (z - zs) % 3 : 0;
+                const int sn = sz == 2 ? 0 : sz + 1, sd = sn == 2 ? 0 : sn + 1;
                 uint32_t bA = lbA0, bU = lbU0, bP = E ? lbP00 : lbP10;
-                if constexpr (LB) asm volatile("" : "+v"(bA), "+v"(bU), "+v"(bP));
+                uint32_t bS = lbS0 + 4u * (uint32_t)(sz * SLOT), bSn = lbS0 + 4u * (uint32_t)(sn * SLOT);
+                uint32_t bUS = lbUS0 + 4u * (uint32_t)(sz * SLOT);
+                if constexpr (LB && T0S)
+                    asm volatile("" : "+v"(bA), "+v"(bU), "+v"(bS), "+v"(bSn), "+v"(bUS));
+                else if constexpr (LB)
+                    asm volatile("" : "+v"(bA), "+v"(bU), "+v"(bP));
                 const uint32_t bB = bA + 4u * kTb2, bUB = bU + 4u * kTb2;
                 auto tp = [&](int l, int d) -> lfloat * {
+                    if (T0S && l == 0) return lds_ptr(bS) + (1 + d) * RS;
                     return l < 2 ? lds_ptr(bA) + (tbase(l) + (1 + d - l) * RS)
                                  : lds_ptr(bB) + (tbase(l) - kTb2 + (1 + d - l) * RS);
                 };
                 auto up = [&](int l, int d) -> const lfloat * {
+                    if (T0S && l == 0) return lds_ptr(bUS) + (1 + d) * RS;
                     return l < 2 ? lds_ptr(bU) + (tbase(l) + (1 + d - l) * RS)
                                  : lds_ptr(bUB) + (tbase(l) - kTb2 + (1 + d - l) * RS);
                 };
+                (void)sd;
                 (void)tp;
                 (void)up;
                 // !RDMA: this step's rhs row (loaded last step) and the next one's load
@@ -823,7 +874,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     const v4i32 rd = plane_rsrc4(a.div, z + 1, nz, plane);
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
-                        if (!ZERO) dma_row(rp, bo[j], pw + (rr[j] - 1) * 256);
+                        if (!ZERO) dma_row(rp, bo[j], T0S ? slot_row(sd, j) : pw + (rr[j] - 1) * 256);
                         if constexpr (RDMA) dma_row(rd, bo[j], rw + (rr[j] - 1) * 256);
                     }
                 } else {
@@ -842,7 +893,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 // phase W: level 0 of plane z and level l of plane z - l
 #pragma unroll
                 for (int j = 0; j < RPW; ++j) {
-                    if (xin) {
+                    if (xin && !T0S) {  // (T0S: level 0 is in its slot already)
                         if constexpr (SPLIT)
                             sts4s(T(0, rr[j]), lane, f4_of(V[j][vs(0)]));
                         else if constexpr (LB)
@@ -902,6 +953,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 for (int j = 0; j < RPW; ++j) {
                     if constexpr (MODE == kRbgs)
                         V[j][vs(1)] = ldsp(pr + (rr[j] - 1) * 256 + 4 * lane);
+                    else if constexpr (LB && T0S)
+                        V[j][vs(1)] = toV(ZERO ? z4 : lds4l(lds_ptr(bSn) + (1 + j * NWR) * RS));
                     else if constexpr (LB)
                         V[j][vs(1)] = toV(ZERO ? z4 : lds4l(lds_ptr(bP) + j * NWR * 256));
                     else
@@ -1270,9 +1323,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
         // which then spills a VGPR)
         constexpr int HPD = DMA && K == 4 ? 2 : PD;
         if constexpr (K == 4)
-            tbr_halo_wave<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT, PT>(a, smem, z0, z1, y0, xs, zl);
+            tbr_halo_wave<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT, PT, T0S>(a, smem, z0, z1, y0, xs, zl, slots);
         else
-            tbr_halo_wave_call<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT, PT>(a, smem, z0, z1, y0, xs, zl);
+            tbr_halo_wave_call<K, NWR, RPW, PRE, HPD, MODE, F, SPLIT, PT, T0S>(a, smem, z0, z1, y0, xs, zl, slots);
     }
     if (MODE == kRbgs && a.maxc) {
         // level l is iteration (h0 >> 1) + q(l), q(l) = ((h0 & 1) + l - 1) >> 1
