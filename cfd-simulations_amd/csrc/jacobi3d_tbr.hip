@@ -85,6 +85,9 @@ constexpr int kStoreNt = 2;
 #ifndef CFD_TBR_XW
 #define CFD_TBR_XW 1
 #endif
+#ifndef CFD_TBR_SD  // per-step scalar state by additions (Jacobi row waves; see the DMA row wave)
+#define CFD_TBR_SD 1
+#endif
 #ifndef CFD_TBR_T0S  // level-0 tile = the DMA staging slot (Jacobi; see jacobi3d_tbr)
 #define CFD_TBR_T0S 1
 #endif
@@ -819,6 +822,37 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             constexpr int kND = ((ZERO ? 0 : 1) + (RDMA ? 1 : 0)) * RPW, kNR = RDMA ? 0 : RPW, kNSK = RPW,
                           kNSR = RHSW ? RPW : 0;
             static_assert(2 * kNSK + 2 * kNR + kNSR + kND < 64, "vmcnt range");
+            // SD (Jacobi, XW): the per-step scalar state -- the plane bases of
+            // the DMA source (in, plane z + 2), the rhs loads (div, z + 1), the
+            // level-K stores (out, z - K + 1) and the first pass's rhs stores
+            // (rhs_out, z), and the slot ring's byte offsets -- carried from
+            // step to step by additions and rotations.  Recomputed per step
+            // they were ~80 SALU per wave in phase W (64-bit products, a
+            // division by 3), and the CU's one scalar unit serialised the 12
+            // waves' phase W (r05 trace: the third wave of each SIMD reached
+            // the first barrier ~1150 cycles after the first)
+            constexpr bool SD = XW && CFD_TBR_SD;
+            const uint64_t pbytes = (uint64_t)plane * sizeof(float);
+            uint64_t sd_in = (uint64_t)(uintptr_t)a.in + (uint64_t)(int64_t)(zs + 2) * pbytes;
+            uint64_t sd_div = (uint64_t)(uintptr_t)a.div + (uint64_t)(int64_t)(zs + 1) * pbytes;
+            uint64_t sd_out = (uint64_t)(uintptr_t)a.out + (uint64_t)(int64_t)(zs - K + 1) * pbytes;
+            uint64_t sd_rhs = (uint64_t)(uintptr_t)a.rhs_out + (uint64_t)(int64_t)zs * pbytes;
+            int sd_oz = 0, sd_on = 4 * SLOT, sd_od = 8 * SLOT;  // slot byte offsets: planes z, z + 1, z + 2
+            // a raw buffer resource over one plane at byte address b (empty unless ok)
+            auto rsrc4 = [&](uint64_t b, bool ok) {
+                v4i32 r;
+                r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+                r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(b >> 32) & 0xffffu));
+                r.z = __builtin_amdgcn_readfirstlane(ok ? (int)pbytes : 0);
+                r.w = 0x00020000;
+                return r;
+            };
+            auto rsrc = [&](uint64_t b, bool ok) {
+                return __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)b, (short)0, ok ? (int)pbytes : 0,
+                                                         0x00020000);
+            };
+            (void)rsrc4;
+            (void)rsrc;
             auto step = [&](int z, auto parc, auto rotc, auto bpc) {
                 constexpr int E = decltype(parc)::value;  // (z - zs) & 1
                 constexpr int R = decltype(rotc)::value;  // (z - zs) mod 6 (ROT), else 0
@@ -840,11 +874,15 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 // that row's first float (uniform)
                 // T0S: slot sz holds plane z (this step's level 0), sn plane
                 // z + 1 (landed), sd receives plane z + 2
-                const int sz = T0S ? (z - zs) % 3 : 0;
+                const int sz = T0S && !SD ? (z - zs) % 3 : 0;
                 const int sn = sz == 2 ? 0 : sz + 1, sd = sn == 2 ? 0 : sn + 1;
+                // byte offsets of the slots of planes z, z + 1, z + 2
+                const uint32_t oz = SD ? (uint32_t)sd_oz : 4u * (uint32_t)(sz * SLOT);
+                const uint32_t on = SD ? (uint32_t)sd_on : 4u * (uint32_t)(sn * SLOT);
+                const uint32_t od = SD ? (uint32_t)sd_od : 4u * (uint32_t)(sd * SLOT);
                 uint32_t bA = lbA0, bU = lbU0, bP = E ? lbP00 : lbP10;
-                uint32_t bS = lbS0 + 4u * (uint32_t)(sz * SLOT), bSn = lbS0 + 4u * (uint32_t)(sn * SLOT);
-                uint32_t bUS = lbUS0 + 4u * (uint32_t)(sz * SLOT);
+                uint32_t bS = lbS0 + oz, bSn = lbS0 + on;
+                uint32_t bUS = lbUS0 + oz;
                 if constexpr (LB && T0S)
                     asm volatile("" : "+v"(bA), "+v"(bU), "+v"(bS), "+v"(bSn), "+v"(bUS));
                 else if constexpr (LB)
@@ -870,11 +908,14 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     for (int j = 0; j < RPW; ++j) Rc[j] = Rn[j];  // landed: see phase R
                 }
                 if constexpr (!EARLY) {
-                    const v4i32 rp = plane_rsrc4(a.in, z + 2, nz, plane);
-                    const v4i32 rd = plane_rsrc4(a.div, z + 1, nz, plane);
+                    const v4i32 rp = SD ? rsrc4(sd_in, z + 2 >= 0 && z + 2 <= nz - 1) : plane_rsrc4(a.in, z + 2, nz, plane);
+                    const v4i32 rd = SD ? rsrc4(sd_div, z + 1 >= 0 && z + 1 <= nz - 1) : plane_rsrc4(a.div, z + 1, nz, plane);
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
-                        if (!ZERO) dma_row(rp, bo[j], T0S ? slot_row(sd, j) : pw + (rr[j] - 1) * 256);
+                        if (!ZERO)
+                            dma_row(rp, bo[j],
+                                    T0S ? (SD ? (float *)((char *)slots + od) + rr[j] * RS + 4 : slot_row(sd, j))
+                                        : pw + (rr[j] - 1) * 256);
                         if constexpr (RDMA) dma_row(rd, bo[j], rw + (rr[j] - 1) * 256);
                     }
                 } else {
@@ -884,10 +925,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 if constexpr (!RDMA) {
                     (void)rw;
                     (void)rdr;
+                    const __amdgpu_buffer_rsrc_t rdn =
+                        SD ? rsrc(sd_div, z + 1 >= 0 && z + 1 <= nz - 1) : plane_rsrc(a.div, z + 1, nz, plane);
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
                         if constexpr (!XW) Rc[j] = Rn[j];
-                        Rn[j] = ldb4(plane_rsrc(a.div, z + 1, nz, plane), bo[j]);
+                        Rn[j] = ldb4(rdn, bo[j]);
                     }
                 }
                 // phase W: level 0 of plane z and level l of plane z - l
@@ -979,9 +1022,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                         // the rhs of plane z for the later passes: owned planes and
                         // rows only (so[j] = kOob elsewhere), every x of the row
                         const bool own = z >= z0 && z < z1;
-                        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-                            a.rhs_out + (size_t)(own ? z : 0) * plane, (short)0,
-                            own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
+                        const __amdgpu_buffer_rsrc_t ro =
+                            SD ? rsrc(sd_rhs, own)
+                               : __builtin_amdgcn_make_buffer_rsrc(a.rhs_out + (size_t)(own ? z : 0) * plane, (short)0,
+                                                                   own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
                         const float4 rq = f4_of(Rq[j][RS0]);
                         const gv4f rv = {rq.x, rq.y, rq.z, rq.w};
                         __builtin_amdgcn_raw_buffer_store_b128(rv, ro, (int)so[j], 0, kStoreNt);
@@ -1138,9 +1182,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 // unconditional buffer store: rows, lanes and planes this
                                 // tile does not own fall out of range and are dropped
                                 const bool own = p >= z0 && p < z1;
-                                const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-                                    a.out + (size_t)(own ? p : 0) * plane, (short)0,
-                                    own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
+                                const __amdgpu_buffer_rsrc_t ro =
+                                    SD ? rsrc(sd_out, own)
+                                       : __builtin_amdgcn_make_buffer_rsrc(a.out + (size_t)(own ? p : 0) * plane,
+                                                                           (short)0,
+                                                                           own ? (int)(plane * sizeof(float)) : 0,
+                                                                           0x00020000);
                                 const gv4f vv = {v.x, v.y, v.z, v.w};
                                 __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, kStoreNt);
                             }
@@ -1162,6 +1209,16 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 trace_mark(a.trace, wv, z - zs, 3);
                 lds_barrier();
                 trace_mark(a.trace, wv, z - zs, 4);
+                if constexpr (SD) {
+                    sd_in += pbytes;
+                    sd_div += pbytes;
+                    sd_out += pbytes;
+                    sd_rhs += pbytes;
+                    const int t_ = sd_oz;
+                    sd_oz = sd_on;
+                    sd_on = sd_od;
+                    sd_od = t_;
+                }
                 if constexpr (!ROT) {
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
