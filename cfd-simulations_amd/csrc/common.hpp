@@ -200,6 +200,18 @@ __device__ inline v4i32 buf_rsrc4(const void *base, uint32_t bytes) {
     r.w = 0x00020000;
     return r;
 }
+// (the same by LDS byte address)
+__device__ inline void dma_row_at(v4i32 rs, uint32_t byte_ofs, uint32_t la) {
+    int saved;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "s"(__builtin_amdgcn_readfirstlane(la)), "v"(byte_ofs), "s"(rs)
+        : "memory");
+}
 __device__ inline void dma_row(v4i32 rs, uint32_t byte_ofs, void *lds_row) {
     const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lds_row;
     int saved;

@@ -838,6 +838,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             uint64_t sd_out = (uint64_t)(uintptr_t)a.out + (uint64_t)(int64_t)(zs - K + 1) * pbytes;
             uint64_t sd_rhs = (uint64_t)(uintptr_t)a.rhs_out + (uint64_t)(int64_t)zs * pbytes;
             int sd_oz = 0, sd_on = 4 * SLOT, sd_od = 8 * SLOT;  // slot byte offsets: planes z, z + 1, z + 2
+            // the launch's fixed (Dirichlet) planes, or a plane no step reaches
+            const int sd_flo = a.fixed_lo ? a.zb - 1 : -(1 << 30), sd_fhi = a.fixed_hi ? a.ze : -(1 << 30);
             // a raw buffer resource over one plane at byte address b (empty unless ok)
             auto rsrc4 = [&](uint64_t b, bool ok) {
                 v4i32 r;
@@ -1093,7 +1095,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
 #pragma unroll
                 for (int l = 1; l <= K; ++l) {
                     const int p = z - l + 1;
-                    const bool fx = fixedp(p);
+                    // (SD: two compares against the fixed planes found once per launch)
+                    const bool fx = SD ? ((p == sd_flo) | (p == sd_fhi)) : fixedp(p);
                     if (!RDMA && XW && l == K) {
                         // the next step's rhs rows (loaded at this step's
                         // start) taken into registers here, as late as
