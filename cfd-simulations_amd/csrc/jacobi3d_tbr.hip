@@ -831,10 +831,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             // division by 3), and the CU's one scalar unit serialised the 12
             // waves' phase W (r05 trace: the third wave of each SIMD reached
             // the first barrier ~1150 cycles after the first)
-            constexpr bool SD = XW && CFD_TBR_SD;
+            // (the red-black GS's EARLY path too: its DMAs fetch planes z + 3 / rhs z + 2)
+            constexpr bool SD = (XW || EARLY) && CFD_TBR_SD;
+            constexpr int kAh = EARLY ? 3 : 2;  // plane of the step's phi DMA, relative to z
             const uint64_t pbytes = (uint64_t)plane * sizeof(float);
-            uint64_t sd_in = (uint64_t)(uintptr_t)a.in + (uint64_t)(int64_t)(zs + 2) * pbytes;
-            uint64_t sd_div = (uint64_t)(uintptr_t)a.div + (uint64_t)(int64_t)(zs + 1) * pbytes;
+            uint64_t sd_in = (uint64_t)(uintptr_t)a.in + (uint64_t)(int64_t)(zs + kAh) * pbytes;
+            uint64_t sd_div = (uint64_t)(uintptr_t)a.div + (uint64_t)(int64_t)(zs + kAh - 1) * pbytes;
             uint64_t sd_out = (uint64_t)(uintptr_t)a.out + (uint64_t)(int64_t)(zs - K + 1) * pbytes;
             uint64_t sd_rhs = (uint64_t)(uintptr_t)a.rhs_out + (uint64_t)(int64_t)zs * pbytes;
             int sd_oz = 0, sd_on = 4 * SLOT, sd_od = 8 * SLOT;  // slot byte offsets: planes z, z + 1, z + 2
@@ -928,7 +930,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     (void)rw;
                     (void)rdr;
                     const __amdgpu_buffer_rsrc_t rdn =
-                        SD ? rsrc(sd_div, z + 1 >= 0 && z + 1 <= nz - 1) : plane_rsrc(a.div, z + 1, nz, plane);
+                        SD ? rsrc(sd_div - (EARLY ? pbytes : 0), z + 1 >= 0 && z + 1 <= nz - 1)  // (sd_div: rhs z + kAh - 1)
+                           : plane_rsrc(a.div, z + 1, nz, plane);
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
                         if constexpr (!XW) Rc[j] = Rn[j];
@@ -1038,8 +1041,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     // reads are done, fetch step z + 2's rows into them (plane
                     // z + 3, rhs z + 2), two steps ahead and off phase W
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    const v4i32 rp = plane_rsrc4(a.in, z + 3, nz, plane);
-                    const v4i32 rd = plane_rsrc4(a.div, z + 2, nz, plane);
+                    const v4i32 rp = SD ? rsrc4(sd_in, z + 3 >= 0 && z + 3 <= nz - 1) : plane_rsrc4(a.in, z + 3, nz, plane);
+                    const v4i32 rd = SD ? rsrc4(sd_div, z + 2 >= 0 && z + 2 <= nz - 1) : plane_rsrc4(a.div, z + 2, nz, plane);
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
                         if (!ZERO) dma_row(rp, bo[j], const_cast<float *>(pr) + (rr[j] - 1) * 256);
@@ -1149,9 +1152,12 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                                 // level K of plane p: this pair at h, level K - 1's at 1 - h
                                 const float4 f = join2(v, Op, h);
                                 const bool own = p >= z0 && p < z1;
-                                const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-                                    a.out + (size_t)(own ? p : 0) * plane, (short)0,
-                                    own ? (int)(plane * sizeof(float)) : 0, 0x00020000);
+                                const __amdgpu_buffer_rsrc_t ro =
+                                    SD ? rsrc(sd_out, own)
+                                       : __builtin_amdgcn_make_buffer_rsrc(a.out + (size_t)(own ? p : 0) * plane,
+                                                                           (short)0,
+                                                                           own ? (int)(plane * sizeof(float)) : 0,
+                                                                           0x00020000);
                                 const gv4f vv = {f.x, f.y, f.z, f.w};
                                 __builtin_amdgcn_raw_buffer_store_b128(vv, ro, (int)so[j], 0, kStoreNt);
                             }
