@@ -486,11 +486,12 @@ def main():
     elif len(shape) == 3:
         nz, ny, nx = shape
         h = 1.0 / (nx - 1)
-        # slab ghosts: as deep as the sweeps per pass, at most 3 -- at R = 8 the
-        # 3-sweep slab pass beats the 4-sweep one (per-rank rehearsal, r03:
-        # 22.5 vs 23.5 ms per 200-sweep solve; equal at R = 2)
+        # slab ghosts: as deep as the sweeps per pass (r05 per-rank rehearsal at
+        # R = 8: 4-deep ghosts / 4 sweeps per slab pass 20.0 ms per 200-sweep
+        # solve against 23.0 with 3-deep ones; r03, before the r05 tall-tile
+        # work, 3-deep ones had been the faster)
         levels = int(lib().cfd_get_jacobi3d_levels())
-        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else (min(levels, 3) if world > 1 else levels))
+        plan = S.SlabPlan(nz, world, rank, ghost=1 if ARGS.tb == 1 else levels)
         if not use_slab:
             div = torch.randn(shape, generator=g, device=dev, dtype=torch.float32)
             phi = torch.zeros_like(div)
