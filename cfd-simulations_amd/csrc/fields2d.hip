@@ -625,6 +625,211 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
     }
 }
 
+// The sweep on a SKEWED copy of phi and div (r05, the default): the staged
+// kernels below keep phi row-major, so the diagonal a wave touches per step
+// (lane l: row r0 + l, column d - l) is 64 cache lines, and a CU's vector
+// memory path moves about one line per clock -- measured 90-100 us per
+// 600-column sweep, several times the ~47-cycle dependent chain per step
+// (scripts/chain_probe.hip).  clean_divergence owns its phi and div (the
+// workspace), so it stores them diagonal-major instead:
+//   rows in blocks of 64 (block m: rows 1 + 64 m + l, l < 64); within a
+//   block, diagonal d = j + l in groups of four:
+//     (m, d, l) -> ((m DG + d / 4) 64 + l) 4 + d % 4,   DG = ceil((nx + 63) / 4)
+// so a wave's four consecutive steps of one field -- lane l's slots d .. d + 3
+// -- are one coalesced 1-KB dwordx4.  The grid-wide kernels pay the scatter
+// instead (k_divergence_skew writes div there, k_sub_gradient_skew reads phi
+// there), spread over every CU.
+// Per wave (one 64-row block, one lane per row, up to 4 waves per band), at
+// step d lane l updates column j = d - l:
+//  * E (old phi of its row at j + 1) is slot d + 1 of its own row;
+//  * N (old phi of row r + 1 at j) is lane l + 1's E of the same step (DPP);
+//    lane 63's is the next block's lane 0 at slot d - 63;
+//  * S (new phi of row r - 1 at j) is lane l - 1's previous result (DPP);
+//    lane 0's is the wave above's last lane, published per 16 steps into an
+//    LDS row with a counter, or for a band's first wave the block above's
+//    lane 63 at slot d + 63 (final: the band before);
+//  * the operands stream kSkewRing groups of four steps ahead in registers
+//    (the two rows from other blocks by lanes 63 and 0 alone); results leave
+//    four steps at a time (0 at the zero side columns and the padding).
+// Same arithmetic and order as the serial loop: bit-identical.
+constexpr int kSkewWaves = 4;  // waves per band: at one wave per SIMD the chain, not the memory path, sets the pace
+constexpr int kSkewRing = 8;   // groups of 4 steps in flight per wave (and per loop iteration)
+__host__ __device__ inline int lex_skew_blocks(int ny) { return (ny - 2 + 63) >> 6; }
+__host__ __device__ inline int lex_skew_groups(int nx) { return (nx + 63 + 3) >> 2; }
+size_t lex_skew_floats(int ny, int nx) { return (size_t)lex_skew_blocks(ny) * (size_t)lex_skew_groups(nx) * 256; }
+// floats per wave row of k_lex_gs_skew's LDS: column c at c + 64 for
+// c = -63 .. nx + 76, 16 B aligned
+constexpr int lex_skew_rsl(int nx) { return (nx + 160 + 3) & ~3; }
+size_t lex_skew_lds_bytes(int nw, int nx) { return (size_t)nw * lex_skew_rsl(nx) * sizeof(float); }
+bool lex_skew_on() {
+    static const bool on = !getenv("CFD_LEX_STAGED");  // A/B knob: the round-4 staged sweeps
+    return on;
+}
+__device__ inline size_t skew_at(int i, int j, int dg) {  // interior row i >= 1, column j >= 0
+    const int m = (i - 1) >> 6, l = (i - 1) & 63, d = j + l;
+    return (((size_t)m * dg + (d >> 2)) * 64 + l) * 4 + (d & 3);
+}
+
+// compute_divergence_fast (v5.py:178-187) into the skewed layout: interior
+// rows, every column (0 at the side columns, as k_divergence).
+__global__ __launch_bounds__(256) void k_divergence_skew(const float *__restrict__ u, const float *__restrict__ v,
+                                                         float *__restrict__ div_s, int ny, int nx, float cx, float cy) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y + 1;
+    if (j >= nx) return;
+    const size_t c = (size_t)i * nx + j;
+    float d = 0.0f;
+    if (j >= 1 && j <= nx - 2) d = (u[c + 1] - u[c - 1]) * cx + (v[c + nx] - v[c - nx]) * cy;
+    div_s[skew_at(i, j, lex_skew_groups(nx))] = d;
+}
+
+// u -= dphi/dx, v -= dphi/dy (v5.py:255-256) with phi in the skewed layout
+// (rows 0 and ny - 1 are the zero boundary).
+__global__ void k_sub_gradient_skew(const float *__restrict__ phi_s, float *__restrict__ u, float *__restrict__ v,
+                                    int ny, int nx, float cx, float cy) {
+    CFD_2D_INDEX
+    if (!interior(i, j, ny, nx)) return;
+    const int dg = lex_skew_groups(nx);
+    const float pe = phi_s[skew_at(i, j + 1, dg)], pw = phi_s[skew_at(i, j - 1, dg)];
+    const float pn = i + 1 <= ny - 2 ? phi_s[skew_at(i + 1, j, dg)] : 0.0f;
+    const float ps = i - 1 >= 1 ? phi_s[skew_at(i - 1, j, dg)] : 0.0f;
+    const float a = (pe - pw) * cx;
+    const float b = (pn - ps) * cy;
+    u[c] = u[c] - a;
+    v[c] = v[c] - b;
+}
+
+__global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_s, const float *__restrict__ div_s,
+                                                     int ny, int nx, float cx, float cy, float cd) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    constexpr int R = kSkewRing;
+    extern __shared__ float lex_rows[];  // [waves][lex_skew_rsl]: wave w's last-lane results, column c at c + 64
+    __shared__ int flags[kSkewWaves];    // 16-step chunks wave w's last lane has published
+    const int nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int RSL = lex_skew_rsl(nx);
+    const int imax = ny - 2, jmax = nx - 2;
+    const int nb = lex_skew_blocks(ny), DG = lex_skew_groups(nx);
+    const int bytes = nb * DG * 1024;
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(phi_s, 0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(div_s), 0, bytes, 0x00020000);
+    const int nq = (nx + 62 + 15) >> 4;  // steps d = 0 .. nx + 61 (lane 63's last column), 16 per chunk
+    const int nc = (nq + R / 4 - 1) / (R / 4);  // loop iterations of 4 R steps
+    for (int b0 = 0; b0 < nb; b0 += nw) {
+        __threadfence();  // the band before is final and visible (a band's first wave reads its last row)
+        __syncthreads();
+        if ((int)threadIdx.x < nw) __hip_atomic_store(&flags[threadIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        const int m = b0 + wv;
+        if (m >= nb) continue;  // wave-uniform
+        const bool rowok = 1 + 64 * m + lane <= imax;
+        // byte offsets of group 0 (group G at + 1024 G): own slots; lane 63:
+        // the next block's lane 0, group G - 16; lane 0 of a band's first
+        // wave: the block above's lane 63, group G + 15
+        const int oS = (m * DG * 64 + lane) * 16;
+        const int oX = lane == 63 ? (m + 1 < nb ? ((m + 1) * DG - 16) * 1024 : (int)kOob)
+                       : lane == 0 && wv == 0 && m > 0 ? (((m - 1) * DG + 15) * 64 + 63) * 16
+                                                        : (int)kOob;
+        const int oW = rowok ? oS : (int)kOob;
+        float *mine = lex_rows + (size_t)wv * RSL + 64;
+        const float *above = lex_rows + (size_t)(wv > 0 ? wv - 1 : 0) * RSL + 64;
+        // a software pipeline of R groups: iteration c computes groups R c ..
+        // R c + R - 1 and loads groups R (c + 1) + g into the slots it frees;
+        // it starts at c = -1, whose steps only load (no lane is at a column
+        // >= 1 there: nothing is stored or kept), so the loop has one shape
+        // and the compiler's wait counts are the steady-state ones
+        f4v P[R], D[R], X[R];
+#pragma unroll
+        for (int g = 0; g < R; ++g) P[g] = D[g] = X[g] = f4v{0.f, 0.f, 0.f, 0.f};
+        float w = 0.f, vprev = 0.f;  // w: phi(i, j - 1), 0 at column 0 (boundary)
+        for (int c = -1; c < nc; ++c) {
+#pragma unroll
+            for (int h = 0; h < R / 4; ++h) {  // 16-step chunks
+                const int qc = (R / 4) * c + h;
+                float S0[16];
+                if (wv == 0 || qc < 0) {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) S0[k] = 0.f;  // X below
+                } else {
+                    // wave w - 1's last lane must have published chunks 0 .. qc + 4
+                    // (its column 16 qc + 15 comes at its step 16 qc + 78)
+                    const int need = qc + 5 < nq ? qc + 5 : nq;
+                    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&flags[wv - 1], __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+                        __builtin_amdgcn_s_sleep(1);
+                    __asm__ volatile("" ::: "memory");  // the row reads stay after the poll
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        const float4 a4 = *reinterpret_cast<const float4 *>(above + 16 * qc + 4 * p);
+                        S0[4 * p] = a4.x;
+                        S0[4 * p + 1] = a4.y;
+                        S0[4 * p + 2] = a4.z;
+                        S0[4 * p + 3] = a4.w;
+                    }
+                }
+                // this chunk's group 0 at + sof; the refills R groups later
+                const int sof = __builtin_amdgcn_readfirstlane(qc * 4 * 1024);
+                float out[16];
+#pragma unroll
+                for (int gg = 0; gg < 4; ++gg) {
+                    const int g = 4 * h + gg;  // ring slot
+                    const f4v p0 = P[g], p1 = P[(g + 1) % R], x0 = X[g], x1 = X[(g + 1) % R], d4 = D[g];
+                    f4v o4;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int d = 16 * qc + 4 * gg + k;
+                        const float e = k < 3 ? p0[k + 1] : p1[0];           // slot d + 1
+                        const float xn = k < 3 ? x0[k + 1] : x1[0];          // lane 63: slot d - 63
+                        const float xs = k == 0 ? x0[3] : x1[k - 1];         // lane 0: slot d + 63
+                        const float n = __int_as_float(__builtin_amdgcn_update_dpp(
+                            __float_as_int(xn), __float_as_int(e), 0x130, 0xf, 0xf, false));  // wave_shl:1
+                        const float S = __int_as_float(__builtin_amdgcn_update_dpp(
+                            __float_as_int(wv == 0 ? xs : S0[4 * gg + k]), __float_as_int(vprev), 0x138, 0xf, 0xf,
+                            false));  // wave_shr:1
+                        const float a = cx * (e + w);
+                        const float bb = cy * (n + S);
+                        const float v = ((a + bb) - d4[k]) * cd;
+                        const int j = d - lane;
+                        const bool act = (uint32_t)(j - 1) < (uint32_t)jmax;
+                        w = act ? v : w;
+                        vprev = v;
+                        out[4 * gg + k] = v;
+                        o4[k] = act ? v : 0.f;  // the side columns and the padding stay 0
+                    }
+                    // (groups past the block's DG belong to the next block: the
+                    // loop's last iteration runs up to 8 groups past the end)
+                    const bool gok = qc >= 0 && 4 * qc + gg < DG;
+                    __builtin_amdgcn_raw_buffer_store_b128(o4, rp, gok ? oW + 1024 * gg : (int)kOob, sof, 0);
+                    // group G + R's operands into the slot just freed (after its
+                    // last use: a load issued before it would need a second
+                    // register and a copy that waits for the load).  Slot g's
+                    // X and P are still read by group G - 1 (done) -- and
+                    // P / X of slot g + 1 by this group, refilled next.
+                    P[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oS + 1024 * gg,
+                                                                                          sof + R * 1024, 0));
+                    D[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rd, oS + 1024 * gg,
+                                                                                          sof + R * 1024, 0));
+                    X[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oX + 1024 * gg,
+                                                                                          sof + R * 1024, 0));
+                    // keep the prefetch where it is: the scheduler would sink it
+                    // next to its use, R groups later, exposing the latency
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (wv + 1 < nw && qc >= 0 && lane == 63) {
+                    // publish the last lane's 16 results (columns 16 qc - 63 + k)
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) mine[16 * qc - 63 + k] = out[k];
+                    // the row before the count (LDS completes in order; this keeps
+                    // the compiler from sinking the row writes past the flag)
+                    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&flags[wv], qc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+    }
+}
+
 size_t lex_dma_lds_bytes(int nt, int lx) {
     return (size_t)lx * 4 * nt * sizeof(float4) + (size_t)(nt / 64) * kLexRing * sizeof(float);
 }
@@ -979,9 +1184,11 @@ int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star
 }
 
 size_t cfd_clean_divergence_workspace_bytes(int ny, int nx) {
-    // phi and div scratch fields, sized for float64 (cfd_clean_divergence2d_f64)
+    // phi and div scratch fields: row-major float64 (cfd_clean_divergence2d_f64)
+    // or the skewed float32 layout of k_lex_gs_skew, whichever is larger
     const size_t n = (size_t)(ny > 0 ? ny : 0) * (size_t)(nx > 0 ? nx : 0);
-    return 2 * sizeof(double) * n;
+    const size_t skew = ny > 2 && nx > 2 ? 2 * sizeof(float) * lex_skew_floats(ny, nx) : 0;
+    return 2 * sizeof(double) * n > skew ? 2 * sizeof(double) * n : skew;
 }
 
 int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, double dy,
@@ -992,10 +1199,41 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
     const size_t n = (size_t)ny * nx;
     float *phi = reinterpret_cast<float *>(ws);
     float *div = phi + n;
-    CFD_CHECK_HIP(hipMemsetAsync(phi, 0, n * sizeof(float), s));  // np.zeros_like (v5.py:242)
     const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy);
     const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv));
     const float cx = (float)(0.5 / dx), cy = (float)(0.5 / dy);
+    if (ny > 2 && nx > 2 && lex_skew_floats(ny, nx) * 4 < ((size_t)1 << 31) && lex_skew_on()) {
+        // phi and div in the skewed layout (k_lex_gs_skew)
+        const size_t F = lex_skew_floats(ny, nx);
+        float *phi_s = reinterpret_cast<float *>(ws);
+        float *div_s = phi_s + F;
+        const size_t ldsmax = kLexRegLdsMax - 1024;
+        static const int wmax = [] {
+            const char *e = getenv("CFD_LEX_SKEW_WAVES");  // A/B knob: waves per band (1 .. 4)
+            const int v = e ? atoi(e) : kSkewWaves;
+            return v >= 1 && v <= kSkewWaves ? v : kSkewWaves;
+        }();
+        int nw = lex_skew_blocks(ny) < wmax ? lex_skew_blocks(ny) : wmax;
+        while (nw > 1 && lex_skew_lds_bytes(nw, nx) > ldsmax) --nw;
+        const size_t lds = lex_skew_lds_bytes(nw, nx);
+        static bool attr_s = false;
+        if (!attr_s) {
+            CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lex_gs_skew),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsmax));
+            attr_s = true;
+        }
+        CFD_CHECK_HIP(hipMemsetAsync(phi_s, 0, F * sizeof(float), s));  // np.zeros_like (v5.py:242)
+        for (int it = 0; it < iterations; ++it) {
+            hipLaunchKernelGGL(k_divergence_skew, dim3(ceil_div(nx, 256), ny - 2), dim3(256), 0, s, u, v, div_s, ny,
+                               nx, cx, cy);
+            hipLaunchKernelGGL(k_lex_gs_skew, dim3(1), dim3(64 * nw), lds, s, phi_s, div_s, ny, nx, (float)dx2_inv,
+                               (float)dy2_inv, (float)denom_inv);
+            hipLaunchKernelGGL(k_sub_gradient_skew, grid2d(ny, nx), dim3(256), 0, s, phi_s, u, v, ny, nx, cx, cy);
+            CFD_LAUNCH_CHECK();
+        }
+        return CFD_OK;
+    }
+    CFD_CHECK_HIP(hipMemsetAsync(phi, 0, n * sizeof(float), s));  // np.zeros_like (v5.py:242)
     for (int it = 0; it < iterations; ++it) {
         hipLaunchKernelGGL(k_divergence, grid2d(ny, nx), dim3(256), 0, s, u, v, div, ny, nx, cx, cy,
                            (float *)nullptr);

@@ -190,10 +190,13 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
     // the health check, v5.py:601, sees it) and the device's failure counter
     // counts the solve.  It then zeroes both words for the ring's next solve.
     __shared__ int last;
+    // every thread's phi stores at agent scope before the workgroup's ticket
+    // (a workgroup barrier alone orders them only within the workgroup)
+    __threadfence();
     const int any_broken = __syncthreads_or(broken ? 1 : 0);
     if (threadIdx.x == 0) {
         if (any_broken) atomicOr(a.status, 1);
-        __threadfence();  // this workgroup's phi stores and status before its ticket
+        __threadfence();  // the status before the ticket
         last = atomicAdd(a.status + 1, 1) == (int)gridDim.x - 1;
     }
     __syncthreads();

@@ -665,15 +665,10 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
     // for the Jacobi, 34 for the GS -- although the shifting queues' moves are
     // about half of the K = 4 passes' VALU instructions)
     constexpr bool ROT = DMA && K <= 3 && (MODE == kJacobi || RPW <= 2) && !SHIFTQ;
-    // CFD_TBR_ROTR4=1 (build knob): at K = 4 the Jacobi's level queues shift
-    // and its rhs queue rotates with period 4 (a march unrolled by 4): 3 float4
-    // moves per row and step fewer, but 22 VGPRs spill and the pass takes
-    // 4.96-5.04 ms against 2.71 (r04, same box) -- off
-#ifndef CFD_TBR_ROTR4
-#define CFD_TBR_ROTR4 0
-#endif
-    constexpr bool ROTR4 = CFD_TBR_ROTR4 && DMA && K == 4 && MODE == kJacobi && !ROT && !SHIFTQ;
-    const int zl = ROT ? zs + 6 * ((zl0 - zs + 6) / 6) - 1 : ROTR4 ? zs + 4 * ((zl0 - zs + 4) / 4) - 1 : zl0;
+    // (a K = 4 Jacobi with its rhs queue rotated with period 4 -- a march
+    // unrolled by 4 -- spilled 22 VGPRs and took 4.96-5.04 ms per pass against
+    // 2.71, r04: removed in r05)
+    const int zl = ROT ? zs + 6 * ((zl0 - zs + 6) / 6) - 1 : zl0;
     auto P = [&](int p) { return a.in + (size_t)p * plane; };
     auto fixedp = [&](int p) { return (p == a.zb - 1 && a.fixed_lo) || (p == a.ze && a.fixed_hi); };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -815,7 +810,7 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             // period 6 is a multiple of K) the rhs of plane q in slot
             // (q - zs) mod K of Rq; the march is unrolled by 6 so that every
             // slot index is a compile-time constant.  (K = 4 shifts Rq.)
-            constexpr bool ROTR = (ROT && 6 % K == 0) || ROTR4;
+            constexpr bool ROTR = ROT && 6 % K == 0;
             // memory operations per step and wave, for EARLY's vmcnt wait:
             // staging DMAs, !RDMA rhs loads, level-K stores (one per row, issued
             // for every row: see phase R), first-pass rhs stores
@@ -1242,15 +1237,6 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
             using I0 = std::integral_constant<int, 0>;
             using I1 = std::integral_constant<int, 1>;
             auto march = [&](auto bpc) {
-                if constexpr (ROTR4) {  // zl - zs + 1 is a multiple of 4
-                    for (int zb = zs; zb <= zl; zb += 4) {
-                        step(zb, I0{}, I0{}, bpc);
-                        step(zb + 1, I1{}, I1{}, bpc);
-                        step(zb + 2, I0{}, std::integral_constant<int, 2>{}, bpc);
-                        step(zb + 3, I1{}, std::integral_constant<int, 3>{}, bpc);
-                    }
-                    return;
-                }
                 if constexpr (!ROT) {
                     for (int zb = zs; zb <= zl; zb += 2) {
                         step(zb, I0{}, I0{}, bpc);

@@ -312,7 +312,9 @@ def project_velocity(phi, u_star, v_star, dx, dy, dt, u=None, v=None, gradmax=No
 def persistent_failures() -> int:
     """Synchronises the device and returns how many persistent small-grid
     solves (the one-launch 2-D Jacobi / red-black GS) had a tile wait expire
-    since the last call; their phi is all NaN (cfd_persistent_status)."""
+    since the last call; their phi is all NaN (cfd_persistent_status).  The
+    count is per device, not per caller: solvers sharing a device share it (a
+    failed solve's NaN phi still fails its own solver's non-finite check)."""
     import ctypes
     n = ctypes.c_int(0)
     call("cfd_persistent_status", ctypes.byref(n))

@@ -484,7 +484,10 @@ int cfd_set_persistent_launch(int cooperative, long long poll_ticks);
 /* Synchronises the current device, then returns in *expired the number of
  * persistent solves on it whose neighbour wait expired since the last call
  * (and clears the count).  The Python solver checks it in
- * monitor_simulation_health (v5.py:599-613). */
+ * monitor_simulation_health (v5.py:599-613).  The count is one word per
+ * device, shared by every caller on it: with several solvers on a device one
+ * caller's read can take another's failure -- whose phi is all NaN, so that
+ * solver's own non-finite check (v5.py:601) still fails the step. */
 int cfd_persistent_status(int *expired);
 /* Frees the calling thread's library-owned device buffers: the persistent
  * Jacobi's exchange rings (24 B per cell of the largest grid the thread

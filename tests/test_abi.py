@@ -41,8 +41,12 @@ def test_library_identifies_itself():
     assert L.cfd_abi_version() == _lib.ABI_VERSION
     assert L.cfd_device_arch() == b"gfx950"
     assert L.cfd_rbgs_workspace_bytes(1500) >= 4 * 1500
-    # sized for float64 (2 fields) and for the f32 pipelined path (phi, div1, div2, u1, v1)
+    # two row-major float64 fields, or two float32 fields in the skewed layout
+    # of the f32 sweep (64-row blocks x (nx + 63) diagonals x 64), the larger
     assert L.cfd_clean_divergence_workspace_bytes(180, 600) == 2 * 8 * 180 * 600
+    assert L.cfd_clean_divergence_workspace_bytes(3, 64) == 2 * 4 * 1 * (64 + 63) * 64
+    assert L.cfd_clean_divergence_workspace_bytes(67, 3) == 2 * 4 * 2 * (3 + 63) * 64
+    assert L.cfd_clean_divergence_workspace_bytes(2, 5000) == 2 * 8 * 2 * 5000
 
 
 def test_invalid_arguments_report_errors_without_gpu():
