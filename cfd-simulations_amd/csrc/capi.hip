@@ -1,6 +1,7 @@
-#include <mutex>
 // capi.hip -- error reporting, identification and sweep timing of libcfdsim.
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "internal.hpp"
@@ -123,6 +124,24 @@ int *persist_fail_word() {
         word[dev] = p;
     }
     return word[dev];
+}
+
+unsigned *energy_scratch(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, unsigned *> bufs;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    unsigned *&p = bufs[{dev, s}];
+    if (!p) {
+        const size_t bytes = 64 + kEnergyBlocks * sizeof(double);
+        if (hipMalloc(&p, bytes) != hipSuccess) return p = nullptr;
+        if (hipMemset(p, 0, bytes) != hipSuccess) {
+            (void)hipFree(p);
+            return p = nullptr;
+        }
+    }
+    return p;
 }
 
 int launch_persistent(const void *f, int nblocks, int threads, void *args, hipStream_t s) {

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void k_predictor(const float *__restrict__ u,
     }
     us[c] = uc + dt * (-cu + lu);
     vs[c] = vc + dt * (-cv + lv);
-    if (SUPG && tau_out) tau_out[c] = t;
+    if (tau_out) tau_out[c] = t;  // 0 without SUPG (v5.py:292: never assigned without SUPG)
 }
 
 // compute_divergence_fast, v5.py:178-187 (+ max|div| diagnostic, v5.py:410)
@@ -653,6 +653,9 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
 //    four steps at a time (0 at the zero side columns and the padding).
 // Same arithmetic and order as the serial loop: bit-identical.
 constexpr int kSkewWaves = 4;  // waves per band: at one wave per SIMD the chain, not the memory path, sets the pace
+#ifndef CFD_SKEW_EXP
+#define CFD_SKEW_EXP 0  // timing experiments only (wrong results): 1 no stores, 2 no loads, 4 no DPP
+#endif
 constexpr int kSkewRing = 8;   // groups of 4 steps in flight per wave (and per loop iteration)
 __host__ __device__ inline int lex_skew_blocks(int ny) { return (ny - 2 + 63) >> 6; }
 __host__ __device__ inline int lex_skew_groups(int nx) { return (nx + 63 + 3) >> 2; }
@@ -671,36 +674,96 @@ __device__ inline size_t skew_at(int i, int j, int dg) {  // interior row i >= 1
 }
 
 // compute_divergence_fast (v5.py:178-187) into the skewed layout: interior
-// rows, every column (0 at the side columns, as k_divergence).
+// rows, every column (0 at the side columns, as k_divergence).  With zphi the
+// grid has one more row, ny - 1, and zphi gets zeros on row ny - 1 when that
+// row is a lane of the last block: the first sweep leaves the rows past ny - 2
+// unwritten, and the next sweep reads that one as the last row's N.
 __global__ __launch_bounds__(256) void k_divergence_skew(const float *__restrict__ u, const float *__restrict__ v,
-                                                         float *__restrict__ div_s, int ny, int nx, float cx, float cy) {
+                                                         float *__restrict__ div_s, float *__restrict__ zphi, int ny,
+                                                         int nx, float cx, float cy) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = blockIdx.y + 1;
     if (j >= nx) return;
+    const int dg = lex_skew_groups(nx);
+    if (i == ny - 1) {  // zphi only
+        if (((ny - 2) & 63) != 0) zphi[skew_at(i, j, dg)] = 0.0f;
+        return;
+    }
     const size_t c = (size_t)i * nx + j;
     float d = 0.0f;
     if (j >= 1 && j <= nx - 2) d = (u[c + 1] - u[c - 1]) * cx + (v[c + nx] - v[c - nx]) * cy;
-    div_s[skew_at(i, j, lex_skew_groups(nx))] = d;
+    div_s[skew_at(i, j, dg)] = d;
 }
 
 // u -= dphi/dx, v -= dphi/dy (v5.py:255-256) with phi in the skewed layout
 // (rows 0 and ny - 1 are the zero boundary).
+__device__ inline float skew_phi(const float *phi_s, int i, int j, int ny, int dg) {
+    return i >= 1 && i <= ny - 2 ? phi_s[skew_at(i, j, dg)] : 0.0f;
+}
 __global__ void k_sub_gradient_skew(const float *__restrict__ phi_s, float *__restrict__ u, float *__restrict__ v,
                                     int ny, int nx, float cx, float cy) {
     CFD_2D_INDEX
     if (!interior(i, j, ny, nx)) return;
     const int dg = lex_skew_groups(nx);
-    const float pe = phi_s[skew_at(i, j + 1, dg)], pw = phi_s[skew_at(i, j - 1, dg)];
-    const float pn = i + 1 <= ny - 2 ? phi_s[skew_at(i + 1, j, dg)] : 0.0f;
-    const float ps = i - 1 >= 1 ? phi_s[skew_at(i - 1, j, dg)] : 0.0f;
-    const float a = (pe - pw) * cx;
-    const float b = (pn - ps) * cy;
+    const float a = (skew_phi(phi_s, i, j + 1, ny, dg) - skew_phi(phi_s, i, j - 1, ny, dg)) * cx;
+    const float b = (skew_phi(phi_s, i + 1, j, ny, dg) - skew_phi(phi_s, i - 1, j, ny, dg)) * cy;
     u[c] = u[c] - a;
     v[c] = v[c] - b;
 }
 
-__global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_s, const float *__restrict__ div_s,
-                                                     int ny, int nx, float cx, float cy, float cd) {
+// clean_divergence's second iteration without materialising the first one's
+// u, v (iterations == 2, the reference's call, v5.py:430): div of
+// u1 = u - dphi1/dx, v1 = v - dphi1/dy, each neighbour's u1 / v1 re-formed with
+// k_sub_gradient_skew's operations (the boundary ring keeps u, v), then
+// k_divergence's -- the same bits as the three launches.
+__global__ __launch_bounds__(256) void k_divergence2_skew(const float *__restrict__ u, const float *__restrict__ v,
+                                                          const float *__restrict__ phi1, float *__restrict__ div_s,
+                                                          int ny, int nx, float cx, float cy) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y + 1;
+    if (j >= nx) return;
+    const int dg = lex_skew_groups(nx);
+    float d = 0.0f;
+    if (j >= 1 && j <= nx - 2) {
+        auto u1 = [&](int jj) {
+            const float u0 = u[(size_t)i * nx + jj];
+            if (jj < 1 || jj > nx - 2) return u0;
+            const float a = (skew_phi(phi1, i, jj + 1, ny, dg) - skew_phi(phi1, i, jj - 1, ny, dg)) * cx;
+            return u0 - a;
+        };
+        auto v1 = [&](int ii) {
+            const float v0 = v[(size_t)ii * nx + j];
+            if (ii < 1 || ii > ny - 2) return v0;
+            const float b = (skew_phi(phi1, ii + 1, j, ny, dg) - skew_phi(phi1, ii - 1, j, ny, dg)) * cy;
+            return v0 - b;
+        };
+        d = (u1(j + 1) - u1(j - 1)) * cx + (v1(i + 1) - v1(i - 1)) * cy;
+    }
+    div_s[skew_at(i, j, dg)] = d;
+}
+
+// both iterations' u -= dphi/dx, v -= dphi/dy in one pass: (u - a1) - a2, the
+// two in-place subtractions' bits
+__global__ void k_sub_gradient2_skew(const float *__restrict__ phi1, const float *__restrict__ phi2,
+                                     float *__restrict__ u, float *__restrict__ v, int ny, int nx, float cx, float cy) {
+    CFD_2D_INDEX
+    if (!interior(i, j, ny, nx)) return;
+    const int dg = lex_skew_groups(nx);
+    const float a1 = (skew_phi(phi1, i, j + 1, ny, dg) - skew_phi(phi1, i, j - 1, ny, dg)) * cx;
+    const float b1 = (skew_phi(phi1, i + 1, j, ny, dg) - skew_phi(phi1, i - 1, j, ny, dg)) * cy;
+    const float a2 = (skew_phi(phi2, i, j + 1, ny, dg) - skew_phi(phi2, i, j - 1, ny, dg)) * cx;
+    const float b2 = (skew_phi(phi2, i + 1, j, ny, dg) - skew_phi(phi2, i - 1, j, ny, dg)) * cy;
+    u[c] = (u[c] - a1) - a2;
+    v[c] = (v[c] - b1) - b2;
+}
+
+// phi: the skewed phi buffers from phi_base (phi_bytes in all); the sweep
+// reads the old values at byte offset old_off (kOob: all zeros, the first
+// sweep of clean_divergence) and writes the new ones at new_off (== old_off:
+// in place).
+__global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_base, int phi_bytes, int old_off,
+                                                     int new_off, const float *__restrict__ div_s, int ny, int nx,
+                                                     float cx, float cy, float cd) {
     typedef float f4v __attribute__((ext_vector_type(4)));
     constexpr int R = kSkewRing;
     extern __shared__ float lex_rows[];  // [waves][lex_skew_rsl]: wave w's last-lane results, column c at c + 64
@@ -711,7 +774,7 @@ __global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_s, 
     const int imax = ny - 2, jmax = nx - 2;
     const int nb = lex_skew_blocks(ny), DG = lex_skew_groups(nx);
     const int bytes = nb * DG * 1024;
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(phi_s, 0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(phi_base, 0, phi_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rd =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(div_s), 0, bytes, 0x00020000);
     const int nq = (nx + 62 + 15) >> 4;  // steps d = 0 .. nx + 61 (lane 63's last column), 16 per chunk
@@ -724,14 +787,16 @@ __global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_s, 
         const int m = b0 + wv;
         if (m >= nb) continue;  // wave-uniform
         const bool rowok = 1 + 64 * m + lane <= imax;
-        // byte offsets of group 0 (group G at + 1024 G): own slots; lane 63:
-        // the next block's lane 0, group G - 16; lane 0 of a band's first
-        // wave: the block above's lane 63, group G + 15
-        const int oS = (m * DG * 64 + lane) * 16;
-        const int oX = lane == 63 ? (m + 1 < nb ? ((m + 1) * DG - 16) * 1024 : (int)kOob)
-                       : lane == 0 && wv == 0 && m > 0 ? (((m - 1) * DG + 15) * 64 + 63) * 16
+        // byte offsets of group 0 (group G at + 1024 G): own slots (div; old
+        // phi; new phi); lane 63: the next block's lane 0, group G - 16, old;
+        // lane 0 of a band's first wave: the block above's lane 63, group
+        // G + 15, new.  (kOob + an offset stays past the buffer.)
+        const int oD = (m * DG * 64 + lane) * 16;
+        const int oS = old_off + oD;
+        const int oX = lane == 63 ? (m + 1 < nb ? old_off + ((m + 1) * DG - 16) * 1024 : (int)kOob)
+                       : lane == 0 && wv == 0 && m > 0 ? new_off + (((m - 1) * DG + 15) * 64 + 63) * 16
                                                         : (int)kOob;
-        const int oW = rowok ? oS : (int)kOob;
+        const int oW = rowok ? new_off + oD : (int)kOob;
         float *mine = lex_rows + (size_t)wv * RSL + 64;
         const float *above = lex_rows + (size_t)(wv > 0 ? wv - 1 : 0) * RSL + 64;
         // a software pipeline of R groups: iteration c computes groups R c ..
@@ -740,18 +805,20 @@ __global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_s, 
         // >= 1 there: nothing is stored or kept), so the loop has one shape
         // and the compiler's wait counts are the steady-state ones
         f4v P[R], D[R], X[R];
-#pragma unroll
-        for (int g = 0; g < R; ++g) P[g] = D[g] = X[g] = f4v{0.f, 0.f, 0.f, 0.f};
-        float w = 0.f, vprev = 0.f;  // w: phi(i, j - 1), 0 at column 0 (boundary)
-        for (int c = -1; c < nc; ++c) {
-#pragma unroll
-            for (int h = 0; h < R / 4; ++h) {  // 16-step chunks
-                const int qc = (R / 4) * c + h;
-                float S0[16];
-                if (wv == 0 || qc < 0) {
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) S0[k] = 0.f;  // X below
-                } else {
+        float w, vprev;  // w: phi(i, j - 1)
+        // One 16-step chunk (ring slots 4 H .. 4 H + 3).  The step is issue-
+        // bound (a wave64 VALU op takes 4 cycles: ~13 per step were ~55 cycles
+        // against the ~47-cycle dependent chain), so the chunk is specialised:
+        // FULL chunks -- every lane at a column 1 .. nx - 2 in all 16 steps,
+        // most of a sweep -- skip the per-step column test and the selects;
+        // FIRST (a band's first wave) takes lane 0's row above from X, the
+        // others from the LDS row, without a per-step select.
+        auto chunk = [&](auto Hc, auto FULLc, auto FIRSTc, int qc) {
+            constexpr int H = decltype(Hc)::value;
+            constexpr bool FULL = decltype(FULLc)::value, FIRST = decltype(FIRSTc)::value;
+            float S0[16];
+            if constexpr (!FIRST) {
+                if (qc >= 0) {
                     // wave w - 1's last lane must have published chunks 0 .. qc + 4
                     // (its column 16 qc + 15 comes at its step 16 qc + 78)
                     const int need = qc + 5 < nq ? qc + 5 : nq;
@@ -767,66 +834,119 @@ __global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_s, 
                         S0[4 * p + 2] = a4.z;
                         S0[4 * p + 3] = a4.w;
                     }
-                }
-                // this chunk's group 0 at + sof; the refills R groups later
-                const int sof = __builtin_amdgcn_readfirstlane(qc * 4 * 1024);
-                float out[16];
+                } else {
 #pragma unroll
-                for (int gg = 0; gg < 4; ++gg) {
-                    const int g = 4 * h + gg;  // ring slot
-                    const f4v p0 = P[g], p1 = P[(g + 1) % R], x0 = X[g], x1 = X[(g + 1) % R], d4 = D[g];
-                    f4v o4;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int d = 16 * qc + 4 * gg + k;
-                        const float e = k < 3 ? p0[k + 1] : p1[0];           // slot d + 1
-                        const float xn = k < 3 ? x0[k + 1] : x1[0];          // lane 63: slot d - 63
-                        const float xs = k == 0 ? x0[3] : x1[k - 1];         // lane 0: slot d + 63
-                        const float n = __int_as_float(__builtin_amdgcn_update_dpp(
-                            __float_as_int(xn), __float_as_int(e), 0x130, 0xf, 0xf, false));  // wave_shl:1
-                        const float S = __int_as_float(__builtin_amdgcn_update_dpp(
-                            __float_as_int(wv == 0 ? xs : S0[4 * gg + k]), __float_as_int(vprev), 0x138, 0xf, 0xf,
-                            false));  // wave_shr:1
-                        const float a = cx * (e + w);
-                        const float bb = cy * (n + S);
-                        const float v = ((a + bb) - d4[k]) * cd;
-                        const int j = d - lane;
-                        const bool act = (uint32_t)(j - 1) < (uint32_t)jmax;
-                        w = act ? v : w;
-                        vprev = v;
-                        out[4 * gg + k] = v;
-                        o4[k] = act ? v : 0.f;  // the side columns and the padding stay 0
-                    }
-                    // (groups past the block's DG belong to the next block: the
-                    // loop's last iteration runs up to 8 groups past the end)
-                    const bool gok = qc >= 0 && 4 * qc + gg < DG;
-                    __builtin_amdgcn_raw_buffer_store_b128(o4, rp, gok ? oW + 1024 * gg : (int)kOob, sof, 0);
-                    // group G + R's operands into the slot just freed (after its
-                    // last use: a load issued before it would need a second
-                    // register and a copy that waits for the load).  Slot g's
-                    // X and P are still read by group G - 1 (done) -- and
-                    // P / X of slot g + 1 by this group, refilled next.
-                    P[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oS + 1024 * gg,
-                                                                                          sof + R * 1024, 0));
-                    D[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rd, oS + 1024 * gg,
-                                                                                          sof + R * 1024, 0));
-                    X[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oX + 1024 * gg,
-                                                                                          sof + R * 1024, 0));
-                    // keep the prefetch where it is: the scheduler would sink it
-                    // next to its use, R groups later, exposing the latency
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (wv + 1 < nw && qc >= 0 && lane == 63) {
-                    // publish the last lane's 16 results (columns 16 qc - 63 + k)
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) mine[16 * qc - 63 + k] = out[k];
-                    // the row before the count (LDS completes in order; this keeps
-                    // the compiler from sinking the row writes past the flag)
-                    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    __hip_atomic_store(&flags[wv], qc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    for (int k = 0; k < 16; ++k) S0[k] = 0.f;
                 }
             }
-        }
+            // this chunk's group 0 at + sof; the refills R groups later
+            const int sof = __builtin_amdgcn_readfirstlane(qc * 4 * 1024);
+            float out[16];
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                const int g = 4 * H + gg;  // ring slot
+                const f4v p0 = P[g], p1 = P[(g + 1) % R], x0 = X[g], x1 = X[(g + 1) % R], d4 = D[g];
+                f4v o4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float e = k < 3 ? p0[k + 1] : p1[0];   // slot d + 1
+                    const float xn = k < 3 ? x0[k + 1] : x1[0];  // lane 63: slot d - 63
+                    float s0;
+                    if constexpr (FIRST)
+                        s0 = k == 0 ? x0[3] : x1[k - 1];  // lane 0: slot d + 63
+                    else
+                        s0 = S0[4 * gg + k];
+                    const float n = __int_as_float(__builtin_amdgcn_update_dpp(
+                        __float_as_int(xn), __float_as_int(e), 0x130, 0xf, 0xf, false));  // wave_shl:1
+                    const float S = (CFD_SKEW_EXP & 4) ? vprev
+                                                       : __int_as_float(__builtin_amdgcn_update_dpp(
+                                                             __float_as_int(s0), __float_as_int(vprev), 0x138, 0xf,
+                                                             0xf, false));  // wave_shr:1
+                    const float a = cx * (e + w);
+                    const float bb = cy * (n + S);
+                    const float v = ((a + bb) - d4[k]) * cd;
+                    if constexpr (FULL) {
+                        w = v;
+                        o4[k] = v;
+                    } else {
+                        const int j = 16 * qc + 4 * gg + k - lane;  // step d = 16 qc + 4 gg + k
+                        const bool act = (uint32_t)(j - 1) < (uint32_t)jmax;
+                        w = act ? v : w;
+                        o4[k] = act ? v : 0.f;  // the side columns and the padding stay 0
+                    }
+                    vprev = v;
+                    out[4 * gg + k] = v;
+                }
+                // (groups past the block's DG belong to the next block: the
+                // loop's last iteration runs up to 8 groups past the end)
+                const bool gok = FULL || (qc >= 0 && 4 * qc + gg < DG);
+                if constexpr (!(CFD_SKEW_EXP & 1))
+                    __builtin_amdgcn_raw_buffer_store_b128(o4, rp, gok ? oW + 1024 * gg : (int)kOob, sof, 0);
+                // group G + R's operands into the slot just freed (after its
+                // last use: a load issued before it would need a second
+                // register and a copy that waits for the load).  Slot g is
+                // also read by group G - 1 (done), slot g + 1 by this group
+                // (refilled next).
+                if constexpr (!(CFD_SKEW_EXP & 2)) {
+                    P[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oS + 1024 * gg,
+                                                                                          sof + R * 1024, 0));
+                    D[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rd, oD + 1024 * gg,
+                                                                                          sof + R * 1024, 0));
+                    // (all lanes load X though only lane 63 -- and lane 0 of a
+                    // band's first wave -- reads it: exec-masking the load to
+                    // those lanes measured 8-11 % slower, r05)
+                    X[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oX + 1024 * gg,
+                                                                                          sof + R * 1024, 0));
+                } else {
+                    P[g] += 1.f;
+                }
+                // keep the prefetch where it is: the scheduler would sink it
+                // next to its use, R groups later, exposing the latency
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (wv + 1 < nw && qc >= 0 && lane == 63) {
+                // publish the last lane's 16 results (columns 16 qc - 63 + k)
+#pragma unroll
+                for (int k = 0; k < 16; ++k) mine[16 * qc - 63 + k] = out[k];
+                // the row before the count (LDS completes in order; this keeps
+                // the compiler from sinking the row writes past the flag)
+                __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __hip_atomic_store(&flags[wv], qc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        };
+        using T1 = std::true_type;
+        using F0 = std::false_type;
+        static_assert(R == 8, "two 16-step chunks per iteration");
+        using H0 = std::integral_constant<int, 0>;
+        using H1 = std::integral_constant<int, 1>;
+        // iterations whose two chunks are both FULL: chunk 2 c >= 4 and
+        // 16 (2 c + 1) + 15 <= jmax; the loop is split into head, middle and
+        // tail loops around them (a per-chunk branch made the register
+        // allocator copy the ring at every merge, waiting for its loads)
+        const int cf0 = 2, cf1 = (jmax - 31) >= 0 ? (jmax - 31) >> 5 : -1;  // [cf0, cf1]
+        const int cm0 = cf1 >= cf0 ? cf0 : nc, cm1 = cf1 >= cf0 ? (cf1 + 1 < nc ? cf1 + 1 : nc) : nc;
+        auto run = [&](auto FIRSTc) {
+#pragma unroll
+            for (int g = 0; g < R; ++g) P[g] = D[g] = X[g] = f4v{0.f, 0.f, 0.f, 0.f};
+            w = 0.f;  // column 0 (boundary)
+            vprev = 0.f;
+            for (int c = -1; c < cm0; ++c) {
+                chunk(H0{}, F0{}, FIRSTc, 2 * c);
+                chunk(H1{}, F0{}, FIRSTc, 2 * c + 1);
+            }
+            for (int c = cm0; c < cm1; ++c) {
+                chunk(H0{}, T1{}, FIRSTc, 2 * c);
+                chunk(H1{}, T1{}, FIRSTc, 2 * c + 1);
+            }
+            for (int c = cm1; c < nc; ++c) {
+                chunk(H0{}, F0{}, FIRSTc, 2 * c);
+                chunk(H1{}, F0{}, FIRSTc, 2 * c + 1);
+            }
+        };
+        if (wv == 0)
+            run(T1{});
+        else
+            run(F0{});
     }
 }
 
@@ -1105,7 +1225,7 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
         a.nu = nu_eff;
         a.us = u_star;
         a.vs = v_star;
-        a.tau = use_supg ? tau : nullptr;
+        a.tau = tau;  // zeros without SUPG
         a.nu_s = nu_eff_scalar;
         a.dt = dt;
         a.ny = ny;
@@ -1184,10 +1304,11 @@ int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star
 }
 
 size_t cfd_clean_divergence_workspace_bytes(int ny, int nx) {
-    // phi and div scratch fields: row-major float64 (cfd_clean_divergence2d_f64)
-    // or the skewed float32 layout of k_lex_gs_skew, whichever is larger
+    // scratch fields: phi and div row-major float64 (cfd_clean_divergence2d_f64)
+    // or div and two phi in the skewed float32 layout of k_lex_gs_skew,
+    // whichever is larger
     const size_t n = (size_t)(ny > 0 ? ny : 0) * (size_t)(nx > 0 ? nx : 0);
-    const size_t skew = ny > 2 && nx > 2 ? 2 * sizeof(float) * lex_skew_floats(ny, nx) : 0;
+    const size_t skew = ny > 2 && nx > 2 ? 3 * sizeof(float) * lex_skew_floats(ny, nx) : 0;
     return 2 * sizeof(double) * n > skew ? 2 * sizeof(double) * n : skew;
 }
 
@@ -1202,11 +1323,15 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
     const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy);
     const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv));
     const float cx = (float)(0.5 / dx), cy = (float)(0.5 / dy);
-    if (ny > 2 && nx > 2 && lex_skew_floats(ny, nx) * 4 < ((size_t)1 << 31) && lex_skew_on()) {
-        // phi and div in the skewed layout (k_lex_gs_skew)
+    if (ny > 2 && nx > 2 && 2 * lex_skew_floats(ny, nx) * 4 < ((size_t)1 << 31) && lex_skew_on()) {
+        // div and two phi buffers in the skewed layout (k_lex_gs_skew): the
+        // first sweep starts from phi = 0 (np.zeros_like, v5.py:242) by
+        // reading nothing; at iterations == 2 the second sweep writes the
+        // second buffer, so both gradients are subtracted in one pass
         const size_t F = lex_skew_floats(ny, nx);
-        float *phi_s = reinterpret_cast<float *>(ws);
-        float *div_s = phi_s + F;
+        float *div_s = reinterpret_cast<float *>(ws);
+        float *phi1 = div_s + F, *phi2 = phi1 + F;
+        const int pbytes = (int)(2 * F * sizeof(float));
         const size_t ldsmax = kLexRegLdsMax - 1024;
         static const int wmax = [] {
             const char *e = getenv("CFD_LEX_SKEW_WAVES");  // A/B knob: waves per band (1 .. 4)
@@ -1222,15 +1347,31 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsmax));
             attr_s = true;
         }
-        CFD_CHECK_HIP(hipMemsetAsync(phi_s, 0, F * sizeof(float), s));  // np.zeros_like (v5.py:242)
-        for (int it = 0; it < iterations; ++it) {
-            hipLaunchKernelGGL(k_divergence_skew, dim3(ceil_div(nx, 256), ny - 2), dim3(256), 0, s, u, v, div_s, ny,
-                               nx, cx, cy);
-            hipLaunchKernelGGL(k_lex_gs_skew, dim3(1), dim3(64 * nw), lds, s, phi_s, div_s, ny, nx, (float)dx2_inv,
-                               (float)dy2_inv, (float)denom_inv);
-            hipLaunchKernelGGL(k_sub_gradient_skew, grid2d(ny, nx), dim3(256), 0, s, phi_s, u, v, ny, nx, cx, cy);
-            CFD_LAUNCH_CHECK();
+        auto sweep = [&](int old_off, int new_off) {
+            hipLaunchKernelGGL(k_lex_gs_skew, dim3(1), dim3(64 * nw), lds, s, phi1, pbytes, old_off, new_off, div_s,
+                               ny, nx, (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
+        };
+        const dim3 gr(ceil_div(nx, 256), ny - 2);
+        if (iterations >= 1) {
+            hipLaunchKernelGGL(k_divergence_skew, dim3(gr.x, ny - 1), dim3(256), 0, s, u, v, div_s, phi1, ny, nx, cx,
+                               cy);
+            sweep((int)kOob, 0);
         }
+        if (iterations == 2) {
+            hipLaunchKernelGGL(k_divergence2_skew, gr, dim3(256), 0, s, u, v, phi1, div_s, ny, nx, cx, cy);
+            sweep(0, (int)(F * sizeof(float)));
+            hipLaunchKernelGGL(k_sub_gradient2_skew, grid2d(ny, nx), dim3(256), 0, s, phi1, phi2, u, v, ny, nx, cx,
+                               cy);
+        } else if (iterations >= 1) {
+            hipLaunchKernelGGL(k_sub_gradient_skew, grid2d(ny, nx), dim3(256), 0, s, phi1, u, v, ny, nx, cx, cy);
+            for (int it = 1; it < iterations; ++it) {  // in place on phi1
+                hipLaunchKernelGGL(k_divergence_skew, gr, dim3(256), 0, s, u, v, div_s, (float *)nullptr, ny, nx, cx,
+                                   cy);
+                sweep(0, 0);
+                hipLaunchKernelGGL(k_sub_gradient_skew, grid2d(ny, nx), dim3(256), 0, s, phi1, u, v, ny, nx, cx, cy);
+            }
+        }
+        CFD_LAUNCH_CHECK();
         return CFD_OK;
     }
     CFD_CHECK_HIP(hipMemsetAsync(phi, 0, n * sizeof(float), s));  // np.zeros_like (v5.py:242)
@@ -1346,8 +1487,12 @@ int cfd_energy_mean2d_f32(const float *u, const float *v, size_t n, double *out,
     CFD_REQUIRE(u && v && out && n > 0, "energy_mean2d: bad arguments");
     hipStream_t s = as_stream(stream);
     if (n <= kEnergyOneBlock) {
-        hipLaunchKernelGGL((k_energy_mean_1blk<float, false>), dim3(1), dim3(1024), 0, s, const_cast<float *>(u),
-                           const_cast<float *>(v), n, out, float(0), float(0));
+        if (unsigned *ws = energy_scratch(s))
+            hipLaunchKernelGGL((k_energy_mean_mb<float, false>), dim3(kEnergyBlocks), dim3(256), 0, s,
+                               const_cast<float *>(u), const_cast<float *>(v), n, out, float(0), float(0), ws);
+        else
+            hipLaunchKernelGGL((k_energy_mean_1blk<float, false>), dim3(1), dim3(1024), 0, s, const_cast<float *>(u),
+                               const_cast<float *>(v), n, out, float(0), float(0));
         CFD_LAUNCH_CHECK();
         return CFD_OK;
     }
@@ -1362,7 +1507,11 @@ int cfd_energy_mean_clip2d_f32(float *u, float *v, size_t n, double *out, float 
     CFD_REQUIRE(u && v && out && n > 0, "energy_mean_clip2d_f32: bad arguments");
     hipStream_t s = as_stream(stream);
     if (n <= kEnergyOneBlock) {
-        hipLaunchKernelGGL((k_energy_mean_1blk<float, true>), dim3(1), dim3(1024), 0, s, u, v, n, out, lo, hi);
+        if (unsigned *ws = energy_scratch(s))
+            hipLaunchKernelGGL((k_energy_mean_mb<float, true>), dim3(kEnergyBlocks), dim3(256), 0, s, u, v, n, out,
+                               lo, hi, ws);
+        else
+            hipLaunchKernelGGL((k_energy_mean_1blk<float, true>), dim3(1), dim3(1024), 0, s, u, v, n, out, lo, hi);
         CFD_LAUNCH_CHECK();
         return CFD_OK;
     }

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void k_predictor64(const double *__restrict__ 
     }
     us[c] = uc + dt * (-cu + lu);
     vs[c] = vc + dt * (-cv + lv);
-    if (SUPG && tau_out) tau_out[c] = t;
+    if (tau_out) tau_out[c] = t;  // 0 without SUPG (v5.py:292: never assigned without SUPG)
 }
 
 // compute_divergence_fast, v5.py:178-187 (+ max|div|, v5.py:410)
@@ -525,7 +525,7 @@ int cfd_predictor2d_f64(const double *u, const double *v, const double *nu_eff, 
         a.nu = nu_eff;
         a.us = u_star;
         a.vs = v_star;
-        a.tau = use_supg ? tau : nullptr;
+        a.tau = tau;  // zeros without SUPG
         a.nu_s = nu_eff_scalar;
         a.dt = dt;
         a.ny = ny;
@@ -660,8 +660,12 @@ int cfd_energy_mean2d_f64(const double *u, const double *v, size_t n, double *ou
     CFD_REQUIRE(u && v && out && n > 0, "energy_mean2d_f64: bad arguments");
     hipStream_t s = as_stream(stream);
     if (n <= kEnergyOneBlock) {
-        hipLaunchKernelGGL((k_energy_mean_1blk<double, false>), dim3(1), dim3(1024), 0, s, const_cast<double *>(u),
-                           const_cast<double *>(v), n, out, double(0), double(0));
+        if (unsigned *ws = energy_scratch(s))
+            hipLaunchKernelGGL((k_energy_mean_mb<double, false>), dim3(kEnergyBlocks), dim3(256), 0, s,
+                               const_cast<double *>(u), const_cast<double *>(v), n, out, double(0), double(0), ws);
+        else
+            hipLaunchKernelGGL((k_energy_mean_1blk<double, false>), dim3(1), dim3(1024), 0, s, const_cast<double *>(u),
+                               const_cast<double *>(v), n, out, double(0), double(0));
         CFD_LAUNCH_CHECK();
         return CFD_OK;
     }
@@ -676,7 +680,11 @@ int cfd_energy_mean_clip2d_f64(double *u, double *v, size_t n, double *out, doub
     CFD_REQUIRE(u && v && out && n > 0, "energy_mean_clip2d_f64: bad arguments");
     hipStream_t s = as_stream(stream);
     if (n <= kEnergyOneBlock) {
-        hipLaunchKernelGGL((k_energy_mean_1blk<double, true>), dim3(1), dim3(1024), 0, s, u, v, n, out, lo, hi);
+        if (unsigned *ws = energy_scratch(s))
+            hipLaunchKernelGGL((k_energy_mean_mb<double, true>), dim3(kEnergyBlocks), dim3(256), 0, s, u, v, n, out,
+                               lo, hi, ws);
+        else
+            hipLaunchKernelGGL((k_energy_mean_1blk<double, true>), dim3(1), dim3(1024), 0, s, u, v, n, out, lo, hi);
         CFD_LAUNCH_CHECK();
         return CFD_OK;
     }

@@ -61,17 +61,24 @@ struct Tuning {
     // NumPy scalars), 1 fast (x*x, correctly rounded sqrt, rcp + Newton
     // divisions: the compiled reference's fastmath arithmetic, within 1e-6)
     int pred_tau = 0;
-    // persistent small-grid solves (jacobi2d_persist, rbgs2d_persist): launch
-    // cooperatively (the runtime guarantees every tile co-resident or refuses
-    // the launch, which then takes the launch-per-pass path); the bound of a
-    // neighbour poll in ticks of the 100 MHz clock (0: 20 s)
-    int persist_coop = 1;
+    // persistent small-grid solves (jacobi2d_persist, rbgs2d_persist): 0 = a
+    // plain launch after the occupancy check (r05 default: the cooperative
+    // launch cost ~30 us of queue gap per solve, 0.79 -> 0.76 ms per v5
+    // cylinder step); 1 = cooperatively (the runtime guarantees every tile
+    // co-resident or refuses the launch, which then takes the launch-per-pass
+    // path); the bound of a neighbour poll in ticks of the 100 MHz clock
+    // (0: 20 s)
+    int persist_coop = 0;
     unsigned long long persist_poll = 0;
 };
 // The current device's failure counter of persistent solves (a device int,
 // process-wide, allocated on first use): a solve whose poll expired adds 1;
 // cfd_persistent_status reads and clears it.  nullptr if allocation failed.
 int *persist_fail_word();
+// k_energy_mean_mb's scratch for the current device and stream s (a zeroed
+// counter word + kEnergyBlocks doubles, kept for the process's life); nullptr
+// if allocation failed
+unsigned *energy_scratch(hipStream_t s);
 // Launch a persistent kernel: cooperatively when tuning().persist_coop (0 if
 // the runtime refuses the size: every tile could not be co-resident -- the
 // error is cleared and the caller takes its launch-per-pass path), else a

@@ -484,7 +484,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) voi
         const uint32_t o = rofs(i);
         pstv<T, VEC>(uo, rus, o);
         pstv<T, VEC>(vo, rvs, o);
-        if (SUPG && a.tau) pstv<T, VEC>(to, rt, o);
+        if (a.tau) pstv<T, VEC>(to, rt, o);  // zeros without SUPG (v5.py:292)
         Um = Uc;
         Vm = Vc;
         Uc = Up;

@@ -282,7 +282,9 @@ def predictor_fused(u, v, dx, dy, dt, nu_eff, use_supg=True, u_star=None, v_star
     tau_mode: "exact" (the reference's NumPy scalar `**`: glibc powf / pow,
     bit-exact), "fast" (the compiled reference's fastmath x*x / sqrt, within
     1e-6 relative L-inf), or None (the calling thread's current setting,
-    cfd_set_predictor2d_tau_mode; "exact" unless changed)."""
+    cfd_set_predictor2d_tau_mode; "exact" unless changed).  Without SUPG a
+    given tau is filled with zeros (the reference's never-assigned
+    np.zeros, v5.py:292)."""
     ny, nx = _shape2d(u)
     if tau_mode is not None:
         if tau_mode not in TAU_MODES:
@@ -294,7 +296,7 @@ def predictor_fused(u, v, dx, dy, dt, nu_eff, use_supg=True, u_star=None, v_star
         tau = torch.empty_like(u)
     nu_a, nu_s = _nu(nu_eff, u.dtype)
     call(_fields("cfd_predictor2d", u, v, us, vs, tau), ptr(u), ptr(v), ptr(nu_a), nu_s, ptr(us), ptr(vs),
-         ptr(tau) if use_supg else None, ny, nx, float(dx), float(dy), _dt_arg(dt, u.dtype), int(bool(use_supg)),
+         ptr(tau), ny, nx, float(dx), float(dy), _dt_arg(dt, u.dtype), int(bool(use_supg)),
          stream_handle())
     return us, vs, tau
 

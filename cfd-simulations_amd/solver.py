@@ -317,8 +317,7 @@ class OptimizedTurbulentSolver:
         nu_eff = self._np(self._np(cfg.nu) + self._np(0.0)) + self._np(cfg.artificial_viscosity)
         K.predictor_fused(self.u, self.v, cfg.dx, cfg.dy, dt, nu_eff, cfg.use_supg,
                           u_star=self.u_star, v_star=self.v_star, tau=self.tau_supg, tau_mode=cfg.supg_tau)
-        if not cfg.use_supg:
-            self.tau_supg.zero_()
+        # (without SUPG the predictor writes tau_supg's zeros itself)
         force_strength = min(1.0, self.step / cfg.initial_steps)
         # apply_boundary_conditions then apply_ibm_fast (v5.py:405-407), one launch
         self._bc_ibm(self.u_star, self.v_star, force_strength)

@@ -165,7 +165,9 @@ int cfd_laplacian2d_f32(const float *phi, const float *nu_eff, float nu_eff_scal
                         int ny, int nx, double dx, double dy, void *stream);
 /* Fused predictor, v5.py:388-403: tau (SUPG), conv_u/v, lap_u/v and
  *   u_star = u + dt*(-conv_u + lap_u),  v_star = v + dt*(-conv_v + lap_v)
- * in one pass over u, v.  tau may be NULL (not stored). */
+ * in one pass over u, v.  tau may be NULL (not stored); with use_supg = 0
+ * it is filled with zeros (the reference never assigns its np.zeros tau
+ * without SUPG, v5.py:292). */
 int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, float nu_eff_scalar,
                         float *u_star, float *v_star, float *tau, int ny, int nx,
                         double dx, double dy, float dt, int use_supg, void *stream);
@@ -471,11 +473,13 @@ int cfd_set_small2d_gs_persistent(int mode);
  * 4, 6, 8.  Its exchange ring lives in a library-owned device buffer. */
 int cfd_set_small2d_jacobi_persistent(int on, int sweeps_per_block);
 /* Both persistent small-grid solves (the GS above and the Jacobi below) are
- * launched cooperatively by default (cooperative = 1): the HIP runtime then
- * guarantees that every tile is resident at once or refuses the launch, and a
- * refused launch takes the launch-per-pass path (same bits).  cooperative = 0:
- * a plain launch after the library's own occupancy check (which assumes the
- * device is otherwise idle).  poll_ticks bounds each wait of a tile for its
+ * plain launches after the library's own occupancy check by default
+ * (cooperative = 0, r05: the check assumes the device is otherwise idle; a
+ * tile queued behind other work only waits, one-way, up to the poll bound).
+ * cooperative = 1: the HIP runtime guarantees that every tile is resident at
+ * once or refuses the launch, and a refused launch takes the launch-per-pass
+ * path (same bits); it costs ~30 us of queue gap per solve (v5 cylinder step
+ * 0.76 -> 0.79 ms).  poll_ticks bounds each wait of a tile for its
  * neighbours, in ticks of the 100 MHz device clock (0 = the default, 20 s; a
  * tiny value forces the failure path in tests).  A solve whose wait expired
  * leaves phi all NaN, the GS's *iters_done = -1, and counts one failure for

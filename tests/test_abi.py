@@ -41,11 +41,14 @@ def test_library_identifies_itself():
     assert L.cfd_abi_version() == _lib.ABI_VERSION
     assert L.cfd_device_arch() == b"gfx950"
     assert L.cfd_rbgs_workspace_bytes(1500) >= 4 * 1500
-    # two row-major float64 fields, or two float32 fields in the skewed layout
-    # of the f32 sweep (64-row blocks x (nx + 63) diagonals x 64), the larger
+    # two row-major float64 fields, or three float32 fields (div, phi1, phi2)
+    # in the skewed layout of the f32 sweep (64-row blocks x ceil((nx + 63) / 4)
+    # groups of 4 diagonals x 64 rows x 4), the larger
+    def skew(ny, nx):
+        return 3 * 4 * ((ny - 2 + 63) // 64) * ((nx + 63 + 3) // 4) * 256
     assert L.cfd_clean_divergence_workspace_bytes(180, 600) == 2 * 8 * 180 * 600
-    assert L.cfd_clean_divergence_workspace_bytes(3, 64) == 2 * 4 * 1 * (64 + 63) * 64
-    assert L.cfd_clean_divergence_workspace_bytes(67, 3) == 2 * 4 * 2 * (3 + 63) * 64
+    assert L.cfd_clean_divergence_workspace_bytes(3, 64) == skew(3, 64) == 98304
+    assert L.cfd_clean_divergence_workspace_bytes(67, 3) == skew(67, 3)
     assert L.cfd_clean_divergence_workspace_bytes(2, 5000) == 2 * 8 * 2 * 5000
 
 

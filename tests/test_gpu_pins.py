@@ -421,8 +421,9 @@ def test_jacobi2d_persistent_streams_and_threads():
 
 @pytest.mark.parametrize("cooperative", [1, 0])
 def test_persistent_cooperative_and_plain_launch_bitexact(cooperative):
-    """Both persistent small-grid solves, launched cooperatively (the default)
-    and plainly, on the cylinder grid: bit-exact, and no failure counted."""
+    """Both persistent small-grid solves, launched plainly (the default since
+    r05) and cooperatively, on the cylinder grid: bit-exact, and no failure
+    counted."""
     call("cfd_set_persistent_launch", cooperative, 0)
     shape = (180, 600)
     rng = np.random.default_rng(21 + cooperative)

@@ -111,6 +111,25 @@ def test_predictor_shapes_bitexact(shape, rows, vec, supg, nu_array):
     _check(u, v, nu, c, np.float32(2e-5), supg, nu_array)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_predictor_without_supg_zeroes_tau(dtype, variant):
+    """Without SUPG the predictor fills a given tau with zeros -- the
+    reference's np.zeros tau_supg, never assigned without SUPG (v5.py:292) --
+    so the solver needs no separate fill; u*, v* are unchanged by it."""
+    ny, nx = 37, 260
+    c, nu = _cfg(ny, nx)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    u = (torch.rand((ny, nx), generator=g, device=DEV) * 2 - 1).to(dtype)
+    v = (torch.rand((ny, nx), generator=g, device=DEV) * 2 - 1).to(dtype)
+    call("cfd_set_predictor2d_config", variant, 0, 0)
+    tau = torch.full((ny, nx), float("nan"), dtype=dtype, device=DEV)
+    us, vs, t = K.predictor_fused(u, v, c.dx, c.dy, 2e-5, float(nu), False, tau=tau)
+    assert t is tau and bool((tau == 0).all())
+    us0, vs0, t0 = K.predictor_fused(u, v, c.dx, c.dy, 2e-5, float(nu), False)
+    assert t0 is None and torch.equal(us, us0) and torch.equal(vs, vs0)
+
+
 def _near_midpoint(rng, n):
     """float32 values whose exact square lies within twice the fast-path
     window of a float rounding midpoint."""
