@@ -30,6 +30,8 @@ PROTOTYPES = {
     "cfd_device_arch": (c_char_p, []),
     "cfd_jacobi2d_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
     "cfd_jacobi2d_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
+    "cfd_jacobi2d_zero_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
+    "cfd_jacobi2d_zero_f64": (c_int, [P, P, P, P, P, c_int, c_int, c_double, c_float, c_int, c_int, P, P]),
     "cfd_jacobi3d_f32": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_double, c_float, c_int, c_int, P,
                                  P]),
     "cfd_jacobi3d_zero_f32": (c_int, [P, P, P, P, c_int, c_int, c_int, c_double, c_float, c_int, P]),

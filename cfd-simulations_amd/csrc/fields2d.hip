@@ -248,385 +248,8 @@ __global__ __launch_bounds__(1024) void k_lex_gs_sweep(float *__restrict__ phi,
     }
 }
 
-// The same sweep with its old-value stream kept in flight and no per-step
-// barrier.  In the kernel above every step drains the memory queue
-// (__syncthreads waits vmcnt(0), and the register queue's moves wait on their
-// loads), so each of the ~1000 dependent steps pays a full memory latency.
-// Here:
-//  * the old values travel memory -> LDS by LDS-DMA (buffer_load_dwordx4 ...
-//    lds), LX blocks of 4 steps ahead, into a ring ring[LX][field][thread] of
-//    float4: lane t's window for a block is 4 consecutive columns of its own
-//    row (E, div), of the row below (N: lane 63 and the last row only) and of
-//    the row above (S: thread 0 only); other lanes get an out-of-range offset
-//    and cost no memory access;
-//  * S inside a wave is lane t-1's output of the previous step, by DPP; N is
-//    lane t+1's E (old values), by DPP;
-//  * wave k runs kLexLag steps behind wave k-1 and takes the row above from
-//    wave k-1's lane-63 outputs in a small LDS ring written at least one
-//    barrier phase earlier, so the waves synchronise once per kLexLag steps;
-//  * results are written once per block: one dwordx4 store for a lane whose 4
-//    columns are all interior, single-dword stores at the row ends.
-// Every memory operation of the step loop is inline asm in a fixed order, so
-// the wait for block b is an exact count: after block b's 4 DMAs come that
-// block's 5 stores and (LX-1) x (4 DMAs + 5 stores).  Needs n*4 < 2^31 (32-bit
-// buffer offsets; kOob = 2^31 is the out-of-range offset).
-constexpr int kLexLX = 4;    // blocks of prefetch (16 steps; 28 measured the same: the loop is issue-bound)
-constexpr int kLexLag = 16;  // steps between waves = steps per barrier phase
-constexpr int kLexRing = 4 * kLexLag;  // lane-63 output ring per wave (steps)
-__device__ inline void lex_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-__device__ inline void buf_store_x4(float4 v, uint32_t ofs, v4i32 rs) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v d = {v.x, v.y, v.z, v.w};
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" ::"v"(d), "v"(ofs), "s"(rs) : "memory");
-}
-__device__ inline void buf_store_x1(float v, uint32_t ofs, v4i32 rs) {
-    asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(ofs), "s"(rs) : "memory");
-}
-
-// buffer_load_dwordx4 ... lds with the LDS destination given as a (uniform) byte address
-__device__ inline void lex_dma_x4(v4i32 rs, uint32_t ofs, uint32_t lds_addr) {
-    int saved;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %1\n\t"
-        "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(saved)
-        : "s"(lds_addr), "v"(ofs), "s"(rs)
-        : "memory");
-}
-
-template <int LX>
-__global__ __launch_bounds__(512) void k_lex_gs_sweep_dma(float *__restrict__ phi,
-                                                          const float *__restrict__ div, int ny,
-                                                          int nx, float cx, float cy, float cd) {
-    extern __shared__ float4 lex_lds[];  // ring[LX][4][nt] float4, then below[nwaves][kLexRing] float
-    const int t = threadIdx.x, nt = blockDim.x, lane = t & 63, wv = t >> 6;
-    float4 *ring = lex_lds;
-    float *below = reinterpret_cast<float *>(lex_lds + LX * 4 * nt);  // wave k's lane-63 outputs by step
-    const long n = (long)ny * nx;
-    const v4i32 rp = buf_rsrc4(phi, (uint32_t)(n * 4)), rd = buf_rsrc4(div, (uint32_t)(n * 4));
-    const int imax = ny - 2, jmax = nx - 2;
-    for (int b0 = 1; b0 <= imax; b0 += nt) {
-        __threadfence();  // the previous band's rows are final and visible
-        __syncthreads();  // (and its DMAs have landed: the fence drained vmcnt)
-        const int nrows = min(nt, imax - b0 + 1);
-        const int nwaves = (nrows + 63) / 64;
-        const int i = b0 + t;
-        const bool rowok = t < nrows;
-        const uint32_t rowc = (uint32_t)(rowok ? i : 0) * (uint32_t)nx;
-        const bool nmem = lane == 63 || t == nrows - 1;
-        const int lag = wv * kLexLag;  // this wave's step = time - lag
-        // Time block tb covers this wave's steps s0 = 4 tb - lag .. s0 + 3, lane
-        // t's columns j0 = jb + 4 tb .. j0 + 3.  Every per-lane byte offset is
-        // a band constant plus 16 tb (32-bit; a window outside the row reads
-        // other rows' cells, which no active step uses, or lies past the
-        // buffer and reads zeros; kOob + 16 tb stays out of range).
-        const int jb = 1 - t - lag;
-        const uint32_t oE = rowok ? (rowc + jb + 1) * 4u : kOob;
-        const uint32_t oD = rowok ? (rowc + jb) * 4u : kOob;
-        const uint32_t oN = rowok && nmem ? (rowc + nx + jb) * 4u : kOob;
-        const uint32_t oS = rowok && t == 0 ? (rowc - nx + jb) * 4u : kOob;
-        const uint32_t oW = (rowc + jb) * 4u;
-        const uint32_t la = (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(ring + wv * 64));
-        const uint32_t fstride = (uint32_t)nt * 16u;  // bytes per ring field
-        auto issue = [&](int tb, int slot) {  // block tb's windows into ring slot
-            const uint32_t d = 16u * (uint32_t)tb, m = la + (uint32_t)slot * 4u * fstride;
-            lex_dma_x4(rp, oE + d, m);
-            lex_dma_x4(rd, oD + d, m + fstride);
-            lex_dma_x4(rp, oN + d, m + 2 * fstride);
-            lex_dma_x4(rp, oS + d, m + 3 * fstride);
-        };
-        const float w0 = rowok ? phi[rowc] : 0.f;  // phi(i, 0): W of column 1
-        wait_vmcnt<0>();  // w0 landed: the waitcnt pass would otherwise drain at every block
-#pragma unroll
-        for (int p = 0; p < LX; ++p) {
-            issue(p, p);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) buf_store_x1(0.f, kOob, rp);  // the loop's store slots
-        }
-        float w = w0, vprev = 0.f;
-        // time blocks: the last wave's last step, rounded up to whole phases
-        const int tsteps = nrows - 1 + jmax + (nwaves - 1) * kLexLag;
-        const int nblocks = (tsteps + kLexLag - 1) / kLexLag * (kLexLag / 4);
-        const float *above = below + (wv - 1) * kLexRing;  // wave k-1's ring (wv >= 1)
-        for (int tb = 0; tb < nblocks; ++tb) {
-            const int s0 = 4 * tb - lag, slot = tb % LX, j0 = jb + 4 * tb;
-            wait_vmcnt<5 + 9 * (LX - 1)>();
-            const float4 *rb = ring + (size_t)slot * 4 * nt + t;
-            const float4 e4 = rb[0], d4 = rb[nt], n4 = rb[2 * nt], s4 = rb[3 * nt];
-            float sa[4] = {s4.x, s4.y, s4.z, s4.w};
-            if (lane == 0 && wv > 0) {  // row above = wave k-1's lane 63, steps s0-1 .. s0+2
-#pragma unroll
-                for (int k = 0; k < 4; ++k) sa[k] = above[(s0 - 1 + k) & (kLexRing - 1)];
-            }
-            const float ea[4] = {e4.x, e4.y, e4.z, e4.w}, da[4] = {d4.x, d4.y, d4.z, d4.w};
-            const float na[4] = {n4.x, n4.y, n4.z, n4.w};
-            bool act[4];
-            float res[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                act[k] = rowok && (uint32_t)(j0 + k - 1) < (uint32_t)jmax;
-                const float E = ea[k];
-                const float nup = dpp_from_upper(E);      // lane t+1's E: old phi(i+1, j)
-                const float sup = dpp_from_lower(vprev);  // lane t-1 at step s-1: new phi(i-1, j)
-                const float S = lane == 0 ? sa[k] : sup;
-                const float N = nmem ? na[k] : nup;
-                const float a = cx * (E + w);
-                const float bb = cy * (N + S);
-                const float v = ((a + bb) - da[k]) * cd;
-                w = act[k] ? v : w;
-                vprev = v;
-                res[k] = v;
-            }
-            if (lane == 63) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) below[wv * kLexRing + ((s0 + k) & (kLexRing - 1))] = res[k];
-            }
-            issue(tb + LX, slot);
-            const uint32_t o = oW + 16u * (uint32_t)tb;
-            const bool full = act[0] && act[3];
-            buf_store_x4(make_float4(res[0], res[1], res[2], res[3]), full ? o : kOob, rp);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) buf_store_x1(res[k], !full && act[k] ? o + 4u * k : kOob, rp);
-            if ((tb + 1) % (kLexLag / 4) == 0) lex_lds_barrier();
-        }
-    }
-}
-// The same sweep in 16-step chunks whose inner loop runs from registers.
-//  * A lane's old values for a chunk -- 16 consecutive columns of its own row
-//    (E) and of div -- travel memory -> LDS by LDS-DMA (buffer_load_dwordx4
-//    ... lds), R - 1 chunks ahead, into a per-wave ring; at the chunk's start
-//    the lane reads its 16 + 16 values into registers (8 ds_read_b128).  The
-//    windows are skewed per lane by its row, so step k of a chunk is register
-//    k in every lane (compile-time indices).
-//  * In a wave, S is lane t-1's previous output and N lane t+1's E, each ONE
-//    DPP move whose `old` operand supplies the wave-edge lane's value: thread
-//    0's row above and lane 63's row below, read from LDS copies of those rows
-//    (taken at the band's start; the row below is still old then) at uniform
-//    addresses.  A lane past the band's last row loads E from the boundary
-//    row ny-1, which makes the last row's N a DPP too.
-//  * Wave k runs one chunk behind wave k-1 and takes its row above from wave
-//    k-1's lane-63 outputs in a 4-chunk LDS ring; one barrier per chunk.
-//  * Every memory operation of the loop is inline asm (8 DMAs, 4 x4 stores,
-//    and at row ends 16 single-word stores), so the wait for a chunk's DMAs is
-//    an exact vmcnt that leaves the later chunks' DMAs in flight.
-// ~13 VALU per step (the LDS-DMA kernel above: ~40).  Up to 256 rows per band.
-#ifndef CFD_LEX_TSTORE  // results stored transposed through LDS (0: per-lane row stores)
-#define CFD_LEX_TSTORE 1
-#endif
-#ifndef CFD_LEX_ABL  // measurement aid only: 1 no barrier, 2 no stores, 4 no DMA wait, 16 no arithmetic
-#define CFD_LEX_ABL 0
-#endif
-constexpr int kLexC = 16;                     // steps per chunk
-constexpr int kLexR = 4;                      // chunks in the DMA ring
-constexpr int kLexPadL = 16, kLexPadR = 32;   // LDS row copy padding (floats)
-constexpr size_t kLexRegLdsMax = 160 * 1024;  // LDS the register sweep may take
-size_t lex_reg_lds_bytes(int nwaves, int nx) {
-    return (size_t)kLexR * 2 * 4 * 64 * nwaves * sizeof(float4) +
-           (size_t)(nwaves + 1) * (size_t)(nx + kLexPadL + kLexPadR) * sizeof(float);
-}
-__global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ phi,
-                                                         const float *__restrict__ div, int ny, int nx,
-                                                         float cx, float cy, float cd) {
-    __shared__ __attribute__((aligned(16))) float below[4][4 * kLexC];  // wave w's lane-63 outputs by band step
-    // [kLexR][2 fields][4 quads][nt lanes] float4, then (waves + 1) row copies:
-    // [0] the row above the band, [1 + w] the row below wave w's lanes
-    extern __shared__ float4 lex_ring[];
-    const int t = threadIdx.x, nt = blockDim.x, lane = t & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int n = ny * nx;
-    const int rs = nx + kLexPadL + kLexPadR;  // LDS row stride
-    float *rows = reinterpret_cast<float *>(lex_ring + (size_t)kLexR * 8 * nt);
-    const v4i32 rp = buf_rsrc4(phi, (uint32_t)(n * 4)), rd = buf_rsrc4(div, (uint32_t)(n * 4));
-    const int imax = ny - 2, jmax = nx - 2;
-    const uint32_t la = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(lex_ring + wv * 64));
-    const uint32_t qstride = (uint32_t)nt * 16u;  // bytes per (slot, field, quad) row
-    for (int b0 = 1; b0 <= imax; b0 += nt) {
-        __threadfence();  // the previous band's rows are final and visible
-        __syncthreads();
-        const int nrows = min(nt, imax - b0 + 1);
-        const int nwaves = (nrows + 63) / 64;
-        for (int r = 0; r <= nwaves; ++r) {
-            const int y = r == 0 ? b0 - 1 : min(b0 + 64 * r, ny - 1);
-            for (int x = t; x < rs; x += nt) {
-                const int col = x - kLexPadL;
-                rows[r * rs + x] = col >= 0 && col < nx ? phi[(size_t)y * nx + col] : 0.f;
-            }
-        }
-        const int i = b0 + t;
-        const bool rowok = t < nrows;
-        const int lag = kLexC * wv;
-        const int jb = 1 - lag - t;  // this lane's column at chunk 0, step 0
-        const int rowc = (i <= ny - 1 ? i : 0) * nx;
-        const uint32_t oE = i <= ny - 1 ? (uint32_t)(rowc + jb + 1) * 4u : kOob;
-        const uint32_t oD = rowok ? (uint32_t)(rowc + jb) * 4u : kOob;
-        const uint32_t oW = (uint32_t)(rowc + jb) * 4u;
-        (void)oW;
-        const float w0 = rowok ? phi[rowc] : 0.f;  // phi(i, 0): W of column 1
-        wait_vmcnt<0>();
-        __syncthreads();  // the row copies are in LDS
-        auto issue = [&](int c, int slot) {  // chunk c's windows into ring slot
-            const uint32_t d = 64u * (uint32_t)c;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                lex_dma_x4(rp, oE + d + 16u * q, la + (uint32_t)((slot * 2 + 0) * 4 + q) * qstride);
-                lex_dma_x4(rd, oD + d + 16u * q, la + (uint32_t)((slot * 2 + 1) * 4 + q) * qstride);
-            }
-        };
-        // chunks: up to the last lane's last step in chunk time (wave w runs
-        // band step s at time s + lag), rounded up to whole rounds of kLexR
-        const int nchunks = ((nrows - 2 + jmax + kLexC * (nwaves - 1)) / kLexC + kLexR) / kLexR * kLexR;
-#pragma unroll
-        for (int r = 0; r < kLexR; ++r) {
-            issue(r, r);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) buf_store_x1(0.f, kOob, rp);  // the loop's x4-store slots
-        }
-        float w = w0, vprev = 0.f;
-        const float *above = rows + kLexPadL;                 // row b0 - 1
-        const float *under = rows + (1 + wv) * rs + kLexPadL;  // the row below lane 63
-        for (int c0 = 0; c0 < nchunks; c0 += kLexR) {
-#pragma unroll
-            for (int r = 0; r < kLexR; ++r) {
-                const int c = c0 + r;
-                // this chunk's DMAs: 12 (kLexR - 1) memory ops were issued after them
-#if !(CFD_LEX_ABL & 4)
-                wait_vmcnt<12 * (kLexR - 1)>();
-#endif
-                float Er[kLexC], Dr[kLexC];
-                const float4 *slot = lex_ring + (size_t)r * 8 * nt + t;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 e = slot[q * nt], d = slot[(4 + q) * nt];
-                    Er[4 * q] = e.x; Er[4 * q + 1] = e.y; Er[4 * q + 2] = e.z; Er[4 * q + 3] = e.w;
-                    Dr[4 * q] = d.x; Dr[4 * q + 1] = d.y; Dr[4 * q + 2] = d.z; Dr[4 * q + 3] = d.w;
-                }
-                // the wave-edge lanes' neighbours (uniform addresses): thread
-                // 0's S (wave 0: the row above; else wave k-1's lane 63 one band
-                // step earlier) and lane 63's N (the row below)
-                float S0[kLexC], N63[kLexC];
-                if (wv == 0) {
-                    const int j0 = min(max(1 + kLexC * c, -kLexPadL), nx);
-#pragma unroll
-                    for (int k = 0; k < kLexC; ++k) S0[k] = above[j0 + k];
-                } else {
-                    const int base = (kLexC * c - lag) & (4 * kLexC - 1);
-                    const float *ab = below[wv - 1];
-                    S0[0] = ab[(base - 1) & (4 * kLexC - 1)];
-#pragma unroll
-                    for (int q = 0; q < kLexC / 4; ++q) {
-                        const float4 v4 = *reinterpret_cast<const float4 *>(ab + base + 4 * q);
-                        if (4 * q + 1 < kLexC) S0[4 * q + 1] = v4.x;
-                        if (4 * q + 2 < kLexC) S0[4 * q + 2] = v4.y;
-                        if (4 * q + 3 < kLexC) S0[4 * q + 3] = v4.z;
-                        if (4 * q + 4 < kLexC) S0[4 * q + 4] = v4.w;
-                    }
-                }
-                {
-                    const int j0 = min(max(1 - lag - (64 * wv + 63) + kLexC * c, -kLexPadL), nx);  // lane 63's column
-#pragma unroll
-                    for (int k = 0; k < kLexC; ++k) N63[k] = under[j0 + k];
-                }
-                const int jc = jb + kLexC * c;
-                float out[kLexC];
-                bool act[kLexC];
-#pragma unroll
-                for (int k = 0; k < kLexC; ++k) {
-                    const float E = Er[k];
-                    const float N = __int_as_float(__builtin_amdgcn_update_dpp(
-                        __float_as_int(N63[k]), __float_as_int(E), 0x130, 0xf, 0xf, false));  // wave_shl:1
-                    const float S = __int_as_float(__builtin_amdgcn_update_dpp(
-                        __float_as_int(S0[k]), __float_as_int(vprev), 0x138, 0xf, 0xf, false));  // wave_shr:1
-#if CFD_LEX_ABL & 16
-                    const float v = E + Dr[k] + N + S;
-#else
-                    const float a = cx * (E + w);
-                    const float bb = cy * (N + S);
-                    const float v = ((a + bb) - Dr[k]) * cd;
-#endif
-                    act[k] = rowok && (uint32_t)(jc + k - 1) < (uint32_t)jmax;
-                    w = act[k] ? v : w;
-                    vprev = v;
-                    out[k] = v;
-                }
-                if (lane == 63) {
-                    float *mine = below[wv] + ((kLexC * c - lag) & (4 * kLexC - 1));
-#pragma unroll
-                    for (int q = 0; q < kLexC / 4; ++q)
-                        *reinterpret_cast<float4 *>(mine + 4 * q) =
-                            make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
-                }
-                // results: one 16-byte store per 4 columns all inside the row,
-                // single words where a group is cut by a row end
-                bool partial = false;
-#if CFD_LEX_TSTORE && !(CFD_LEX_ABL & 2)
-                // transposed through this wave's quarter of the ring slot just
-                // read (free until its refill below): lane l stores row
-                // 16 q + (l & 15), columns 4 (l >> 4) .. + 3 of the chunk, so
-                // a store instruction writes 16 rows x 64 contiguous bytes
-                // instead of 64 rows x 16 bytes (the scattered stores cost
-                // ~23 us of a 98 us sweep: CFD_LEX_ABL=2)
-                {
-                    float4 *tw = lex_ring + (size_t)r * 8 * nt + 64 * wv;
-#pragma unroll
-                    for (int q = 0; q < kLexC / 4; ++q)
-                        tw[q * nt + lane] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
-                    const int g = lane >> 4;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int rho = 16 * q + (lane & 15), tr = 64 * wv + rho;
-                        const float4 v4 = tw[g * nt + rho];
-                        const int j0 = 1 - lag - tr + kLexC * c + 4 * g;  // first column of these 4
-                        const bool rok = tr < nrows;
-                        bool ae[4];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) ae[e] = rok && (uint32_t)(j0 + e - 1) < (uint32_t)jmax;
-                        const bool full = ae[0] && ae[3];
-                        const uint32_t o = (uint32_t)((b0 + tr) * nx + j0) * 4u;
-                        buf_store_x4(v4, full ? o : kOob, rp);
-                        const bool part = !full && (ae[0] || ae[1] || ae[2] || ae[3]);
-                        if (__any(part)) {
-                            buf_store_x1(v4.x, part && ae[0] ? o : kOob, rp);
-                            buf_store_x1(v4.y, part && ae[1] ? o + 4u : kOob, rp);
-                            buf_store_x1(v4.z, part && ae[2] ? o + 8u : kOob, rp);
-                            buf_store_x1(v4.w, part && ae[3] ? o + 12u : kOob, rp);
-                        }
-                    }
-                    (void)partial;
-                }
-#elif !(CFD_LEX_ABL & 2)
-#pragma unroll
-                for (int q = 0; q < kLexC / 4; ++q) {
-                    const bool full = act[4 * q] && act[4 * q + 3];
-                    partial = partial || (!full && (act[4 * q] || act[4 * q + 1] || act[4 * q + 2] || act[4 * q + 3]));
-                    buf_store_x4(make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]),
-                                 full ? oW + 64u * c + 16u * q : kOob, rp);
-                }
-                if (__any(partial)) {
-#pragma unroll
-                    for (int k = 0; k < kLexC; ++k) {
-                        const bool full = act[k & ~3] && act[(k & ~3) + 3];
-                        buf_store_x1(out[k], act[k] && !full ? oW + 64u * c + 4u * k : kOob, rp);
-                    }
-                }
-#else
-#pragma unroll
-                for (int q = 0; q < kLexC / 4; ++q) buf_store_x1(0.f, kOob, rp);
-#endif
-                issue(c + kLexR, r);
-#if !(CFD_LEX_ABL & 1)
-                lex_lds_barrier();
-#endif
-            }
-        }
-    }
-}
-
-// The sweep on a SKEWED copy of phi and div (r05, the default): the staged
-// kernels below keep phi row-major, so the diagonal a wave touches per step
+// The sweep on a SKEWED copy of phi and div (r05, the default): the r02-r04
+// staged kernels kept phi row-major, so the diagonal a wave touches per step
 // (lane l: row r0 + l, column d - l) is 64 cache lines, and a CU's vector
 // memory path moves about one line per clock -- measured 90-100 us per
 // 600-column sweep, several times the ~47-cycle dependent chain per step
@@ -652,6 +275,7 @@ __global__ __launch_bounds__(256) void k_lex_gs_sweep_reg(float *__restrict__ ph
 //    (the two rows from other blocks by lanes 63 and 0 alone); results leave
 //    four steps at a time (0 at the zero side columns and the padding).
 // Same arithmetic and order as the serial loop: bit-identical.
+constexpr size_t kLexLdsMax = 160 * 1024;  // LDS a sweep workgroup may take
 constexpr int kSkewWaves = 4;  // waves per band: at one wave per SIMD the chain, not the memory path, sets the pace
 #ifndef CFD_SKEW_EXP
 #define CFD_SKEW_EXP 0  // timing experiments only (wrong results): 1 no stores, 2 no loads, 4 no DPP
@@ -664,10 +288,6 @@ size_t lex_skew_floats(int ny, int nx) { return (size_t)lex_skew_blocks(ny) * (s
 // c = -63 .. nx + 76, 16 B aligned
 constexpr int lex_skew_rsl(int nx) { return (nx + 160 + 3) & ~3; }
 size_t lex_skew_lds_bytes(int nw, int nx) { return (size_t)nw * lex_skew_rsl(nx) * sizeof(float); }
-bool lex_skew_on() {
-    static const bool on = !getenv("CFD_LEX_STAGED");  // A/B knob: the round-4 staged sweeps
-    return on;
-}
 __device__ inline size_t skew_at(int i, int j, int dg) {  // interior row i >= 1, column j >= 0
     const int m = (i - 1) >> 6, l = (i - 1) & 63, d = j + l;
     return (((size_t)m * dg + (d >> 2)) * 64 + l) * 4 + (d & 3);
@@ -777,7 +397,10 @@ __global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_bas
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(phi_base, 0, phi_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rd =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(div_s), 0, bytes, 0x00020000);
-    const int nq = (nx + 62 + 15) >> 4;  // steps d = 0 .. nx + 61 (lane 63's last column), 16 per chunk
+    // steps d = 0 .. 4 DG - 1, 16 per chunk: every slot of the block is stored
+    // (lane 63's last interior column is at d = nx + 61, its zero side column
+    // at nx + 62, and the padding up to 4 DG - 1 is written too)
+    const int nq = (DG + 3) >> 2;
     const int nc = (nq + R / 4 - 1) / (R / 4);  // loop iterations of 4 R steps
     for (int b0 = 0; b0 < nb; b0 += nw) {
         __threadfence();  // the band before is final and visible (a band's first wave reads its last row)
@@ -948,10 +571,6 @@ __global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_bas
         else
             run(F0{});
     }
-}
-
-size_t lex_dma_lds_bytes(int nt, int lx) {
-    return (size_t)lx * 4 * nt * sizeof(float4) + (size_t)(nt / 64) * kLexRing * sizeof(float);
 }
 
 // u[1:-1,1:-1] -= grad_x[1:-1,1:-1] (no dt: v5.py:255-256)
@@ -1323,7 +942,7 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
     const double dx2_inv = 1.0 / (dx * dx), dy2_inv = 1.0 / (dy * dy);
     const double denom_inv = 1.0 / (2.0 * (dx2_inv + dy2_inv));
     const float cx = (float)(0.5 / dx), cy = (float)(0.5 / dy);
-    if (ny > 2 && nx > 2 && 2 * lex_skew_floats(ny, nx) * 4 < ((size_t)1 << 31) && lex_skew_on()) {
+    if (ny > 2 && nx > 2 && 2 * lex_skew_floats(ny, nx) * 4 < ((size_t)1 << 31)) {
         // div and two phi buffers in the skewed layout (k_lex_gs_skew): the
         // first sweep starts from phi = 0 (np.zeros_like, v5.py:242) by
         // reading nothing; at iterations == 2 the second sweep writes the
@@ -1332,7 +951,7 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
         float *div_s = reinterpret_cast<float *>(ws);
         float *phi1 = div_s + F, *phi2 = phi1 + F;
         const int pbytes = (int)(2 * F * sizeof(float));
-        const size_t ldsmax = kLexRegLdsMax - 1024;
+        const size_t ldsmax = kLexLdsMax - 1024;
         static const int wmax = [] {
             const char *e = getenv("CFD_LEX_SKEW_WAVES");  // A/B knob: waves per band (1 .. 4)
             const int v = e ? atoi(e) : kSkewWaves;
@@ -1378,49 +997,9 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
     for (int it = 0; it < iterations; ++it) {
         hipLaunchKernelGGL(k_divergence, grid2d(ny, nx), dim3(256), 0, s, u, v, div, ny, nx, cx, cy,
                            (float *)nullptr);
-        if (ny > 2 && nx > 2) {
-            // one thread per row of a band: as many waves as rows (idle
-            // waves would only add barrier traffic to every step)
-            if (n * 4 < ((size_t)1 << 31)) {
-                // bands of at most 256 rows, one wave per 64 rows, with LDS
-                // copies of (waves + 1) rows
-                const int ntr = ny - 2 >= 256 ? 256 : 64 * ceil_div(ny - 2, 64);
-                const size_t rows_lds = lex_reg_lds_bytes(ntr / 64, nx);
-                if (rows_lds + 1024 <= kLexRegLdsMax && !getenv("CFD_LEX_DMA")) {
-                    static bool attr_reg = false;
-                    if (!attr_reg) {
-                        CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lex_gs_sweep_reg),
-                                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                          (int)(kLexRegLdsMax - 1024)));
-                        attr_reg = true;
-                    }
-                    hipLaunchKernelGGL(k_lex_gs_sweep_reg, dim3(1), dim3(ntr), rows_lds, s, phi, div, ny, nx,
-                                       (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
-                    goto swept;
-                }
-                // bands of at most 512 rows (the ring's LDS), one wave per 64 rows
-                static const int band = [] {
-                    const char *e = getenv("CFD_LEX_BAND");  // rows per band (A/B knob)
-                    const int b = e ? atoi(e) : 512;
-                    return b >= 64 && b <= 512 ? b / 64 * 64 : 512;
-                }();
-                const int nt = ny - 2 >= band ? band : 64 * ceil_div(ny - 2, 64);
-                const size_t lds = lex_dma_lds_bytes(nt, kLexLX);
-                static bool attr = false;
-                if (!attr) {
-                    CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lex_gs_sweep_dma<kLexLX>),
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)lex_dma_lds_bytes(512, kLexLX)));
-                    attr = true;
-                }
-                hipLaunchKernelGGL(k_lex_gs_sweep_dma<kLexLX>, dim3(1), dim3(nt), lds, s, phi, div, ny, nx,
-                                   (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
-            } else {
-                hipLaunchKernelGGL(k_lex_gs_sweep, dim3(1), dim3(ny - 2 >= 1024 ? 1024 : 64 * ceil_div(ny - 2, 64)), 0, s, phi, div, ny, nx,
-                                   (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
-            }
-        }
-    swept:
+        if (ny > 2 && nx > 2)  // past the skewed layout's 2^31-byte offsets: the plain wavefront
+            hipLaunchKernelGGL(k_lex_gs_sweep, dim3(1), dim3(ny - 2 >= 1024 ? 1024 : 64 * ceil_div(ny - 2, 64)), 0, s,
+                               phi, div, ny, nx, (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
         hipLaunchKernelGGL(k_sub_gradient, grid2d(ny, nx), dim3(256), 0, s, phi, u, v, ny, nx, cx,
                            cy);
         CFD_LAUNCH_CHECK();

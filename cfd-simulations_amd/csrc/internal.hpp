@@ -95,7 +95,7 @@ inline unsigned long long persist_poll_ticks() {
 // jacobi2d_persist.hip: 1 if it ran the solve (phi <- the result; *rc set on
 // a HIP error), 0 if the persistent path does not apply
 int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t *mask, int ny, int nx,
-                           float dx2, float dtv, int iterations, hipStream_t s, int *rc);
+                           float dx2, float dtv, int iterations, hipStream_t s, int *rc, bool zero = false);
 
 // poisson3d.hip
 int launch_fix_faces3d(const float *src, float *dst, const uint8_t *mask, int ny, int nx, int za,

@@ -58,6 +58,7 @@ struct JPersistArgs {
     unsigned epoch;         // this solve's tag prefix: granule tags are epoch << 16 | block + 1
     unsigned long long spin;  // poll bound, 100 MHz ticks
     int ny, nx, nseg, niters, pre;
+    int zero;  // start from phi = 0 (v5.py:337): read nothing of phi, write the edge rows' zeros too
     float dx2, dtv;
 };
 
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
         const int i = kJRW * w + j, y = ytop + i;
         const bool in_ = valid && y >= 0 && y <= a.ny - 1;
         off[j] = (size_t)min(max(y, 0), a.ny - 1) * a.nx + (valid ? x : 0);
-        const float v = a.phi[off[j]], d = a.src[off[j]];
+        const float v = a.zero ? 0.f : a.phi[off[j]], d = a.src[off[j]];
         const bool mk = MASK ? a.mask[off[j]] != 0 : false;
         A[j] = in_ ? v : 0.f;
         const float dd = in_ ? d : 0.f;
@@ -105,8 +106,9 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
         zero[j] = in_ && mk;  // v5.py:345: after the interior, masked cells <- 0
         own[j] = writer && i >= NI && i < kJT0 - NI && y <= a.ny - 2;
         inner[j] = in_ && y >= 1 && y <= a.ny - 2;  // the cells some tile owns
-        // a masked cell of row 0 or ny - 1 (no tile owns it) becomes 0 too
-        edgez[j] = writer && in_ && !inner[j] && mk;
+        // a masked cell of row 0 or ny - 1 (no tile owns it) becomes 0 too,
+        // and with a zero start every cell of those rows
+        edgez[j] = writer && in_ && !inner[j] && (mk || a.zero);
     }
     const size_t plane = (size_t)a.ny * a.nx;
     const int i0 = kJRW * w;
@@ -183,7 +185,7 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
 #pragma unroll
     for (int j = 0; j < kJRW; ++j) {
         if (own[j]) a.phi[off[j]] = A[j];
-        if (MASK && edgez[j]) a.phi[off[j]] = 0.f;
+        if (edgez[j]) a.phi[off[j]] = 0.f;
     }
     // The last workgroup to finish reads the status: an expired poll left
     // garbage, so the whole result becomes NaN (it cannot pass for a solution:
@@ -309,7 +311,7 @@ void release_thread_rings() {
 }
 
 int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t *mask, int ny, int nx,
-                           float dx2, float dtv, int iterations, hipStream_t s, int *rc) {
+                           float dx2, float dtv, int iterations, hipStream_t s, int *rc, bool zero) {
     *rc = CFD_OK;
     const int NI = tuning().j2p_ni;
     if (!tuning().j2_persist || iterations <= NI || ny < 3 || nx < 3) return 0;
@@ -322,6 +324,7 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
     a.nx = nx;
     a.niters = iterations;
     a.pre = pre ? 1 : 0;
+    a.zero = zero ? 1 : 0;
     a.dx2 = dx2;
     a.dtv = dtv;
     const int ntiles = jtiles_for(NI, ny, nx, &a.nseg);

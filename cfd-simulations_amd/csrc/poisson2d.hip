@@ -332,7 +332,7 @@ thread_local int g_j2_last[2] = {0, 0};
 template <typename T>
 static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t *mask, int ny,
                           int nx, T dx2, T dtv, int iters, int resid_every, T *resid_out,
-                          hipStream_t s) {
+                          hipStream_t s, bool zero = false) {
     CFD_REQUIRE(div && phi && tmp, "jacobi2d: null array pointer");
     CFD_REQUIRE(ny >= 1 && nx >= 1, "jacobi2d: bad shape (%d, %d)", ny, nx);
     CFD_REQUIRE(iters >= 0, "jacobi2d: iters < 0");
@@ -348,7 +348,7 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
             auto_levels2d<T>(ny, nx) != kDefaultLevels2d) {
             int prc = CFD_OK;
             const int tk = timing_begin(s);
-            if (jacobi2d_persist_solve(phi, div, false, mask, ny, nx, dx2, dtv, iters, s, &prc)) {
+            if (jacobi2d_persist_solve(phi, div, false, mask, ny, nx, dx2, dtv, iters, s, &prc, zero)) {
                 if (prc) return prc;
                 g_j2_last[0] = 1;
                 g_j2_last[1] = iters;
@@ -358,6 +358,7 @@ static int jacobi2d_solve(const T *div, T *phi, T *tmp, T *rhs_ws, const uint8_t
             timing_cancel(tk);
         }
     }
+    if (zero) CFD_CHECK_HIP(hipMemsetAsync(phi, 0, sizeof(T) * (size_t)ny * nx, s));  // v5.py:337
     // Dirichlet rows 0 and ny-1 of the first output buffer (masked -> 0)
     if ((rc = fix_edge_rows<T>(phi, tmp, mask, ny, nx, s))) return rc;
     const int nres = resid_every > 0 ? iters / resid_every : 0;
@@ -1192,6 +1193,24 @@ int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rh
                      int resid_every, double *resid_out, void *stream) {
     return jacobi2d_solve<double>(div, phi, phi_tmp, rhs_ws, mask, ny, nx, dx * dx, (double)dt,
                                   iters, resid_every, resid_out, as_stream(stream));
+}
+
+int cfd_jacobi2d_zero_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws,
+                          const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
+                          int resid_every, float *resid_out, void *stream) {
+    if (iters == 0 && phi && ny >= 1 && nx >= 1)
+        CFD_CHECK_HIP(hipMemsetAsync(phi, 0, sizeof(float) * (size_t)ny * nx, as_stream(stream)));
+    return jacobi2d_solve<float>(div, phi, phi_tmp, rhs_ws, mask, ny, nx, (float)(dx * dx), dt, iters, resid_every,
+                                 resid_out, as_stream(stream), true);
+}
+
+int cfd_jacobi2d_zero_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
+                          const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
+                          int resid_every, double *resid_out, void *stream) {
+    if (iters == 0 && phi && ny >= 1 && nx >= 1)
+        CFD_CHECK_HIP(hipMemsetAsync(phi, 0, sizeof(double) * (size_t)ny * nx, as_stream(stream)));
+    return jacobi2d_solve<double>(div, phi, phi_tmp, rhs_ws, mask, ny, nx, dx * dx, (double)dt, iters, resid_every,
+                                  resid_out, as_stream(stream), true);
 }
 
 int cfd_get_jacobi2d_levels(void) { return tuning().j2_blocking >= 2 ? tuning().j2_blocking : kDefaultLevels2d; }

@@ -182,10 +182,13 @@ def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iteratio
 
 
 def solve_pressure_jacobi(phi, div_u_star, dx, dt, mask, iterations, phi_tmp=None,
-                          resid_every=0, resid_out=None, rhs_ws=None):
+                          resid_every=0, resid_out=None, rhs_ws=None, zero_start=False):
     """Jacobi branch of solve_pressure_fast, v5.py:336-346, bit-exact; in place
     on ``phi`` (float32 or float64 fields); returns ``phi``.  ``rhs_ws``: an
-    optional same-size workspace that lets the sweeps skip the division."""
+    optional same-size workspace that lets the sweeps skip the division.
+    ``zero_start``: phi = zeros first (v5.py:337) inside the solve
+    (cfd_jacobi2d_zero_*: the persistent small-grid solve reads nothing of
+    phi, no fill launch)."""
     ny, nx = _shape2d(phi)
     if div_u_star.dtype != phi.dtype:
         raise TypeError("phi and div_u_star must share a dtype")
@@ -193,7 +196,8 @@ def solve_pressure_jacobi(phi, div_u_star, dx, dt, mask, iterations, phi_tmp=Non
     _like(phi, rhs_ws, "rhs_ws")
     tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
     m = _mask_u8(mask, phi.shape)
-    fn = {torch.float32: "cfd_jacobi2d_f32", torch.float64: "cfd_jacobi2d_f64"}.get(phi.dtype)
+    z = "_zero" if zero_start else ""
+    fn = {torch.float32: f"cfd_jacobi2d{z}_f32", torch.float64: f"cfd_jacobi2d{z}_f64"}.get(phi.dtype)
     if fn is None:
         raise TypeError(f"unsupported dtype {phi.dtype}")
     call(fn, ptr(div_u_star), ptr(phi), ptr(tmp), ptr(rhs_ws), ptr(m), ny, nx, float(dx),

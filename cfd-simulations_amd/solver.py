@@ -222,15 +222,16 @@ class OptimizedTurbulentSolver:
 
     def solve_pressure_fast(self, div_u_star):  # v5.py:328-347
         cfg = self.config
-        self.phi.zero_()
         if cfg.use_fast_pressure:
+            self.phi.zero_()
             K.solve_pressure_gauss_seidel_fast(self.phi, div_u_star, cfg.dx, cfg.dy, cfg.dt,
                                                self._mask_u8, cfg.pressure_iterations,
                                                cfg.pressure_tolerance, workspace=self._gs_ws,
                                                iters_done=self._gs_done, phi_tmp=self._phi_tmp)
-        else:
+        else:  # phi = zeros (v5.py:337) inside the solve
             K.solve_pressure_jacobi(self.phi, div_u_star, cfg.dx, cfg.dt, self._mask_u8,
-                                    cfg.pressure_iterations, phi_tmp=self._phi_tmp, rhs_ws=self._rhs_ws)
+                                    cfg.pressure_iterations, phi_tmp=self._phi_tmp, rhs_ws=self._rhs_ws,
+                                    zero_start=True)
         return self.phi
 
     def apply_boundary_conditions(self, u, v):  # v5.py:349-360

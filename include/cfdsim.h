@@ -93,6 +93,16 @@ int cfd_get_last_jacobi2d_path(int *sweeps_per_launch);
 int cfd_jacobi2d_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
                      const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
                      int resid_every, double *resid_out, void *stream);
+/* The reference's whole Jacobi solve, zero fill included (v5.py:337-346):
+ * phi = zeros (boundary ring included), then iters sweeps as cfd_jacobi2d_*.
+ * The persistent small-grid solve starts from the zeros itself (it reads
+ * nothing of phi, and writes every cell); other paths zero-fill phi first. */
+int cfd_jacobi2d_zero_f32(const float *div, float *phi, float *phi_tmp, float *rhs_ws,
+                          const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
+                          int resid_every, float *resid_out, void *stream);
+int cfd_jacobi2d_zero_f64(const double *div, double *phi, double *phi_tmp, double *rhs_ws,
+                          const uint8_t *mask, int ny, int nx, double dx, float dt, int iters,
+                          int resid_every, double *resid_out, void *stream);
 
 /* 3-D 7-point generalisation of the same Jacobi template (the reference is
  * 2-D only): phi_new = f32(1/6) * (((((E+W)+N)+S)+U)+D - f32(h*h)*div/dt),

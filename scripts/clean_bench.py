@@ -1,7 +1,7 @@
 """Time clean_divergence_fast (v5.py:240-256) alone: the serial lexicographic
 phi sweep dominates it.  Prints one JSON line per shape with microseconds per
-call (two iterations: two divergence + sweep + gradient-subtraction rounds).
-A/B: CFD_LEX_STAGED=1 selects the round-4 staged sweeps."""
+call (two iterations: 5 launches on the skewed layout, k_lex_gs_skew).
+A/B: CFD_LEX_SKEW_WAVES=1..4 sets the waves per band."""
 import argparse
 import json
 import os
@@ -39,7 +39,7 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.reps
         print(json.dumps({"shape": [ny, nx], "us_per_call": round(us, 2),
-                          "staged": bool(os.environ.get("CFD_LEX_STAGED")),
+                          "waves": os.environ.get("CFD_LEX_SKEW_WAVES", "4"),
                           "finite": bool(torch.isfinite(u).all())}), flush=True)
 
 

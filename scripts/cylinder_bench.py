@@ -41,13 +41,17 @@ def main():
     ap.add_argument("--jacobi", action="store_true", help="use_fast_pressure=False (NumPy-branch Jacobi)")
     ap.add_argument("--levels", type=int, default=0, help="cfd_set_jacobi2d_blocking (0 auto)")
     ap.add_argument("--cpu-steps", type=int, default=3, help="CPU-baseline steps per form (0: none)")
-    ap.add_argument("--plain-launch", action="store_true",
-                    help="persistent solves as plain launches (cfd_set_persistent_launch(0, 0))")
+    ap.add_argument("--coop-launch", action="store_true",
+                    help="persistent solves as cooperative launches (cfd_set_persistent_launch(1, 0)); "
+                         "the library default since r05 is a plain launch")
+    ap.add_argument("--pred-rows", type=int, default=0, help="cfd_set_predictor2d_config(0, rows, 0) (0 auto)")
     a = ap.parse_args()
     from cfd_simulations_amd._lib import call
+    if a.pred_rows:
+        call("cfd_set_predictor2d_config", 0, a.pred_rows, 0)
     call("cfd_set_jacobi2d_blocking", a.levels)
-    if a.plain_launch:
-        call("cfd_set_persistent_launch", 0, 0)
+    if a.coop_launch:
+        call("cfd_set_persistent_launch", 1, 0)
     cfg = OptimizedTurbulentConfig(nx=a.nx, ny=a.ny, use_fast_pressure=not a.jacobi)
     s = OptimizedTurbulentSolver(cfg)
     for _ in range(a.warmup):
@@ -69,7 +73,7 @@ def main():
     it = cfg.pressure_iterations
     cells = (a.ny - 2) * (a.nx - 2) * it
     out = {"workload": f"cylinder_v5_{a.nx}x{a.ny}", "pressure": "jacobi" if a.jacobi else "rbgs",
-           "levels": a.levels, "persistent_launch": "plain" if a.plain_launch else "cooperative",
+           "levels": a.levels, "persistent_launch": "cooperative" if a.coop_launch else "plain",
            "pressure_iterations": it, "steps_per_s": round(1.0 / t_step, 2),
            "ms_per_step": round(t_step * 1e3, 3), "pressure_ms": round(t_p * 1e3, 3),
            "pressure_share": round(t_p / t_step, 3),

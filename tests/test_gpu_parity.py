@@ -454,7 +454,7 @@ def test_project_and_clean_divergence_bitexact(golden):
 @pytest.mark.parametrize("ny,nx", [(3, 3), (3, 50), (4, 7), (66, 30), (67, 30), (130, 17), (180, 600),
                                    (194, 33), (258, 70), (322, 51), (323, 20), (36, 1200),
                                    (514, 9), (515, 9), (1030, 40), (1027, 64), (2060, 66), (130, 131),
-                                   (70, 1023), (1100, 97)])
+                                   (70, 1023), (1100, 97), (300, 66), (130, 67)])
 def test_clean_divergence_lexicographic_shapes(ny, nx):
     """The serial lexicographic phi sweep of clean_divergence_fast (v5.py:250-253)
     on ragged shapes: one and several waves per band, a band edge inside a wave,

@@ -419,6 +419,26 @@ def test_jacobi2d_persistent_streams_and_threads():
         assert r is not None and np.array_equal(r, ref)
 
 
+@pytest.mark.parametrize("shape,masked,dtype", [((180, 600), False, np.float32), ((180, 600), True, np.float32),
+                                                ((37, 70), True, np.float32), ((180, 600), False, np.float64),
+                                                ((1030, 70), False, np.float32)])
+def test_jacobi2d_zero_start_matches_fill_then_solve(shape, masked, dtype):
+    """cfd_jacobi2d_zero_* (phi = zeros inside the solve, v5.py:337): phi
+    starts as garbage -- NaN inside, 7.0 on the boundary ring -- and ends
+    equal to the oracle's zero-start solve, boundary ring included, on the
+    persistent small-grid path (cylinder grid, with and without a mask) and
+    on the fill-then-sweeps paths (f64; a grid past the persistent tiles)."""
+    rng = np.random.default_rng(shape[0] + shape[1] + int(masked))
+    div = rng.standard_normal(shape).astype(dtype)
+    mask = rng.random(shape) < 0.03 if masked else None
+    dx, dt, it = 20 / (shape[1] - 1), np.float32(5e-5), 40
+    phi = torch.full(shape, float("nan"), dtype=torch.from_numpy(div).dtype, device=DEV)
+    phi[0, :] = phi[-1, :] = phi[:, 0] = phi[:, -1] = 7.0
+    K.solve_pressure_jacobi(phi, dev(div), dx, dt, None if mask is None else dev(mask), it, zero_start=True)
+    ref = oracle.jacobi2d(div, dx=dx, dt=dt, iters=it, mask=mask)
+    assert np.array_equal(host(phi), ref)
+
+
 @pytest.mark.parametrize("cooperative", [1, 0])
 def test_persistent_cooperative_and_plain_launch_bitexact(cooperative):
     """Both persistent small-grid solves, launched plainly (the default since
