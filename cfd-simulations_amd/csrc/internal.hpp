@@ -52,7 +52,7 @@ struct Tuning {
     void *tbr_trace = nullptr;
     // fused 2-D predictor (cfd_predictor2d_f32 / _f64): 0 auto (the row march
     // whenever the arrays are below 2^31 bytes), 1 one thread per cell, 2 row
-    // march; rows per chunk of the row march (0: one resident round, 8..16)
+    // march; rows per chunk of the row march (0: one resident round, 2..16)
     int pred_variant = 0, pred_rows = 0;
     // row march: preferred cells per lane (0: 2; f32 1, 2, 4; f64 1, 2),
     // halved until nx and every pointer's alignment fit

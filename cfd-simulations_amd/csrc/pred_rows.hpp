@@ -522,7 +522,7 @@ int pred_rows_resident(const void *f);
 void set_last_predictor(int path, int tau, int vec);
 
 // Row-march launch: cells per lane `vec` (16 bytes per lane at most), rows per
-// chunk `rows` (0: one resident round, 8..16); a.nseg / a.groups / a.rows are
+// chunk `rows` (0: one resident round, 2..16); a.nseg / a.groups / a.rows are
 // filled here.  The caller has checked shape and alignment.
 template <typename T>
 hipError_t pred_rows_launch(PredRowArgs<T> a, bool supg, int tau, int vec, int rows, hipStream_t s) {
@@ -538,15 +538,17 @@ hipError_t pred_rows_launch(PredRowArgs<T> a, bool supg, int tau, int vec, int r
     a.nseg = ceil_div(a.nx, 64 * vec);
     a.groups = ceil_div(a.nseg, 4);
     // rows per chunk: every workgroup resident at once (one round at the
-    // kernel's occupancy), chunks of 8..16 rows (2 halo rows each) (r04 sweep,
-    // 8192^2 SUPG f32: 16-row chunks beat 32 / 64 by 2-7 %)
+    // kernel's occupancy), chunks of 2..16 rows (2 halo rows each) (r04 sweep,
+    // 8192^2 SUPG f32: 16-row chunks beat 32 / 64 by 2-7 %; r05, 600 x 180:
+    // 2-row chunks -- 450 workgroups instead of 46 -- take ~8 us off the
+    // latency-bound launch)
     a.rows = rows;
     if (a.rows <= 0) {
         const int resident = pred_rows_resident(f);
         const int chunks = resident / a.groups > 0 ? resident / a.groups : 1;
         a.rows = ceil_div(a.ny, chunks);
         if (a.rows > 16) a.rows = 16;
-        if (a.rows < 8) a.rows = 8;
+        if (a.rows < 2) a.rows = 2;
     }
     const int nblk = a.groups * ceil_div(a.ny, a.rows);
     void *args[] = {&a};

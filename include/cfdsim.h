@@ -185,7 +185,7 @@ int cfd_predictor2d_f32(const float *u, const float *v, const float *nu_eff, flo
  * either way): variant 0 = auto (the row-march tile kernel when the arrays are
  * below 2^31 bytes; else one thread per cell), 1 = one thread per cell, 2 =
  * row march where it applies; rows = rows per row-march chunk (0 = auto: every
- * workgroup resident in one round, 8..16 rows); cells_per_lane = adjacent
+ * workgroup resident in one round, 2..16 rows); cells_per_lane = adjacent
  * cells per lane of the row march (0 = auto: 2; f32 1, 2, 4; f64 1, 2),
  * halved until nx % it == 0 and every array is aligned to it elements. */
 int cfd_set_predictor2d_config(int variant, int rows, int cells_per_lane);
