@@ -11,6 +11,7 @@
 //
 // These kernels are one-pass per cell and HBM-bound; the fused predictor
 // reads u, v once (5-point neighbourhoods from L1/L2) and writes u*, v*, tau.
+#include <atomic>
 #include <map>
 #include <mutex>
 
@@ -281,9 +282,13 @@ constexpr int kSkewWaves = 4;  // waves per band: at one wave per SIMD the chain
 #define CFD_SKEW_EXP 0  // timing experiments only (wrong results): 1 no stores, 2 no loads, 4 no DPP
 #endif
 constexpr int kSkewRing = 8;   // groups of 4 steps in flight per wave (and per loop iteration)
+constexpr int kSkewMcBlocks = 128;        // k_lex_gs_skew_mc: blocks (workgroups) at most
+constexpr size_t kSkewMcLds = 64 * 1024;  // k_lex_gs_skew_mc: LDS asked for (unused; two per CU at most)
 __host__ __device__ inline int lex_skew_blocks(int ny) { return (ny - 2 + 63) >> 6; }
 __host__ __device__ inline int lex_skew_groups(int nx) { return (nx + 63 + 3) >> 2; }
 size_t lex_skew_floats(int ny, int nx) { return (size_t)lex_skew_blocks(ny) * (size_t)lex_skew_groups(nx) * 256; }
+// the per-block progress words of k_lex_gs_skew_mc, after div and the two phi
+size_t lex_skew_prog_offset(int ny, int nx) { return (3 * sizeof(float) * lex_skew_floats(ny, nx) + 255) & ~(size_t)255; }
 // floats per wave row of k_lex_gs_skew's LDS: column c at c + 64 for
 // c = -63 .. nx + 76, 16 B aligned
 constexpr int lex_skew_rsl(int nx) { return (nx + 160 + 3) & ~3; }
@@ -377,31 +382,276 @@ __global__ void k_sub_gradient2_skew(const float *__restrict__ phi1, const float
     v[c] = (v[c] - b1) - b2;
 }
 
-// phi: the skewed phi buffers from phi_base (phi_bytes in all); the sweep
-// reads the old values at byte offset old_off (kOob: all zeros, the first
-// sweep of clean_divergence) and writes the new ones at new_off (== old_off:
-// in place).
-__global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_base, int phi_bytes, int old_off,
-                                                     int new_off, const float *__restrict__ div_s, int ny, int nx,
-                                                     float cx, float cy, float cd) {
+struct SkewArgs {
+    float *phi_base;  // the skewed phi buffers (phi_bytes in all)
+    const float *div_s;
+    unsigned long long *prog;  // MC: per block {epoch, groups stored and complete}
+    int *fail;                 // MC: the device's persistent-failure counter
+    unsigned long long poll_ticks;
+    int phi_bytes, old_off, new_off;  // old_off kOob: all zeros (the first sweep)
+    int ny, nx;
+    unsigned epoch;
+    float cx, cy, cd;
+};
+
+// One wave's sweep of block m.  !MC: up to 4 waves per band share a workgroup
+// (one CU), lane 0's row above from the wave above through an LDS row, a
+// band's first wave (FIRST) from memory.  MC (r05): one wave per workgroup,
+// every block on its own CU, each wave FIRST: lane 0's row above is block
+// m - 1's lane 63 in the new buffer, read with sc1 loads once block m - 1 has
+// published (sc1, per 16 steps) that those groups are stored and complete;
+// the progress word is polled two chunks ahead, so the poll's wait is the
+// ring's own.
+template <bool MC>
+__device__ inline void lex_skew_wave(const SkewArgs &sa, int m, int wv, int nw, int lane, float *lex_rows,
+                                     int *flags) {
     typedef float f4v __attribute__((ext_vector_type(4)));
     constexpr int R = kSkewRing;
-    extern __shared__ float lex_rows[];  // [waves][lex_skew_rsl]: wave w's last-lane results, column c at c + 64
-    __shared__ int flags[kSkewWaves];    // 16-step chunks wave w's last lane has published
-    const int nw = blockDim.x >> 6, lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int RSL = lex_skew_rsl(nx);
-    const int imax = ny - 2, jmax = nx - 2;
-    const int nb = lex_skew_blocks(ny), DG = lex_skew_groups(nx);
+    constexpr int XA = MC ? 16 : 0;  // sc1 on the cross-block loads and the stores
+    const int old_off = sa.old_off, new_off = sa.new_off;
+    const float cx = sa.cx, cy = sa.cy, cd = sa.cd;
+    const int RSL = lex_skew_rsl(sa.nx);
+    const int imax = sa.ny - 2, jmax = sa.nx - 2;
+    const int nb = lex_skew_blocks(sa.ny), DG = lex_skew_groups(sa.nx);
     const int bytes = nb * DG * 1024;
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(phi_base, 0, phi_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(sa.phi_base, 0, sa.phi_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rd =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(div_s), 0, bytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(sa.div_s), 0, bytes, 0x00020000);
     // steps d = 0 .. 4 DG - 1, 16 per chunk: every slot of the block is stored
     // (lane 63's last interior column is at d = nx + 61, its zero side column
     // at nx + 62, and the padding up to 4 DG - 1 is written too)
     const int nq = (DG + 3) >> 2;
     const int nc = (nq + R / 4 - 1) / (R / 4);  // loop iterations of 4 R steps
+    const bool rowok = 1 + 64 * m + lane <= imax;
+    // byte offsets of group 0 (group G at + 1024 G): own slots (div; old
+    // phi; new phi); lane 63: the next block's lane 0, group G - 16, old;
+    // lane 0 of a band's first wave: the block above's lane 63, group
+    // G + 15, new.  (kOob + an offset stays past the buffer.)
+    const int oD = (m * DG * 64 + lane) * 16;
+    const int oS = old_off + oD;
+    const int oX = lane == 63 ? (m + 1 < nb ? old_off + ((m + 1) * DG - 16) * 1024 : (int)kOob)
+                   : lane == 0 && (MC || wv == 0) && m > 0 ? new_off + (((m - 1) * DG + 15) * 64 + 63) * 16
+                                                    : (int)kOob;
+    const int oW = rowok ? new_off + oD : (int)kOob;
+    float *mine = MC ? nullptr : lex_rows + (size_t)wv * RSL + 64;
+    const float *above = MC ? nullptr : lex_rows + (size_t)(wv > 0 ? wv - 1 : 0) * RSL + 64;
+    // MC: block m - 1's progress (groups stored and complete), the two polls
+    // in flight (issued two and one chunks back) and what is known so far
+    unsigned long long poll_a = 0, poll_b = 0;
+    int known = 0;
+    // the in-flight polls must stay vector registers: a value the compiler
+    // sees as uniform is moved to scalar registers right after its load,
+    // which waits for it (and, memory operations completing in order, for
+    // the whole prefetch ring) -- an opaque lane-dependent zero in the
+    // address keeps it per lane until it is used, two chunks later
+    int vz = 0;
+    __asm__ volatile("" : "+v"(vz));
+    unsigned long long *const prog_up = MC && m > 0 ? sa.prog + (m - 1) + vz : nullptr;
+    auto progress_of = [&](unsigned long long v) {
+        return (unsigned)(v >> 32) == sa.epoch ? (int)(unsigned)(v & 0x7fffffffull) : 0;
+    };
+    // a software pipeline of R groups: iteration c computes groups R c ..
+    // R c + R - 1 and loads groups R (c + 1) + g into the slots it frees;
+    // it starts at c = -1, whose steps only load (no lane is at a column
+    // >= 1 there: nothing is stored or kept), so the loop has one shape
+    // and the compiler's wait counts are the steady-state ones
+    f4v P[R], D[R], X[R];
+    float w, vprev;  // w: phi(i, j - 1)
+    // One 16-step chunk (ring slots 4 H .. 4 H + 3).  The step is issue-
+    // bound (a wave64 VALU op takes 4 cycles: ~13 per step were ~55 cycles
+    // against the ~47-cycle dependent chain), so the chunk is specialised:
+    // FULL chunks -- every lane at a column 1 .. nx - 2 in all 16 steps,
+    // most of a sweep -- skip the per-step column test and the selects;
+    // FIRST (a band's first wave) takes lane 0's row above from X, the
+    // others from the LDS row, without a per-step select.
+    auto chunk = [&](auto Hc, auto FULLc, auto FIRSTc, int qc) {
+        constexpr int H = decltype(Hc)::value;
+        constexpr bool FULL = decltype(FULLc)::value, FIRST = decltype(FIRSTc)::value;
+        float S0[16];
+        if constexpr (!FIRST) {
+            if (qc >= 0) {
+                // wave w - 1's last lane must have published chunks 0 .. qc + 4
+                // (its column 16 qc + 15 comes at its step 16 qc + 78)
+                const int need = qc + 5 < nq ? qc + 5 : nq;
+                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&flags[wv - 1], __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+                    __builtin_amdgcn_s_sleep(1);
+                __asm__ volatile("" ::: "memory");  // the row reads stay after the poll
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const float4 a4 = *reinterpret_cast<const float4 *>(above + 16 * qc + 4 * p);
+                    S0[4 * p] = a4.x;
+                    S0[4 * p + 1] = a4.y;
+                    S0[4 * p + 2] = a4.z;
+                    S0[4 * p + 3] = a4.w;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) S0[k] = 0.f;
+            }
+        }
+        if constexpr (MC) {
+            if (m > 0) {
+                // this chunk's refills read block m - 1's groups up to
+                // 4 qc + 3 + R + 16: they must be stored and complete
+                const unsigned long long v = poll_a;
+                poll_a = poll_b;
+                poll_b = __hip_atomic_load(prog_up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int pv = progress_of(v);
+                known = pv > known ? pv : known;
+                const int need = 4 * qc + R + 20;
+                if (known < need) {  // wait (draining) until two chunks past the need
+                    const unsigned long long t0 = wall_clock64();
+                    while (true) {
+                        const int p2 = progress_of(
+                            __hip_atomic_load(sa.prog + (m - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        known = p2 > known ? p2 : known;
+                        if (known >= need + 8 || known == 0x7fffffff) break;
+                        if (wall_clock64() - t0 > sa.poll_ticks) {  // fail loudly: counted, results garbage
+                            if (lane == 0 && sa.fail) atomicAdd(sa.fail, 1);
+                            known = 0x7fffffff;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
+            }
+        }
+        // this chunk's group 0 at + sof; the refills R groups later
+        const int sof = __builtin_amdgcn_readfirstlane(qc * 4 * 1024);
+        float out[16];
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+            const int g = 4 * H + gg;  // ring slot
+            const f4v p0 = P[g], p1 = P[(g + 1) % R], x0 = X[g], x1 = X[(g + 1) % R], d4 = D[g];
+            f4v o4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float e = k < 3 ? p0[k + 1] : p1[0];   // slot d + 1
+                const float xn = k < 3 ? x0[k + 1] : x1[0];  // lane 63: slot d - 63
+                float s0;
+                if constexpr (FIRST)
+                    s0 = k == 0 ? x0[3] : x1[k - 1];  // lane 0: slot d + 63
+                else
+                    s0 = S0[4 * gg + k];
+                const float n = __int_as_float(__builtin_amdgcn_update_dpp(
+                    __float_as_int(xn), __float_as_int(e), 0x130, 0xf, 0xf, false));  // wave_shl:1
+                const float S = (CFD_SKEW_EXP & 4) ? vprev
+                                                   : __int_as_float(__builtin_amdgcn_update_dpp(
+                                                         __float_as_int(s0), __float_as_int(vprev), 0x138, 0xf,
+                                                         0xf, false));  // wave_shr:1
+                const float a = cx * (e + w);
+                const float bb = cy * (n + S);
+                const float v = ((a + bb) - d4[k]) * cd;
+                if constexpr (FULL) {
+                    w = v;
+                    o4[k] = v;
+                } else {
+                    const int j = 16 * qc + 4 * gg + k - lane;  // step d = 16 qc + 4 gg + k
+                    const bool act = (uint32_t)(j - 1) < (uint32_t)jmax;
+                    w = act ? v : w;
+                    o4[k] = act ? v : 0.f;  // the side columns and the padding stay 0
+                }
+                vprev = v;
+                out[4 * gg + k] = v;
+            }
+            // (groups past the block's DG belong to the next block: the
+            // loop's last iteration runs up to 8 groups past the end)
+            const bool gok = FULL || (qc >= 0 && 4 * qc + gg < DG);
+            if constexpr (!(CFD_SKEW_EXP & 1))
+                __builtin_amdgcn_raw_buffer_store_b128(o4, rp, gok ? oW + 1024 * gg : (int)kOob, sof, XA);
+            // group G + R's operands into the slot just freed (after its
+            // last use: a load issued before it would need a second
+            // register and a copy that waits for the load).  Slot g is
+            // also read by group G - 1 (done), slot g + 1 by this group
+            // (refilled next).
+            if constexpr (!(CFD_SKEW_EXP & 2)) {
+                P[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oS + 1024 * gg,
+                                                                                      sof + R * 1024, 0));
+                D[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rd, oD + 1024 * gg,
+                                                                                      sof + R * 1024, 0));
+                // (all lanes load X though only lane 63 -- and lane 0 of a
+                // band's first wave -- reads it: exec-masking the load to
+                // those lanes measured 8-11 % slower, r05)
+                X[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oX + 1024 * gg,
+                                                                                      sof + R * 1024, XA));
+            } else {
+                P[g] += 1.f;
+            }
+            // keep the prefetch where it is: the scheduler would sink it
+            // next to its use, R groups later, exposing the latency
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (wv + 1 < nw && qc >= 0 && lane == 63) {
+            // publish the last lane's 16 results (columns 16 qc - 63 + k)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) mine[16 * qc - 63 + k] = out[k];
+            // the row before the count (LDS completes in order; this keeps
+            // the compiler from sinking the row writes past the flag)
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __hip_atomic_store(&flags[wv], qc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr (MC) {
+            // groups stored and complete: the operands of group 4 qc + 3, just
+            // consumed (the compiler's wait came before their first use), were
+            // loaded after the store of group 4 qc + 3 - R, and memory
+            // operations complete in order
+            const int cnt = 4 * qc + 4 - R;
+            __asm__ volatile("" ::: "memory");
+            if (cnt > 0 && lane == 0)
+                __hip_atomic_store(sa.prog + m, ((unsigned long long)sa.epoch << 32) | (unsigned)cnt, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    using T1 = std::true_type;
+    using F0 = std::false_type;
+    static_assert(R == 8, "two 16-step chunks per iteration");
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    // iterations whose two chunks are both FULL: chunk 2 c >= 4 and
+    // 16 (2 c + 1) + 15 <= jmax; the loop is split into head, middle and
+    // tail loops around them (a per-chunk branch made the register
+    // allocator copy the ring at every merge, waiting for its loads)
+    const int cf0 = 2, cf1 = (jmax - 31) >= 0 ? (jmax - 31) >> 5 : -1;  // [cf0, cf1]
+    const int cm0 = cf1 >= cf0 ? cf0 : nc, cm1 = cf1 >= cf0 ? (cf1 + 1 < nc ? cf1 + 1 : nc) : nc;
+    auto run = [&](auto FIRSTc) {
+#pragma unroll
+        for (int g = 0; g < R; ++g) P[g] = D[g] = X[g] = f4v{0.f, 0.f, 0.f, 0.f};
+        w = 0.f;  // column 0 (boundary)
+        vprev = 0.f;
+        for (int c = -1; c < cm0; ++c) {
+            chunk(H0{}, F0{}, FIRSTc, 2 * c);
+            chunk(H1{}, F0{}, FIRSTc, 2 * c + 1);
+        }
+        for (int c = cm0; c < cm1; ++c) {
+            chunk(H0{}, T1{}, FIRSTc, 2 * c);
+            chunk(H1{}, T1{}, FIRSTc, 2 * c + 1);
+        }
+        for (int c = cm1; c < nc; ++c) {
+            chunk(H0{}, F0{}, FIRSTc, 2 * c);
+            chunk(H1{}, F0{}, FIRSTc, 2 * c + 1);
+        }
+    };
+    if constexpr (MC) {
+        run(T1{});
+        // every group stored and complete (a release: waits for the stores)
+        if (lane == 0)
+            __hip_atomic_store(sa.prog + m, ((unsigned long long)sa.epoch << 32) | 0x7fffffffull, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        if (wv == 0)
+            run(T1{});
+        else
+            run(F0{});
+    }
+}
+
+__global__ __launch_bounds__(256) void k_lex_gs_skew(SkewArgs sa) {
+    extern __shared__ float lex_rows[];  // [waves][lex_skew_rsl]: wave w's last-lane results, column c at c + 64
+    __shared__ int flags[kSkewWaves];    // 16-step chunks wave w's last lane has published
+    const int nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nb = lex_skew_blocks(sa.ny);
     for (int b0 = 0; b0 < nb; b0 += nw) {
         __threadfence();  // the band before is final and visible (a band's first wave reads its last row)
         __syncthreads();
@@ -409,168 +659,14 @@ __global__ __launch_bounds__(256) void k_lex_gs_skew(float *__restrict__ phi_bas
         __syncthreads();
         const int m = b0 + wv;
         if (m >= nb) continue;  // wave-uniform
-        const bool rowok = 1 + 64 * m + lane <= imax;
-        // byte offsets of group 0 (group G at + 1024 G): own slots (div; old
-        // phi; new phi); lane 63: the next block's lane 0, group G - 16, old;
-        // lane 0 of a band's first wave: the block above's lane 63, group
-        // G + 15, new.  (kOob + an offset stays past the buffer.)
-        const int oD = (m * DG * 64 + lane) * 16;
-        const int oS = old_off + oD;
-        const int oX = lane == 63 ? (m + 1 < nb ? old_off + ((m + 1) * DG - 16) * 1024 : (int)kOob)
-                       : lane == 0 && wv == 0 && m > 0 ? new_off + (((m - 1) * DG + 15) * 64 + 63) * 16
-                                                        : (int)kOob;
-        const int oW = rowok ? new_off + oD : (int)kOob;
-        float *mine = lex_rows + (size_t)wv * RSL + 64;
-        const float *above = lex_rows + (size_t)(wv > 0 ? wv - 1 : 0) * RSL + 64;
-        // a software pipeline of R groups: iteration c computes groups R c ..
-        // R c + R - 1 and loads groups R (c + 1) + g into the slots it frees;
-        // it starts at c = -1, whose steps only load (no lane is at a column
-        // >= 1 there: nothing is stored or kept), so the loop has one shape
-        // and the compiler's wait counts are the steady-state ones
-        f4v P[R], D[R], X[R];
-        float w, vprev;  // w: phi(i, j - 1)
-        // One 16-step chunk (ring slots 4 H .. 4 H + 3).  The step is issue-
-        // bound (a wave64 VALU op takes 4 cycles: ~13 per step were ~55 cycles
-        // against the ~47-cycle dependent chain), so the chunk is specialised:
-        // FULL chunks -- every lane at a column 1 .. nx - 2 in all 16 steps,
-        // most of a sweep -- skip the per-step column test and the selects;
-        // FIRST (a band's first wave) takes lane 0's row above from X, the
-        // others from the LDS row, without a per-step select.
-        auto chunk = [&](auto Hc, auto FULLc, auto FIRSTc, int qc) {
-            constexpr int H = decltype(Hc)::value;
-            constexpr bool FULL = decltype(FULLc)::value, FIRST = decltype(FIRSTc)::value;
-            float S0[16];
-            if constexpr (!FIRST) {
-                if (qc >= 0) {
-                    // wave w - 1's last lane must have published chunks 0 .. qc + 4
-                    // (its column 16 qc + 15 comes at its step 16 qc + 78)
-                    const int need = qc + 5 < nq ? qc + 5 : nq;
-                    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&flags[wv - 1], __ATOMIC_RELAXED,
-                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
-                        __builtin_amdgcn_s_sleep(1);
-                    __asm__ volatile("" ::: "memory");  // the row reads stay after the poll
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        const float4 a4 = *reinterpret_cast<const float4 *>(above + 16 * qc + 4 * p);
-                        S0[4 * p] = a4.x;
-                        S0[4 * p + 1] = a4.y;
-                        S0[4 * p + 2] = a4.z;
-                        S0[4 * p + 3] = a4.w;
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) S0[k] = 0.f;
-                }
-            }
-            // this chunk's group 0 at + sof; the refills R groups later
-            const int sof = __builtin_amdgcn_readfirstlane(qc * 4 * 1024);
-            float out[16];
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) {
-                const int g = 4 * H + gg;  // ring slot
-                const f4v p0 = P[g], p1 = P[(g + 1) % R], x0 = X[g], x1 = X[(g + 1) % R], d4 = D[g];
-                f4v o4;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float e = k < 3 ? p0[k + 1] : p1[0];   // slot d + 1
-                    const float xn = k < 3 ? x0[k + 1] : x1[0];  // lane 63: slot d - 63
-                    float s0;
-                    if constexpr (FIRST)
-                        s0 = k == 0 ? x0[3] : x1[k - 1];  // lane 0: slot d + 63
-                    else
-                        s0 = S0[4 * gg + k];
-                    const float n = __int_as_float(__builtin_amdgcn_update_dpp(
-                        __float_as_int(xn), __float_as_int(e), 0x130, 0xf, 0xf, false));  // wave_shl:1
-                    const float S = (CFD_SKEW_EXP & 4) ? vprev
-                                                       : __int_as_float(__builtin_amdgcn_update_dpp(
-                                                             __float_as_int(s0), __float_as_int(vprev), 0x138, 0xf,
-                                                             0xf, false));  // wave_shr:1
-                    const float a = cx * (e + w);
-                    const float bb = cy * (n + S);
-                    const float v = ((a + bb) - d4[k]) * cd;
-                    if constexpr (FULL) {
-                        w = v;
-                        o4[k] = v;
-                    } else {
-                        const int j = 16 * qc + 4 * gg + k - lane;  // step d = 16 qc + 4 gg + k
-                        const bool act = (uint32_t)(j - 1) < (uint32_t)jmax;
-                        w = act ? v : w;
-                        o4[k] = act ? v : 0.f;  // the side columns and the padding stay 0
-                    }
-                    vprev = v;
-                    out[4 * gg + k] = v;
-                }
-                // (groups past the block's DG belong to the next block: the
-                // loop's last iteration runs up to 8 groups past the end)
-                const bool gok = FULL || (qc >= 0 && 4 * qc + gg < DG);
-                if constexpr (!(CFD_SKEW_EXP & 1))
-                    __builtin_amdgcn_raw_buffer_store_b128(o4, rp, gok ? oW + 1024 * gg : (int)kOob, sof, 0);
-                // group G + R's operands into the slot just freed (after its
-                // last use: a load issued before it would need a second
-                // register and a copy that waits for the load).  Slot g is
-                // also read by group G - 1 (done), slot g + 1 by this group
-                // (refilled next).
-                if constexpr (!(CFD_SKEW_EXP & 2)) {
-                    P[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oS + 1024 * gg,
-                                                                                          sof + R * 1024, 0));
-                    D[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rd, oD + 1024 * gg,
-                                                                                          sof + R * 1024, 0));
-                    // (all lanes load X though only lane 63 -- and lane 0 of a
-                    // band's first wave -- reads it: exec-masking the load to
-                    // those lanes measured 8-11 % slower, r05)
-                    X[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oX + 1024 * gg,
-                                                                                          sof + R * 1024, 0));
-                } else {
-                    P[g] += 1.f;
-                }
-                // keep the prefetch where it is: the scheduler would sink it
-                // next to its use, R groups later, exposing the latency
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if (wv + 1 < nw && qc >= 0 && lane == 63) {
-                // publish the last lane's 16 results (columns 16 qc - 63 + k)
-#pragma unroll
-                for (int k = 0; k < 16; ++k) mine[16 * qc - 63 + k] = out[k];
-                // the row before the count (LDS completes in order; this keeps
-                // the compiler from sinking the row writes past the flag)
-                __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __hip_atomic_store(&flags[wv], qc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        };
-        using T1 = std::true_type;
-        using F0 = std::false_type;
-        static_assert(R == 8, "two 16-step chunks per iteration");
-        using H0 = std::integral_constant<int, 0>;
-        using H1 = std::integral_constant<int, 1>;
-        // iterations whose two chunks are both FULL: chunk 2 c >= 4 and
-        // 16 (2 c + 1) + 15 <= jmax; the loop is split into head, middle and
-        // tail loops around them (a per-chunk branch made the register
-        // allocator copy the ring at every merge, waiting for its loads)
-        const int cf0 = 2, cf1 = (jmax - 31) >= 0 ? (jmax - 31) >> 5 : -1;  // [cf0, cf1]
-        const int cm0 = cf1 >= cf0 ? cf0 : nc, cm1 = cf1 >= cf0 ? (cf1 + 1 < nc ? cf1 + 1 : nc) : nc;
-        auto run = [&](auto FIRSTc) {
-#pragma unroll
-            for (int g = 0; g < R; ++g) P[g] = D[g] = X[g] = f4v{0.f, 0.f, 0.f, 0.f};
-            w = 0.f;  // column 0 (boundary)
-            vprev = 0.f;
-            for (int c = -1; c < cm0; ++c) {
-                chunk(H0{}, F0{}, FIRSTc, 2 * c);
-                chunk(H1{}, F0{}, FIRSTc, 2 * c + 1);
-            }
-            for (int c = cm0; c < cm1; ++c) {
-                chunk(H0{}, T1{}, FIRSTc, 2 * c);
-                chunk(H1{}, T1{}, FIRSTc, 2 * c + 1);
-            }
-            for (int c = cm1; c < nc; ++c) {
-                chunk(H0{}, F0{}, FIRSTc, 2 * c);
-                chunk(H1{}, F0{}, FIRSTc, 2 * c + 1);
-            }
-        };
-        if (wv == 0)
-            run(T1{});
-        else
-            run(F0{});
+        lex_skew_wave<false>(sa, m, wv, nw, lane, lex_rows, flags);
     }
+}
+
+// one block per workgroup (the dynamic LDS the launch asks for keeps at most
+// two such workgroups on a CU)
+__global__ __launch_bounds__(64) void k_lex_gs_skew_mc(SkewArgs sa) {
+    lex_skew_wave<true>(sa, (int)blockIdx.x, 0, 1, (int)threadIdx.x, nullptr, nullptr);
 }
 
 // u[1:-1,1:-1] -= grad_x[1:-1,1:-1] (no dt: v5.py:255-256)
@@ -927,7 +1023,7 @@ size_t cfd_clean_divergence_workspace_bytes(int ny, int nx) {
     // or div and two phi in the skewed float32 layout of k_lex_gs_skew,
     // whichever is larger
     const size_t n = (size_t)(ny > 0 ? ny : 0) * (size_t)(nx > 0 ? nx : 0);
-    const size_t skew = ny > 2 && nx > 2 ? 3 * sizeof(float) * lex_skew_floats(ny, nx) : 0;
+    const size_t skew = ny > 2 && nx > 2 ? lex_skew_prog_offset(ny, nx) + 8 * (size_t)lex_skew_blocks(ny) : 0;
     return 2 * sizeof(double) * n > skew ? 2 * sizeof(double) * n : skew;
 }
 
@@ -966,9 +1062,50 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsmax));
             attr_s = true;
         }
+        // past one band, one block per workgroup (k_lex_gs_skew_mc) up to
+        // kSkewMcBlocks blocks: the bands ran one after another on one CU.
+        // Within one band the single workgroup stays: the multi-CU wave is
+        // ~10 % slower per step (sc1 stores, the polls) and lags its
+        // neighbour by ~160 steps (r05: 600 x 180 87 -> 89 us per call with
+        // it, 1026^2 504 -> 403 us)
+        const int nbk = lex_skew_blocks(ny);
+        static const int mc_on = [] {
+            const char *e = getenv("CFD_LEX_SKEW_MC");  // A/B knob: 0 = the banded single-workgroup sweep
+            return e ? atoi(e) : 1;
+        }();
+        const bool mc = mc_on && nbk > kSkewWaves && nbk <= kSkewMcBlocks;
+        if (mc) {
+            static bool attr_mc = false;
+            if (!attr_mc) {
+                CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lex_gs_skew_mc),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSkewMcLds));
+                attr_mc = true;
+            }
+        }
+        SkewArgs sa;
+        sa.phi_base = phi1;
+        sa.div_s = div_s;
+        sa.prog = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(ws) + lex_skew_prog_offset(ny, nx));
+        sa.fail = mc ? persist_fail_word() : nullptr;
+        sa.poll_ticks = persist_poll_ticks();
+        sa.phi_bytes = pbytes;
+        sa.ny = ny;
+        sa.nx = nx;
+        sa.cx = (float)dx2_inv;
+        sa.cy = (float)dy2_inv;
+        sa.cd = (float)denom_inv;
         auto sweep = [&](int old_off, int new_off) {
-            hipLaunchKernelGGL(k_lex_gs_skew, dim3(1), dim3(64 * nw), lds, s, phi1, pbytes, old_off, new_off, div_s,
-                               ny, nx, (float)dx2_inv, (float)dy2_inv, (float)denom_inv);
+            sa.old_off = old_off;
+            sa.new_off = new_off;
+            if (mc) {
+                static std::atomic<unsigned> epoch{0};
+                unsigned e = epoch.fetch_add(1) + 1;
+                if (e == 0) e = epoch.fetch_add(1) + 1;
+                sa.epoch = e;
+                hipLaunchKernelGGL(k_lex_gs_skew_mc, dim3(nbk), dim3(64), kSkewMcLds, s, sa);
+            } else {
+                hipLaunchKernelGGL(k_lex_gs_skew, dim3(1), dim3(64 * nw), lds, s, sa);
+            }
         };
         const dim3 gr(ceil_div(nx, 256), ny - 2);
         if (iterations >= 1) {

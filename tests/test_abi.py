@@ -44,10 +44,11 @@ def test_library_identifies_itself():
     # two row-major float64 fields, or three float32 fields (div, phi1, phi2)
     # in the skewed layout of the f32 sweep (64-row blocks x ceil((nx + 63) / 4)
     # groups of 4 diagonals x 64 rows x 4), the larger
-    def skew(ny, nx):
-        return 3 * 4 * ((ny - 2 + 63) // 64) * ((nx + 63 + 3) // 4) * 256
+    def skew(ny, nx):  # + 8 B of progress word per block, 256-B aligned (the multi-CU sweep)
+        nb = (ny - 2 + 63) // 64
+        return (3 * 4 * nb * ((nx + 63 + 3) // 4) * 256 + 255) // 256 * 256 + 8 * nb
     assert L.cfd_clean_divergence_workspace_bytes(180, 600) == 2 * 8 * 180 * 600
-    assert L.cfd_clean_divergence_workspace_bytes(3, 64) == skew(3, 64) == 98304
+    assert L.cfd_clean_divergence_workspace_bytes(3, 64) == skew(3, 64) == 98304 + 8
     assert L.cfd_clean_divergence_workspace_bytes(67, 3) == skew(67, 3)
     assert L.cfd_clean_divergence_workspace_bytes(2, 5000) == 2 * 8 * 2 * 5000
 
