@@ -278,9 +278,6 @@ __global__ __launch_bounds__(1024) void k_lex_gs_sweep(float *__restrict__ phi,
 // Same arithmetic and order as the serial loop: bit-identical.
 constexpr size_t kLexLdsMax = 160 * 1024;  // LDS a sweep workgroup may take
 constexpr int kSkewWaves = 4;  // waves per band: at one wave per SIMD the chain, not the memory path, sets the pace
-#ifndef CFD_SKEW_EXP
-#define CFD_SKEW_EXP 0  // timing experiments only (wrong results): 1 no stores, 2 no loads, 4 no DPP
-#endif
 constexpr int kSkewRing = 8;   // groups of 4 steps in flight per wave (and per loop iteration)
 constexpr int kSkewMcBlocks = 128;        // k_lex_gs_skew_mc: blocks (workgroups) at most
 constexpr size_t kSkewMcLds = 64 * 1024;  // k_lex_gs_skew_mc: LDS asked for (unused; two per CU at most)
@@ -536,10 +533,8 @@ __device__ inline void lex_skew_wave(const SkewArgs &sa, int m, int wv, int nw, 
                     s0 = S0[4 * gg + k];
                 const float n = __int_as_float(__builtin_amdgcn_update_dpp(
                     __float_as_int(xn), __float_as_int(e), 0x130, 0xf, 0xf, false));  // wave_shl:1
-                const float S = (CFD_SKEW_EXP & 4) ? vprev
-                                                   : __int_as_float(__builtin_amdgcn_update_dpp(
-                                                         __float_as_int(s0), __float_as_int(vprev), 0x138, 0xf,
-                                                         0xf, false));  // wave_shr:1
+                const float S = __int_as_float(__builtin_amdgcn_update_dpp(
+                    __float_as_int(s0), __float_as_int(vprev), 0x138, 0xf, 0xf, false));  // wave_shr:1
                 const float a = cx * (e + w);
                 const float bb = cy * (n + S);
                 const float v = ((a + bb) - d4[k]) * cd;
@@ -558,26 +553,21 @@ __device__ inline void lex_skew_wave(const SkewArgs &sa, int m, int wv, int nw, 
             // (groups past the block's DG belong to the next block: the
             // loop's last iteration runs up to 8 groups past the end)
             const bool gok = FULL || (qc >= 0 && 4 * qc + gg < DG);
-            if constexpr (!(CFD_SKEW_EXP & 1))
-                __builtin_amdgcn_raw_buffer_store_b128(o4, rp, gok ? oW + 1024 * gg : (int)kOob, sof, XA);
+            __builtin_amdgcn_raw_buffer_store_b128(o4, rp, gok ? oW + 1024 * gg : (int)kOob, sof, XA);
             // group G + R's operands into the slot just freed (after its
             // last use: a load issued before it would need a second
             // register and a copy that waits for the load).  Slot g is
             // also read by group G - 1 (done), slot g + 1 by this group
             // (refilled next).
-            if constexpr (!(CFD_SKEW_EXP & 2)) {
-                P[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oS + 1024 * gg,
-                                                                                      sof + R * 1024, 0));
-                D[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rd, oD + 1024 * gg,
-                                                                                      sof + R * 1024, 0));
-                // (all lanes load X though only lane 63 -- and lane 0 of a
-                // band's first wave -- reads it: exec-masking the load to
-                // those lanes measured 8-11 % slower, r05)
-                X[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oX + 1024 * gg,
-                                                                                      sof + R * 1024, XA));
-            } else {
-                P[g] += 1.f;
-            }
+            P[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oS + 1024 * gg,
+                                                                                  sof + R * 1024, 0));
+            D[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rd, oD + 1024 * gg,
+                                                                                  sof + R * 1024, 0));
+            // (all lanes load X though only lane 63 -- and lane 0 of a
+            // band's first wave -- reads it: exec-masking the load to
+            // those lanes measured 8-11 % slower, r05)
+            X[g] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rp, oX + 1024 * gg,
+                                                                                  sof + R * 1024, XA));
             // keep the prefetch where it is: the scheduler would sink it
             // next to its use, R groups later, exposing the latency
             __builtin_amdgcn_sched_barrier(0);
