@@ -483,6 +483,31 @@ def test_last_jacobi2d_path_reports_the_persistent_solve():
         call("cfd_set_small2d_jacobi_persistent", 0, 0)
 
 
+def test_clean_divergence_multi_cu_expiry_fails_loudly():
+    """clean_divergence past one band of row blocks runs one block per
+    workgroup (k_lex_gs_skew_mc), each waiting for the block above's progress
+    word; the wait is bounded like the persistent solves'.  With a 1-tick
+    bound every wait expires at once: no hang, and the failures are counted
+    (cfd_persistent_status).  With the default bound the result is the
+    oracle's again and nothing is counted."""
+    assert K.persistent_failures() == 0
+    ny, nx = 1030, 70  # 16 row blocks: past one band of 4
+    rng = np.random.default_rng(77)
+    u0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+    v0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
+    dx, dy = 20.0 / (nx - 1), 6.0 / (ny - 1)
+    call("cfd_set_persistent_launch", 0, 1)
+    u, v = dev(u0), dev(v0)
+    K.clean_divergence_fast(u, v, dx, dy, iterations=2)
+    assert K.persistent_failures() >= 1
+    call("cfd_set_persistent_launch", 0, 0)
+    u, v = dev(u0), dev(v0)
+    K.clean_divergence_fast(u, v, dx, dy, iterations=2)
+    cu, cv = oracle.clean_divergence2d(u0, v0, dx=dx, dy=dy, iterations=2)
+    assert np.array_equal(host(u), cu) and np.array_equal(host(v), cv)
+    assert K.persistent_failures() == 0
+
+
 def test_persistent_forced_expiry_fails_loudly():
     """A neighbour wait that expires (forced by a 1-tick poll bound) must not
     pass silently: the persistent Jacobi leaves phi all NaN, the persistent
