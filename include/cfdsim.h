@@ -223,7 +223,11 @@ int cfd_project2d_f32(const float *phi, const float *u_star, const float *v_star
 
 /* clean_divergence_fast, v5.py:239-257, with the serial (lexicographic)
  * Gauss-Seidel order of its phi sweep as the defined semantics (under numba's
- * prange that sweep races).  ws: cfd_clean_divergence_workspace_bytes(ny,nx). */
+ * prange that sweep races).  ws: cfd_clean_divergence_workspace_bytes(ny,nx):
+ * the f32 path keeps div and phi in a diagonal-major layout of 64-row blocks
+ * (DESIGN.md §5 Round-5), past 4 blocks one block per workgroup with a
+ * progress word per block in ws (its waits bounded like the persistent
+ * solves', an expired one counted for cfd_persistent_status). */
 size_t cfd_clean_divergence_workspace_bytes(int ny, int nx);
 int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, double dy,
                                int iterations, void *ws, void *stream);
@@ -302,7 +306,7 @@ int cfd_gradient2d_f64(const double *phi, double *grad_x, double *grad_y, int ny
 int cfd_project2d_f64(const double *phi, const double *u_star, const double *v_star, double *u,
                       double *v, int ny, int nx, double dx, double dy, double dt, double *gradmax,
                       void *stream);
-/* ws: cfd_clean_divergence_workspace_bytes(ny, nx) (sized for float64) */
+/* ws: cfd_clean_divergence_workspace_bytes(ny, nx) (at least two float64 fields) */
 int cfd_clean_divergence2d_f64(double *u, double *v, int ny, int nx, double dx, double dy,
                                int iterations, void *ws, void *stream);
 int cfd_apply_bc2d_f64(double *u, double *v, const double *y, int ny, int nx, double y_max,
