@@ -454,6 +454,21 @@ __device__ inline void lex_skew_wave(const SkewArgs &sa, int m, int wv, int nw, 
     // and the compiler's wait counts are the steady-state ones
     f4v P[R], D[R], X[R];
     float w, vprev;  // w: phi(i, j - 1)
+    // !FIRST: the row above for the next chunk, read one chunk ahead, and the
+    // wave above's count read just before it
+    float S0n[16];
+    int s0_flag = 0;
+    auto s0_read = [&](int q) {
+        __asm__ volatile("" ::: "memory");  // after the count read, in issue order
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const float4 a4 = *reinterpret_cast<const float4 *>(above + 16 * q + 4 * p);
+            S0n[4 * p] = a4.x;
+            S0n[4 * p + 1] = a4.y;
+            S0n[4 * p + 2] = a4.z;
+            S0n[4 * p + 3] = a4.w;
+        }
+    };
     // One 16-step chunk (ring slots 4 H .. 4 H + 3).  The step is issue-
     // bound (a wave64 VALU op takes 4 cycles: ~13 per step were ~55 cycles
     // against the ~47-cycle dependent chain), so the chunk is specialised:
@@ -468,23 +483,31 @@ __device__ inline void lex_skew_wave(const SkewArgs &sa, int m, int wv, int nw, 
         if constexpr (!FIRST) {
             if (qc >= 0) {
                 // wave w - 1's last lane must have published chunks 0 .. qc + 4
-                // (its column 16 qc + 15 comes at its step 16 qc + 78)
+                // (its column 16 qc + 15 comes at its step 16 qc + 78).  The
+                // count and the row were read one chunk ago (s0_prefetch);
+                // only when that count fell short are they read again here
                 const int need = qc + 5 < nq ? qc + 5 : nq;
-                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&flags[wv - 1], __ATOMIC_RELAXED,
-                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
-                    __builtin_amdgcn_s_sleep(1);
-                __asm__ volatile("" ::: "memory");  // the row reads stay after the poll
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const float4 a4 = *reinterpret_cast<const float4 *>(above + 16 * qc + 4 * p);
-                    S0[4 * p] = a4.x;
-                    S0[4 * p + 1] = a4.y;
-                    S0[4 * p + 2] = a4.z;
-                    S0[4 * p + 3] = a4.w;
+                if (!(s0_flag >= need)) {
+                    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&flags[wv - 1], __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+                        __builtin_amdgcn_s_sleep(1);
+                    s0_read(qc);
                 }
+#pragma unroll
+                for (int k = 0; k < 16; ++k) S0[k] = S0n[k];
             } else {
 #pragma unroll
                 for (int k = 0; k < 16; ++k) S0[k] = 0.f;
+            }
+            // the next chunk's count and row, in flight during this chunk: the
+            // wait for them no longer stalls a chunk (two LDS round trips a
+            // chunk made the waves that read them ~25 % slower per step).
+            // LDS operations of a wave run in issue order, and the writer
+            // stores the row before the count, so a row read issued after a
+            // count read that saw the writer's count holds the row
+            if (qc + 1 >= 0 && qc + 1 < nq) {
+                s0_flag = __hip_atomic_load(&flags[wv - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                s0_read(qc + 1);
             }
         }
         if constexpr (MC) {
