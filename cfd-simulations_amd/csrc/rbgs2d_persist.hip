@@ -27,21 +27,22 @@
 // tol (a NaN change never raises the reference's max).  So a tile publishes,
 // per block, one granule of flags (bit q: did any own cell change by >= tol in
 // iteration q; ring of 8 blocks; block k's go out at block k + 1's start).  At the end
-// of block k, before block k is published, wave 0 folds every tile's flags of
+// of block k, after block k is published, wave 0 folds every tile's flags of
 // block k - 3 by ballots (their loads were issued at the block's second level,
 // so their latency hides behind the levels; two blocks of slack cover the
 // tiles' skew, ~0.5 block); the first flag-free iteration n stops the solve:
 // every tile then re-runs block B = n / NI from its input (block B - 1's slot,
 // which no tile has overwritten: nobody publishes block k without having ruled
-// out a stop in block k - 3, and the ring holds 4 blocks) for the n - B NI + 1
+// out a stop in block k - 4, and the ring holds 5 blocks) for the n - B NI + 1
 // iterations it needs.  The last three blocks are checked after the loop.  With tol <= 0 nothing is
 // published or polled for the stop rule (it can never fire).
 //
-// Ordering of the granule ring (4 slots): a tile publishes block k over block
-// k - 4's granules only after it has consumed its neighbours' block k - 1
-// output, which they published after reading their block k - 2 input, later
-// than the last read of block k - 4's granules (their block k - 3 input, or a
-// rollback of block k - 3, ruled out before block k is published).  The flag
+// Ordering of the granule ring (5 slots): a tile publishes block k (before
+// its stop decision at the end of block k) over block k - 5's granules only
+// after it has consumed its neighbours' block k - 1 output, which they
+// published after reading their block k - 2 input, later than the last read
+// of block k - 5's granules (their block k - 4 input, or the rollback of a
+// stop in block k - 4, ruled out at the end of block k - 1).  The flag
 // ring (8 blocks): block j's flags go out at block j + 1, after this tile
 // ruled out a stop in block j - 2, so every tile has published block j - 2's
 // flags, i.e. is in block j - 1 or later and reads flags of block j - 4 or
@@ -63,7 +64,7 @@ constexpr int kPW = 16, kPRW = 2, kPT0 = kPW * kPRW;  // waves, rows per wave, t
 #define CFD_GS_LAG 3
 #endif
 constexpr int kPLag = CFD_GS_LAG;                      // the stop test looks kPLag blocks back
-constexpr int kPGSlots = kPLag + 1;                    // granule planes (block outputs)
+constexpr int kPGSlots = kPLag + 2;                    // granule planes (block outputs)
 constexpr int kPMSlots = 8;                            // per-block flag ring (>= kPLag + 2)
 static_assert(kPMSlots >= kPLag + 2, "flag ring too short for the lag");
 constexpr int kPMaxTiles = 256;                        // one tile per CU at most
@@ -248,6 +249,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
     // tile's flags of block k - 1 at the second level and folds every tile's
     // flags of block k - 3 after the last level (the stop decision, in sh_stop
     // after the block's last barrier).
+    const int nb = (a.niters + NI - 1) / NI;
     bool hot[NI];  // per lane: an own cell changed by >= tol (a NaN change never counts, as in v5.py:221)
     const bool own_rows = kPRW * w + 1 >= L && kPRW * w < kPT0 - L;  // wave-uniform
     auto levels = [&](int m, int k) {
@@ -356,6 +358,17 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
             if (l < 2 * m) lds_barrier_p();
         }
         }
+        // block k's output goes out before the stop decision, so the fold
+        // and the barrier do not delay the neighbours' next block.  It takes
+        // the slot of block k - kPLag - 2: a stop in block k - kPLag - 1 or
+        // earlier was ruled out at the end of block k - 1, and the rollback of
+        // a stop in block k - kPLag (decided below) reads block k - kPLag - 1's
+        // slot, hence kPLag + 2 slots
+        if (k >= 0 && (k + 1 < nb || check)) {
+#pragma unroll
+            for (int j = 0; j < kPRW; ++j)
+                if (own[j]) gstore(a.G + (size_t)(k % kPGSlots) * plane + off[j], A[j], (unsigned)(k + 1));
+        }
         // the last level's barrier, behind the stop decision
         if (check && k >= kPLag && w == 0) {
             const int n = fold_maxima(k - kPLag, NI);
@@ -365,7 +378,6 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         if (a.trace && k >= 0 && w == 0 && lane == 0) a.trace[((size_t)k * a.ntiles + bid) * 4 + 3] = wall_clock64();
     };
 
-    const int nb = (a.niters + NI - 1) / NI;
     int stop = -1;  // first iteration meeting the tolerance (workgroup-uniform)
     if (w == 0) sh_stop = -1;
     if (w == 0 && lane < NI) busy[lane] = 0;
@@ -383,11 +395,6 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                 for (int q = 0; q < NI; ++q)
                     if (__any(hot[q]) && lane == 0) busy[q] = 1;
             }
-        }
-        if (k + 1 < nb || check) {  // the last block's granules are read only by a rollback
-#pragma unroll
-            for (int j = 0; j < kPRW; ++j)
-                if (own[j]) gstore(a.G + (size_t)(k % kPGSlots) * plane + off[j], A[j], (unsigned)(k + 1));
         }
     }
     if (check && stop < 0) {
