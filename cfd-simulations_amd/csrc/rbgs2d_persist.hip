@@ -289,30 +289,31 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                     const f2 nh = ((a.cx * (f2{dpp_from_upper(A[1]), dpp_from_upper(up1)} +
                                             f2{dpp_from_lower(A[1]), dpp_from_lower(up1)}) +
                                     a.cy * (f2{up1, up2} + f2{A[0], A[1]})) - rhu) * a.cd;
-                    const bool ul0 = (i0 - 1 >= l && i0 - 1 < kPT0 - l) && U0h[0];
-                    const bool ul1 = (i0 >= l && i0 < kPT0 - l) && U0[0];
-                    const bool uh0 = (i0 + 1 >= l && i0 + 1 < kPT0 - l) && U0[1];
-                    const bool uh1 = (i0 + 2 >= l && i0 + 2 < kPT0 - l) && U0h[1];
+                    // no per-row liveness test: a row outside level l's live
+                    // rows [l, 32 - l) is read at level l + 1 only by rows
+                    // outside [l + 1, 31 - l), so updating it changes no live
+                    // cell (and the masks stay loop-invariant)
+                    const bool ul0 = U0h[0], ul1 = U0[0], uh0 = U0[1], uh1 = U0h[1];
                     const float q0 = ul0 ? nl[0] : cl[0], q1 = ul1 ? nl[1] : cl[1];
                     const float q2 = uh0 ? nh[0] : ch2[0], q3 = uh1 ? nh[1] : ch2[1];
                     if (check && own_rows) {
+                        // bitwise, not short-circuit: no exec-mask branches
                         const f2 dl = nl - cl, dh = nh - ch2;
-                        hot[p - 1] = hot[p - 1] || (own[0] && ul1 && fabsf(dl[1]) >= a.tol) ||
-                                     (own[1] && uh0 && fabsf(dh[0]) >= a.tol);
+                        hot[p - 1] = hot[p - 1] | (own[0] & ul1 & (fabsf(dl[1]) >= a.tol)) |
+                                     (own[1] & uh0 & (fabsf(dh[0]) >= a.tol));
                     }
                     // level l + 1 (colour 1): rows i0, i0 + 1 from q0..q3
                     const f2 c2 = {q1, q2};
                     const f2 nv = ((a.cx * (f2{dpp_from_upper(q1), dpp_from_upper(q2)} +
                                             f2{dpp_from_lower(q1), dpp_from_lower(q2)}) +
                                     a.cy * (f2{q2, q3} + f2{q0, q1})) - rh) * a.cd;
-                    const bool v0 = (i0 >= l + 1 && i0 < kPT0 - l - 1) && U1[0];
-                    const bool v1 = (i0 + 1 >= l + 1 && i0 + 1 < kPT0 - l - 1) && U1[1];
+                    const bool v0 = U1[0], v1 = U1[1];
                     A[0] = v0 ? nv[0] : c2[0];
                     A[1] = v1 ? nv[1] : c2[1];
                     if (check && own_rows) {
                         const f2 d2 = nv - c2;
-                        hot[p - 1] = hot[p - 1] || (own[0] && v0 && fabsf(d2[0]) >= a.tol) ||
-                                     (own[1] && v1 && fabsf(d2[1]) >= a.tol);
+                        hot[p - 1] = hot[p - 1] | (own[0] & v0 & (fabsf(d2[0]) >= a.tol)) |
+                                     (own[1] & v1 & (fabsf(d2[1]) >= a.tol));
                     }
                     S[wb][i0][lane] = A[0];
                     S[wb][i0 + 1][lane] = A[1];
