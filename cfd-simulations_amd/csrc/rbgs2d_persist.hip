@@ -252,6 +252,24 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
     const int nb = (a.niters + NI - 1) / NI;
     bool hot[NI];  // per lane: an own cell changed by >= tol (a NaN change never counts, as in v5.py:221)
     const bool own_rows = kPRW * w + 1 >= L && kPRW * w < kPT0 - L;  // wave-uniform
+    // PAIRS: the colour masks as VGPR bit masks (v_bfi_b32 selects) and the
+    // stop threshold as a per-lane VGPR (tol on a lane of own cells, NaN
+    // elsewhere: no compare is true).  As 64-bit lane masks they outgrew the
+    // SGPRs, and every select read its mask back with two v_readlane.
+    auto vmask = [](bool b) {
+        uint32_t m = b ? ~0u : 0u;
+        __asm__ volatile("" : "+v"(m));
+        return m;
+    };
+    const uint32_t mU0h0 = vmask(U0h[0]), mU00 = vmask(U0[0]), mU01 = vmask(U0[1]), mU0h1 = vmask(U0h[1]);
+    const uint32_t mU10 = vmask(U1[0]), mU11 = vmask(U1[1]);
+    float tolv = own[0] ? a.tol : __int_as_float(0x7fc00000);
+    __asm__ volatile("" : "+v"(tolv));
+    auto bsel = [](uint32_t m, float t, float f) {  // (t & m) | (f & ~m), one v_bfi_b32
+        float r;
+        __asm__("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(t), "v"(f));
+        return r;
+    };
     auto levels = [&](int m, int k) {
 #pragma unroll
         for (int q = 0; q < NI; ++q) hot[q] = false;
@@ -293,27 +311,31 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                     // rows [l, 32 - l) is read at level l + 1 only by rows
                     // outside [l + 1, 31 - l), so updating it changes no live
                     // cell (and the masks stay loop-invariant)
-                    const bool ul0 = U0h[0], ul1 = U0[0], uh0 = U0[1], uh1 = U0h[1];
-                    const float q0 = ul0 ? nl[0] : cl[0], q1 = ul1 ? nl[1] : cl[1];
-                    const float q2 = uh0 ? nh[0] : ch2[0], q3 = uh1 ? nh[1] : ch2[1];
+                    const float q0 = bsel(mU0h0, nl[0], cl[0]), q1 = bsel(mU00, nl[1], cl[1]);
+                    const float q2 = bsel(mU01, nh[0], ch2[0]), q3 = bsel(mU0h1, nh[1], ch2[1]);
+                    // the stop test's largest change of the wave's own-row cells
+                    // in this iteration: the change of the SELECTED values, 0
+                    // for a cell the colour leaves alone; fmaxf drops a NaN
+                    // change (it never counts, v5.py:221)
+                    float dmax = 0.f;
                     if (check && own_rows) {
-                        // bitwise, not short-circuit: no exec-mask branches
-                        const f2 dl = nl - cl, dh = nh - ch2;
-                        hot[p - 1] = hot[p - 1] | (own[0] & ul1 & (fabsf(dl[1]) >= a.tol)) |
-                                     (own[1] & uh0 & (fabsf(dh[0]) >= a.tol));
+                        const f2 d0 = f2{q1, q2} - f2{cl[1], ch2[0]};
+                        dmax = fmaxf(fmaxf(fabsf(d0[0]), fabsf(d0[1])), dmax);
                     }
                     // level l + 1 (colour 1): rows i0, i0 + 1 from q0..q3
                     const f2 c2 = {q1, q2};
                     const f2 nv = ((a.cx * (f2{dpp_from_upper(q1), dpp_from_upper(q2)} +
                                             f2{dpp_from_lower(q1), dpp_from_lower(q2)}) +
                                     a.cy * (f2{q2, q3} + f2{q0, q1})) - rh) * a.cd;
-                    const bool v0 = U1[0], v1 = U1[1];
-                    A[0] = v0 ? nv[0] : c2[0];
-                    A[1] = v1 ? nv[1] : c2[1];
+                    A[0] = bsel(mU10, nv[0], c2[0]);
+                    A[1] = bsel(mU11, nv[1], c2[1]);
                     if (check && own_rows) {
-                        const f2 d2 = nv - c2;
-                        hot[p - 1] = hot[p - 1] | (own[0] & v0 & (fabsf(d2[0]) >= a.tol)) |
-                                     (own[1] & v1 & (fabsf(d2[1]) >= a.tol));
+                        const f2 d1 = f2{A[0], A[1]} - c2;
+                        dmax = fmaxf(fmaxf(fabsf(d1[0]), fabsf(d1[1])), dmax);
+                        // own[0] covers own[1] wherever row i0 + 1 can change
+                        // (i0 and L even: both rows own or neither; past the
+                        // last interior row nothing is updated)
+                        hot[p - 1] = dmax >= tolv;
                     }
                     S[wb][i0][lane] = A[0];
                     S[wb][i0 + 1][lane] = A[1];
