@@ -140,6 +140,17 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
 
     // sweeps 1..m of one block: level l keeps the tile rows [l, 32 - l); a
     // wave whose two rows are both dead at level l skips it
+    // (s2 - rh) * 0.25 on the two rows as two packed ops: left to itself the
+    // compiler splits both into scalar pairs (v_pk_mul_f32 takes no literal,
+    // and the selects that follow are per row); the same IEEE operations
+    f2 quarter = {0.25f, 0.25f};
+    __asm__ volatile("" : "+v"(quarter));
+    auto pk_quarter_diff = [&](f2 s2v) {
+        f2 d, r;
+        __asm__("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(s2v), "v"(rh));
+        __asm__("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(d), "v"(quarter));
+        return r;
+    };
     auto levels = [&](int m) {
 #pragma unroll
         for (int j = 0; j < kJRW; ++j) S[0][i0 + j][lane] = A[j];
@@ -156,7 +167,7 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
                 f2 s2 = e2 + w2;
                 s2 = s2 + f2{A[1], up};  // N
                 s2 = s2 + f2{dn, A[0]};  // S
-                const f2 nv = 0.25f * (s2 - rh);
+                const f2 nv = pk_quarter_diff(s2);
 #pragma unroll
                 for (int j = 0; j < kJRW; ++j) {
                     float b = upd[j] ? nv[j] : A[j];
