@@ -151,7 +151,14 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
         __asm__("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(d), "v"(quarter));
         return r;
     };
-    auto levels = [&](int m) {
+    // after the first sweep every masked cell of the tile holds 0 (each wave
+    // has a live row at sweep 1, halo cells arrive zeroed from their owners,
+    // cells no tile owns keep their sweep-1 zero), so later sweeps need one
+    // select: upd && !zero ? new : old
+    bool updnz[kJRW];
+#pragma unroll
+    for (int j = 0; j < kJRW; ++j) updnz[j] = upd[j] && !zero[j];
+    auto levels = [&](int m, int k) {
 #pragma unroll
         for (int j = 0; j < kJRW; ++j) S[0][i0 + j][lane] = A[j];
         lds_barrier_j();
@@ -168,12 +175,21 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
                 s2 = s2 + f2{A[1], up};  // N
                 s2 = s2 + f2{dn, A[0]};  // S
                 const f2 nv = pk_quarter_diff(s2);
+                if (MASK && k == 0 && l == 1) {  // block-uniform
 #pragma unroll
-                for (int j = 0; j < kJRW; ++j) {
-                    float b = upd[j] ? nv[j] : A[j];
-                    if (MASK && zero[j]) b = 0.f;
-                    A[j] = b;
-                    S[wb][i0 + j][lane] = b;
+                    for (int j = 0; j < kJRW; ++j) {
+                        float b = upd[j] ? nv[j] : A[j];
+                        if (zero[j]) b = 0.f;
+                        A[j] = b;
+                        S[wb][i0 + j][lane] = b;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kJRW; ++j) {
+                        const float b = (MASK ? updnz[j] : upd[j]) ? nv[j] : A[j];
+                        A[j] = b;
+                        S[wb][i0 + j][lane] = b;
+                    }
                 }
             }
             if (l < m) lds_barrier_j();
@@ -184,7 +200,7 @@ __global__ __launch_bounds__(1024) void jacobi2d_persist(JPersistArgs a) {
     for (int k = 0; k < nb; ++k) {
         const int m = min(NI, a.niters - k * NI);
         if (k > 0) fetch(k);
-        levels(m);
+        levels(m, k);
         if (k + 1 < nb) {
 #pragma unroll
             for (int j = 0; j < kJRW; ++j)
