@@ -94,6 +94,11 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--transport", default="ce", choices=["ce", "rccl"],
                     help="slab halo transport: copy engines over IPC (default) or RCCL send/recv")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal of the N-rank path on ONE GPU: every rank on device 0, a gloo "
+                         "process group, the copy-engine transport (timing is not a scaling number)")
+    ap.add_argument("--grid", default="",
+                    help="3-D workloads: override the grid as NZ,NY,NX (e.g. a small rbgs3d rehearsal)")
     ap.add_argument("--no-rhs-ws", action="store_true", help="form the RHS in-register every sweep")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="skip the N>1 parity check")
@@ -398,8 +403,11 @@ def spawn_ranks(args, argv, run=None, device_count=None):
     if device_count is None:
         import torch
         device_count = torch.cuda.device_count()
-    if device_count < n:
+    need = 1 if getattr(args, "shared_gpu", False) else n
+    if device_count < need:
         raise SystemExit(f"--gpus {n}: only {device_count} GPU(s) visible on this node")
+    if getattr(args, "shared_gpu", False) and args.transport != "ce":
+        raise SystemExit("--shared-gpu runs the copy-engine transport (RCCL refuses two ranks on one device)")
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -430,10 +438,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != ARGS.gpus:
         print(f"WARNING: --gpus {ARGS.gpus} but WORLD_SIZE={world}: running {world} rank(s)", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if ARGS.shared_gpu and ARGS.transport != "ce":
+        raise SystemExit("--shared-gpu runs the copy-engine transport (RCCL refuses two ranks on one device)")
+    # --shared-gpu: every rank on device 0 (the rehearsal of the N-rank path on
+    # a one-GPU lease); otherwise one GPU per rank
+    local_dev = 0 if ARGS.shared_gpu else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     use_slab = world > 1 or ARGS.force_slab
-    if use_slab:
+    if use_slab and ARGS.shared_gpu:
+        # RCCL refuses two ranks on one device: the process group (IPC blob
+        # exchange, verification gathers, the timing max) runs on gloo
+        dist.init_process_group("gloo")
+    elif use_slab:
         # bound RCCL's send/recv kernel to 16 blocks: the overlapped slab
         # drivers confine the exchange to 16 reserved CUs (slab.hip,
         # partition_streams), where up to 48 such blocks fit at once
@@ -441,6 +458,11 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     shape, dt_name, iters_default, bpc = WORKLOADS[ARGS.workload]
+    if ARGS.grid:
+        grid = tuple(int(x) for x in ARGS.grid.split(","))
+        if len(shape) != 3 or len(grid) != 3 or min(grid) < 8:
+            raise SystemExit("--grid NZ,NY,NX applies to the 3-D workloads (each extent >= 8)")
+        shape = grid
     iters = ARGS.iters or iters_default
     call("cfd_set_jacobi3d_config", ARGS.variant, ARGS.waves, ARGS.zchunk)
     if len(shape) == 3:
@@ -566,7 +588,7 @@ def main():
     sweep_ms = ms.value / max(nsw.value, 1)
 
     if use_slab:
-        t = torch.tensor([elapsed, sweep_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, sweep_ms], dtype=torch.float64, device=coll_device(dist, dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, sweep_ms_max = float(t[0]), float(t[1])
     else:
@@ -592,7 +614,7 @@ def main():
     launch_ms = sweep_ms * spl
     alg_bytes = cells_rank * bpc  # one pass moves bpc bytes per cell whatever it fuses
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-    traffic = load_traffic(ARGS.workload, world)
+    traffic = None if ARGS.grid else load_traffic(ARGS.workload, world)
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -631,6 +653,9 @@ def main():
         out["config"]["tolerance"] = GS_TOL
         out["config"]["iterations_done_last_step"] = int(gs_done.item())
         out["roofline"]["bytes_per_cell_update"] = bpc / spl if blocked else 2 * bpc
+    if ARGS.shared_gpu and use_slab:
+        out["config"]["shared_gpu"] = (f"rehearsal: {world} ranks (processes) on device 0, gloo process group; "
+                                       f"the timing is not a scaling number")
     if verified is not None:
         out["config"]["multi_gpu_parity"] = (("bit-exact vs 1-GPU solve (96^3, 9 its + early stop, both ghost depths)"
                                               if gs else
@@ -669,6 +694,8 @@ def make_comm(S, rank, world):
         except Exception as e:  # noqa: BLE001 -- reported, then RCCL
             if comm is not None:
                 comm.close()
+            if ARGS.shared_gpu:
+                raise
             print(f"WARNING: copy-engine transport unavailable ({e}); using RCCL", file=sys.stderr)
     TRANSPORT = "rccl"
     return S.RcclComm(rank, world)
@@ -702,12 +729,12 @@ def verify_slabs(S, K, dist, comm, world, rank, dev):
         mine = sj.owned().contiguous()
         sizes = [S.SlabPlan(nz, world, r, ghost=ghost).nz_local for r in range(world)]
         parts = [torch.empty((n, ny, nx), dtype=torch.float32, device=dev) for n in sizes]
-        dist.all_gather(parts, mine) if len(set(sizes)) == 1 else _gather_uneven(dist, parts, mine, rank)
+        parts = gather_planes(dist, parts, mine, rank, dev)
         if rank == 0:
             ref = torch.zeros_like(div)
             K.solve_pressure_jacobi3d(ref, div, 0.03, np.float32(1e-3), None, iters)
             ok &= bool(torch.equal(torch.cat(parts), ref))
-    flag = torch.tensor([1 if ok else 0], device=dev)
+    flag = torch.tensor([1 if ok else 0], device=coll_device(dist, dev))
     dist.broadcast(flag, src=0)
     if not bool(flag.item()) and rank == 0:
         print("WARNING: multi-GPU slab result differs from the single-GPU solve", file=sys.stderr)
@@ -733,7 +760,7 @@ def verify_slabs_rbgs(S, K, dist, comm, world, rank, dev):
         mine = sg.owned().contiguous()
         sizes = [S.SlabPlan(nz, world, r, ghost=ghost).nz_local for r in range(world)]
         parts = [torch.empty((n, ny, nx), dtype=torch.float32, device=dev) for n in sizes]
-        dist.all_gather(parts, mine) if len(set(sizes)) == 1 else _gather_uneven(dist, parts, mine, rank)
+        parts = gather_planes(dist, parts, mine, rank, dev)
         n_mine = int(sg.iters_done.item())
         if rank == 0:
             ref = torch.zeros_like(div)
@@ -741,18 +768,34 @@ def verify_slabs_rbgs(S, K, dist, comm, world, rank, dev):
             K.solve_pressure_gauss_seidel3d(ref, div, 0.05, 0.05, 0.05, np.float32(1e-2), None, iters, tol,
                                             iters_done=done)
             ok &= bool(torch.equal(torch.cat(parts), ref)) and n_mine == int(done.item())
-    flag = torch.tensor([1 if ok else 0], device=dev)
+    flag = torch.tensor([1 if ok else 0], device=coll_device(dist, dev))
     dist.broadcast(flag, src=0)
     if not bool(flag.item()) and rank == 0:
         print("WARNING: multi-GPU RB-GS result differs from the single-GPU solve", file=sys.stderr)
     return bool(flag.item())
 
 
-def _gather_uneven(dist, parts, mine, rank):
-    for r, p in enumerate(parts):
-        if r == rank:
-            p.copy_(mine)
-        dist.broadcast(p, src=r)
+def coll_device(dist, dev):
+    """Where a tensor of a torch.distributed collective lives: the GPU under
+    RCCL, the host under gloo (the --shared-gpu rehearsal)."""
+    import torch
+    return dev if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def gather_planes(dist, parts, mine, rank, dev):
+    """All-gather every rank's owned planes into `parts` (rank order), equal or
+    uneven counts, on the process group's device; returns them on `dev`."""
+    cd = coll_device(dist, dev)
+    mine = mine.to(cd)
+    parts = [p.to(cd) for p in parts]
+    if len({p.shape for p in parts}) == 1:
+        dist.all_gather(parts, mine)
+    else:
+        for r, p in enumerate(parts):
+            if r == rank:
+                p.copy_(mine)
+            dist.broadcast(p, src=r)
+    return [p.to(dev) for p in parts]
 
 
 def tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells, rhs=None):

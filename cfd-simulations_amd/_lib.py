@@ -51,9 +51,11 @@ PROTOTYPES = {
                                     c_float, c_int, P]),
     "cfd_set_predictor2d_config": (c_int, [c_int, c_int, c_int]),
     "cfd_set_predictor2d_tau_mode": (c_int, [c_int]),
+    "cfd_get_predictor2d_tau_mode": (c_int, []),
     "cfd_get_last_predictor2d_path": (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "cfd_set_persistent_launch": (c_int, [c_int, ctypes.c_longlong]),
     "cfd_persistent_status": (c_int, [P]),
+    "cfd_persistent_status_stream": (c_int, [P, P]),
     "cfd_release_thread_resources": (c_int, []),
     "cfd_divergence2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, P, P]),
     "cfd_gradient2d_f32": (c_int, [P, P, P, c_int, c_int, c_double, c_double, P]),

@@ -20,7 +20,11 @@ void set_error(const char *fmt, ...) {
 // with a HIP event pair recorded on the stream it launches on.
 // The event pool is reused after each cfd_timing_read(reset) / enable and
 // capped: past kMaxPairs unread solves, further solves are not timed and the
-// next read reports the overflow.  A thread's events are released when it exits.
+// next read reports the overflow.  Nothing here runs at thread or process
+// exit: a destructor calling hipEventDestroy would run from exit(), where the
+// HIP runtime's own teardown (an exit handler of libamdhip64) may already have
+// released the device (the r05 exit-time SIGSEGV).  The events
+// are released by cfd_release_thread_resources, or with the process.
 struct Timing {
     static constexpr size_t kMaxPairs = 1 << 14;
     bool on = false, overflow = false;
@@ -28,13 +32,22 @@ struct Timing {
     std::vector<long long> sweeps;
     std::vector<int> channel;
     size_t used = 0;
-    ~Timing() {
-        // return codes ignored: at process exit the runtime may already be gone
-        for (hipEvent_t e : start) (void)hipEventDestroy(e);
-        for (hipEvent_t e : stop) (void)hipEventDestroy(e);
-    }
 };
 static thread_local Timing g_timing;  // per host thread, like the tuning knobs
+
+static void release_thread_timing() {
+    for (size_t k = 0; k < g_timing.start.size(); ++k) {
+        (void)hipEventSynchronize(g_timing.stop[k]);
+        (void)hipEventDestroy(g_timing.start[k]);
+        (void)hipEventDestroy(g_timing.stop[k]);
+    }
+    g_timing.start.clear();
+    g_timing.stop.clear();
+    g_timing.sweeps.clear();
+    g_timing.channel.clear();
+    g_timing.used = 0;
+    g_timing.overflow = false;
+}
 
 // Process defaults of the tuning knobs: the CFD_* environment variables (A/B
 // knobs of the bench scripts), validated, read once.
@@ -108,22 +121,48 @@ void timing_end(int k, hipStream_t s, long long sweeps) {
     (void)hipEventRecord(g_timing.stop[k], s);
 }
 
-int *persist_fail_word() {
-    static std::mutex mu;
-    static int *word[64] = {};
+// Failure words of the persistent solves, one per (device, stream): a solve
+// counts its expired waits into the word of the stream it runs on, and
+// cfd_persistent_status_stream reads and clears that word with an async copy
+// on the same stream (no device-wide synchronisation, no other stream's
+// failures consumed).  Kept for the life of the process (never freed at exit).
+namespace {
+struct FailWords {
+    std::mutex mu;
+    std::map<std::pair<int, hipStream_t>, int *> words;
+};
+FailWords &fail_words() {
+    static FailWords *f = new FailWords;  // never destroyed: no exit-time teardown
+    return *f;
+}
+}  // namespace
+
+int *persist_fail_word(hipStream_t s, bool create) {
+    thread_local int c_dev = -1;
+    thread_local hipStream_t c_s = nullptr;
+    thread_local int *c_w = nullptr;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    if (!word[dev]) {
-        int *p = nullptr;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (c_w && c_dev == dev && c_s == s) return c_w;
+    FailWords &f = fail_words();
+    std::lock_guard<std::mutex> lk(f.mu);
+    auto it = f.words.find({dev, s});
+    int *p = it == f.words.end() ? nullptr : it->second;
+    if (!p && create) {
         if (hipMalloc(&p, 256) != hipSuccess) return nullptr;
-        if (hipMemset(p, 0, 256) != hipSuccess) {
+        // zeroed on the stream that will use it, ahead of its first solve
+        if (hipMemsetAsync(p, 0, 256, s) != hipSuccess) {
             (void)hipFree(p);
             return nullptr;
         }
-        word[dev] = p;
+        f.words[{dev, s}] = p;
     }
-    return word[dev];
+    if (p) {
+        c_dev = dev;
+        c_s = s;
+        c_w = p;
+    }
+    return p;
 }
 
 unsigned *energy_scratch(hipStream_t s) {
@@ -136,7 +175,9 @@ unsigned *energy_scratch(hipStream_t s) {
     if (!p) {
         const size_t bytes = 64 + kEnergyBlocks * sizeof(double);
         if (hipMalloc(&p, bytes) != hipSuccess) return p = nullptr;
-        if (hipMemset(p, 0, bytes) != hipSuccess) {
+        // on s, ahead of the first k_energy_mean_mb (s may be a non-blocking
+        // stream, which the null stream does not order)
+        if (hipMemsetAsync(p, 0, bytes, s) != hipSuccess) {
             (void)hipFree(p);
             return p = nullptr;
         }
@@ -144,8 +185,46 @@ unsigned *energy_scratch(hipStream_t s) {
     return p;
 }
 
+// Persistent launches of this process on one device run one at a time: each
+// waits (on the device) for the previous one, whatever stream or host thread
+// launched it.  A plain launch rests on the occupancy check, which assumes the
+// chip is otherwise free of persistent tiles; two persistent solves on two
+// streams could each end up partly resident, every resident tile waiting for a
+// neighbour that cannot start until the poll bound expires.  The chain costs
+// one event record per solve.  (Across processes on one device nothing orders
+// them: cfd_set_persistent_launch(1, ...) -- cooperative launches -- is the
+// setting for that.)
+namespace {
+struct PersistOrder {
+    std::mutex mu;
+    hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;
+    bool any = false;
+};
+PersistOrder *persist_order(int dev) {
+    static PersistOrder *o = new PersistOrder[64];  // never destroyed
+    return dev >= 0 && dev < 64 ? &o[dev] : nullptr;
+}
+}  // namespace
+
 int launch_persistent(const void *f, int nblocks, int threads, void *args, hipStream_t s) {
     void *kargs[] = {args};
+    int dev = 0;
+    PersistOrder *o = hipGetDevice(&dev) == hipSuccess ? persist_order(dev) : nullptr;
+    if (!o) {
+        set_error("persistent launch: no device");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(o->mu);
+    if (!o->ev && hipEventCreateWithFlags(&o->ev, hipEventDisableTiming) != hipSuccess) {
+        o->ev = nullptr;
+        set_error("persistent launch: event creation failed");
+        return -1;
+    }
+    if (o->any && o->last != s && hipStreamWaitEvent(s, o->ev, 0) != hipSuccess) {
+        set_error("persistent launch: ordering after the previous persistent solve failed");
+        return -1;
+    }
     hipError_t e;
     if (tuning().persist_coop) {
         e = hipLaunchCooperativeKernel(f, dim3(nblocks), dim3(threads), kargs, 0, s);
@@ -160,6 +239,12 @@ int launch_persistent(const void *f, int nblocks, int threads, void *args, hipSt
         (void)hipGetLastError();
         set_error("persistent launch failed: %s", hipGetErrorString(e));
         return -1;
+    }
+    if (hipEventRecord(o->ev, s) == hipSuccess) {
+        o->last = s;
+        o->any = true;
+    } else {
+        o->any = false;  // nothing to wait for: the next launch orders by its stream only
     }
     return 1;
 }
@@ -188,18 +273,39 @@ int cfd_set_persistent_launch(int cooperative, long long poll_ticks) {
 int cfd_persistent_status(int *expired) {
     CFD_REQUIRE(expired, "persistent_status: null pointer");
     *expired = 0;
-    int *w = persist_fail_word();
-    CFD_REQUIRE(w, "persistent_status: no status word on this device");
+    int dev = 0;
+    CFD_CHECK_HIP(hipGetDevice(&dev));
     CFD_CHECK_HIP(hipDeviceSynchronize());
-    int h = 0;
-    CFD_CHECK_HIP(hipMemcpy(&h, w, sizeof(int), hipMemcpyDeviceToHost));
-    if (h) CFD_CHECK_HIP(hipMemset(w, 0, sizeof(int)));
-    *expired = h;
+    FailWords &f = fail_words();
+    std::lock_guard<std::mutex> lk(f.mu);
+    for (auto &kv : f.words) {
+        if (kv.first.first != dev) continue;
+        int h = 0;
+        CFD_CHECK_HIP(hipMemcpy(&h, kv.second, sizeof(int), hipMemcpyDeviceToHost));
+        if (h) CFD_CHECK_HIP(hipMemset(kv.second, 0, sizeof(int)));
+        *expired += h;
+    }
+    return CFD_OK;
+}
+
+int cfd_persistent_status_stream(void *stream, int *expired) {
+    CFD_REQUIRE(expired, "persistent_status_stream: null pointer");
+    *expired = 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int *w = persist_fail_word(s, false);
+    if (!w) return CFD_OK;  // no persistent solve has run on this stream
+    thread_local int *host = nullptr;  // pinned: the copy is a true async one
+    if (!host) CFD_CHECK_HIP(hipHostMalloc(reinterpret_cast<void **>(&host), 64, hipHostMallocDefault));
+    CFD_CHECK_HIP(hipMemcpyAsync(host, w, sizeof(int), hipMemcpyDeviceToHost, s));
+    CFD_CHECK_HIP(hipMemsetAsync(w, 0, sizeof(int), s));
+    CFD_CHECK_HIP(hipStreamSynchronize(s));
+    *expired = *host;
     return CFD_OK;
 }
 
 int cfd_release_thread_resources(void) {
     release_thread_rings();
+    release_thread_timing();
     return CFD_OK;
 }
 
@@ -292,7 +398,19 @@ int cfd_timing_read_channel(int channel, double *ms, long long *sweeps, int rese
     *ms = total;
     *sweeps = n;
     if (reset) {
-        g_timing.used = 0;
+        // drop this channel's pairs only: the other channel's unread timings stay
+        size_t j = 0;
+        for (size_t k = 0; k < g_timing.used; ++k) {
+            if (g_timing.channel[k] == channel) continue;
+            if (j != k) {
+                std::swap(g_timing.start[j], g_timing.start[k]);
+                std::swap(g_timing.stop[j], g_timing.stop[k]);
+                std::swap(g_timing.sweeps[j], g_timing.sweeps[k]);
+                std::swap(g_timing.channel[j], g_timing.channel[k]);
+            }
+            ++j;
+        }
+        g_timing.used = j;
         g_timing.overflow = false;
     }
     return CFD_OK;

@@ -984,6 +984,8 @@ int cfd_set_predictor2d_tau_mode(int mode) {
     return CFD_OK;
 }
 
+int cfd_get_predictor2d_tau_mode(void) { return tuning().pred_tau; }
+
 int cfd_get_last_predictor2d_path(int *tau_mode, int *cells_per_lane) {
     if (tau_mode) *tau_mode = g_last_pred[1];
     if (cells_per_lane) *cells_per_lane = g_last_pred[2];
@@ -1068,7 +1070,10 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
         }();
         int nw = lex_skew_blocks(ny) < wmax ? lex_skew_blocks(ny) : wmax;
         while (nw > 1 && lex_skew_lds_bytes(nw, nx) > ldsmax) --nw;
-        const size_t lds = lex_skew_lds_bytes(nw, nx);
+        // one wave per band neither publishes nor reads a row through LDS (no
+        // wave below it, and a band's first wave takes the row above from
+        // memory): no dynamic LDS, whatever nx (short, very wide grids)
+        const size_t lds = nw > 1 ? lex_skew_lds_bytes(nw, nx) : 0;
         static bool attr_s = false;
         if (!attr_s) {
             CFD_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lex_gs_skew),
@@ -1099,7 +1104,7 @@ int cfd_clean_divergence2d_f32(float *u, float *v, int ny, int nx, double dx, do
         sa.phi_base = phi1;
         sa.div_s = div_s;
         sa.prog = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(ws) + lex_skew_prog_offset(ny, nx));
-        sa.fail = mc ? persist_fail_word() : nullptr;
+        sa.fail = mc ? persist_fail_word(s) : nullptr;
         sa.poll_ticks = persist_poll_ticks();
         sa.phi_bytes = pbytes;
         sa.ny = ny;

@@ -71,10 +71,12 @@ struct Tuning {
     int persist_coop = 0;
     unsigned long long persist_poll = 0;
 };
-// The current device's failure counter of persistent solves (a device int,
-// process-wide, allocated on first use): a solve whose poll expired adds 1;
-// cfd_persistent_status reads and clears it.  nullptr if allocation failed.
-int *persist_fail_word();
+// The failure counter of persistent solves on the current device and stream
+// s (a device int, allocated on first use when create): a solve whose poll
+// expired adds 1; cfd_persistent_status_stream reads and clears it (and
+// cfd_persistent_status every stream's of the device).  nullptr if allocation
+// failed (or, without create, if s never had one).
+int *persist_fail_word(hipStream_t s, bool create = true);
 // k_energy_mean_mb's scratch for the current device and stream s (a zeroed
 // counter word + kEnergyBlocks doubles, kept for the process's life); nullptr
 // if allocation failed
@@ -82,7 +84,9 @@ unsigned *energy_scratch(hipStream_t s);
 // Launch a persistent kernel: cooperatively when tuning().persist_coop (0 if
 // the runtime refuses the size: every tile could not be co-resident -- the
 // error is cleared and the caller takes its launch-per-pass path), else a
-// plain launch.  1 = launched; -1 = another launch error (set_error done).
+// plain launch; in either case ordered after this process's previous
+// persistent launch on the device (any stream).  1 = launched; -1 = another
+// launch error (set_error done).
 int launch_persistent(const void *f, int nblocks, int threads, void *args, hipStream_t s);
 // free the calling thread's persistent Jacobi rings (jacobi2d_persist.hip)
 void release_thread_rings();

@@ -34,8 +34,11 @@
 // an expired one leaves phi all NaN and counts a failure (cfd_persistent_status):
 // the last workgroup to finish (a ticket counter) checks and resets the status,
 // so a solve is this one launch with no prologue or epilogue kernel.
-// The launch is cooperative (launch_persistent): the runtime guarantees that
-// every tile is resident at once, or refuses and the launch-per-pass path runs.
+// The launch (launch_persistent) is a plain one after the occupancy check by
+// default (every tile fits on an otherwise idle chip), ordered after this
+// process's previous persistent launch on the device; cfd_set_persistent_launch
+// (1, ...) makes it cooperative, where the runtime guarantees that every tile
+// is resident at once or refuses and the launch-per-pass path runs.
 #include "internal.hpp"
 
 #include <atomic>
@@ -397,7 +400,7 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
         ep = 0;
     }
     a.epoch = ++ep;
-    a.fail = persist_fail_word();
+    a.fail = persist_fail_word(s);
     a.spin = persist_poll_ticks();
     const void *f = nullptr;
 #define CFD_KF(N_) f = mask ? (const void *)jacobi2d_persist<true, N_> : (const void *)jacobi2d_persist<false, N_>

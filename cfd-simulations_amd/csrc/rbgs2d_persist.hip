@@ -46,9 +46,11 @@
 // ring (8 blocks): block j's flags go out at block j + 1, after this tile
 // ruled out a stop in block j - 2, so every tile has published block j - 2's
 // flags, i.e. is in block j - 1 or later and reads flags of block j - 4 or
-// later.  The launch is cooperative (launch_persistent): the runtime
-// guarantees that every tile is resident at once, or refuses it and the
-// launch-per-block path runs.  Every poll is still bounded (20 s of the 100
+// later.  The launch (launch_persistent) is a plain one after the
+// occupancy check by default, ordered after this process's previous persistent
+// launch on the device; cfd_set_persistent_launch(1, ...) makes it cooperative
+// (the runtime guarantees that every tile is resident at once, or refuses it
+// and the launch-per-block path runs).  Every poll is still bounded (20 s of the 100
 // MHz clock from the kernel's start by default, cfd_set_persistent_launch):
 // an expired one ends the solve with phi all NaN, *iters_done = -1 and a
 // failure counted for cfd_persistent_status, instead of a hang.
@@ -583,7 +585,7 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     }
     const size_t n = (size_t)ny * nx;
     hipLaunchKernelGGL(rbgs_persist_finish, dim3(ceil_div((long)(n / 4 + 1), 256)), dim3(256), 0, s, ws, phi,
-                       phi_tmp, n, iters_done, persist_fail_word());
+                       phi_tmp, n, iters_done, persist_fail_word(s));
     const hipError_t e2 = hipGetLastError();
     if (e2 != hipSuccess) {
         *rc = CFD_E_HIP;

@@ -286,22 +286,32 @@ def predictor_fused(u, v, dx, dy, dt, nu_eff, use_supg=True, u_star=None, v_star
     tau_mode: "exact" (the reference's NumPy scalar `**`: glibc powf / pow,
     bit-exact), "fast" (the compiled reference's fastmath x*x / sqrt, within
     1e-6 relative L-inf), or None (the calling thread's current setting,
-    cfd_set_predictor2d_tau_mode; "exact" unless changed).  Without SUPG a
-    given tau is filled with zeros (the reference's never-assigned
-    np.zeros, v5.py:292)."""
+    cfd_set_predictor2d_tau_mode; "exact" unless changed).  A given mode
+    applies to this call only: the thread's setting is restored after it.
+    Without SUPG a given tau is filled with zeros (the reference's
+    never-assigned np.zeros, v5.py:292)."""
     ny, nx = _shape2d(u)
-    if tau_mode is not None:
-        if tau_mode not in TAU_MODES:
-            raise ValueError(f"tau_mode must be one of {sorted(TAU_MODES)}, not {tau_mode!r}")
-        call("cfd_set_predictor2d_tau_mode", TAU_MODES[tau_mode])
+    if tau_mode is not None and tau_mode not in TAU_MODES:
+        raise ValueError(f"tau_mode must be one of {sorted(TAU_MODES)}, not {tau_mode!r}")
     us = torch.empty_like(u) if u_star is None else u_star
     vs = torch.empty_like(v) if v_star is None else v_star
     if tau is None and use_supg:
         tau = torch.empty_like(u)
     nu_a, nu_s = _nu(nu_eff, u.dtype)
-    call(_fields("cfd_predictor2d", u, v, us, vs, tau), ptr(u), ptr(v), ptr(nu_a), nu_s, ptr(us), ptr(vs),
-         ptr(tau), ny, nx, float(dx), float(dy), _dt_arg(dt, u.dtype), int(bool(use_supg)),
-         stream_handle())
+    prev = None
+    if tau_mode is not None:
+        prev = int(lib().cfd_get_predictor2d_tau_mode())
+        if prev != TAU_MODES[tau_mode]:
+            call("cfd_set_predictor2d_tau_mode", TAU_MODES[tau_mode])
+        else:
+            prev = None
+    try:
+        call(_fields("cfd_predictor2d", u, v, us, vs, tau), ptr(u), ptr(v), ptr(nu_a), nu_s, ptr(us), ptr(vs),
+             ptr(tau), ny, nx, float(dx), float(dy), _dt_arg(dt, u.dtype), int(bool(use_supg)),
+             stream_handle())
+    finally:
+        if prev is not None:
+            call("cfd_set_predictor2d_tau_mode", prev)
     return us, vs, tau
 
 
@@ -315,13 +325,14 @@ def project_velocity(phi, u_star, v_star, dx, dy, dt, u=None, v=None, gradmax=No
     return u, v
 
 
-def persistent_failures() -> int:
-    """Synchronises the device and returns how many persistent small-grid
-    solves (the one-launch 2-D Jacobi / red-black GS) had a tile wait expire
-    since the last call; their phi is all NaN (cfd_persistent_status).  The
-    count is per device, not per caller: solvers sharing a device share it (a
-    failed solve's NaN phi still fails its own solver's non-finite check)."""
+def persistent_failures(stream=None) -> int:
+    """How many persistent small-grid solves (the one-launch 2-D Jacobi /
+    red-black GS) run on ``stream`` (default: the current stream) had a tile
+    wait expire since the last call; their phi is all NaN.  Reads and clears
+    that stream's failure word with an async copy and synchronises that
+    stream only (cfd_persistent_status_stream): solvers on other streams keep
+    running and keep their own counts."""
     import ctypes
     n = ctypes.c_int(0)
-    call("cfd_persistent_status", ctypes.byref(n))
+    call("cfd_persistent_status_stream", stream_handle(stream), ctypes.byref(n))
     return int(n.value)

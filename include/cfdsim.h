@@ -201,6 +201,8 @@ int cfd_set_predictor2d_config(int variant, int rows, int cells_per_lane);
  * The one-thread-per-cell kernel (variant 1, or arrays past 2^31 bytes)
  * always computes mode 0. */
 int cfd_set_predictor2d_tau_mode(int mode);
+/* The calling thread's current tau mode (0 exact / 1 fast). */
+int cfd_get_predictor2d_tau_mode(void);
 /* The calling thread's last predictor launch: returns 1 = row march, 0 = one
  * thread per cell, -1 = none yet; *tau_mode (0 exact / 1 fast) and
  * *cells_per_lane of that launch (either pointer may be NULL). */
@@ -488,29 +490,34 @@ int cfd_set_small2d_gs_persistent(int mode);
 int cfd_set_small2d_jacobi_persistent(int on, int sweeps_per_block);
 /* Both persistent small-grid solves (the GS above and the Jacobi below) are
  * plain launches after the library's own occupancy check by default
- * (cooperative = 0, r05: the check assumes the device is otherwise idle; a
- * tile queued behind other work only waits, one-way, up to the poll bound).
- * cooperative = 1: the HIP runtime guarantees that every tile is resident at
- * once or refuses the launch, and a refused launch takes the launch-per-pass
- * path (same bits); it costs ~30 us of queue gap per solve (v5 cylinder step
+ * (cooperative = 0, r05).  The check assumes no other persistent solve holds
+ * CUs, so the library orders a process's persistent launches on a device one
+ * after another (each waits on the device for the previous one, whatever its
+ * stream or host thread).  Processes sharing a device are not ordered: there,
+ * cooperative = 1 makes the HIP runtime guarantee that every tile is resident
+ * at once or refuse the launch (a refused launch takes the launch-per-pass
+ * path, same bits); it costs ~30 us of queue gap per solve (v5 cylinder step
  * 0.76 -> 0.79 ms).  poll_ticks bounds each wait of a tile for its
  * neighbours, in ticks of the 100 MHz device clock (0 = the default, 20 s; a
  * tiny value forces the failure path in tests).  A solve whose wait expired
- * leaves phi all NaN, the GS's *iters_done = -1, and counts one failure for
- * cfd_persistent_status. */
+ * leaves phi all NaN, the GS's *iters_done = -1, and counts one failure in the
+ * failure word of the stream it ran on. */
 int cfd_set_persistent_launch(int cooperative, long long poll_ticks);
-/* Synchronises the current device, then returns in *expired the number of
- * persistent solves on it whose neighbour wait expired since the last call
- * (and clears the count).  The Python solver checks it in
- * monitor_simulation_health (v5.py:599-613).  The count is one word per
- * device, shared by every caller on it: with several solvers on a device one
- * caller's read can take another's failure -- whose phi is all NaN, so that
- * solver's own non-finite check (v5.py:601) still fails the step. */
+/* The health check of one stream (the Python solver's
+ * monitor_simulation_health, v5.py:599-613): returns in *expired the number
+ * of persistent solves run on `stream` (the current device) whose neighbour
+ * wait expired since the last read, and clears that count.  An async copy on
+ * `stream` followed by a synchronisation of that stream only: other streams
+ * keep running, and other streams' failures stay for their own readers. */
+int cfd_persistent_status_stream(void *stream, int *expired);
+/* The device-wide form: synchronises the current device, then sums and clears
+ * the failure counts of every stream on it. */
 int cfd_persistent_status(int *expired);
-/* Frees the calling thread's library-owned device buffers: the persistent
+/* Frees the calling thread's library-owned device resources: the persistent
  * Jacobi's exchange rings (24 B per cell of the largest grid the thread
- * solved, one per device), after the solves that use them have finished.
- * Later solves on the thread allocate them again. */
+ * solved, one per device) and the timing events, after the work that uses them
+ * has finished.  Later calls on the thread allocate them again.  The library
+ * makes no HIP call at thread or process exit. */
 int cfd_release_thread_resources(void);
 /* Diagnostics: the persistent GS writes 4 timestamps (100 MHz device clock)
  * per tile and block into buf -- block start, halo received, tile ready,
@@ -560,7 +567,7 @@ int cfd_timing_read(double *ms, long long *sweeps, int reset);
 /* The same for one channel: 0 = the pressure solves (cfd_timing_read), 1 =
  * the predictor launches (cfd_predictor2d_f32 / _f64, one count per launch),
  * so a timed time_step reports the solve's sweeps without the predictor in
- * them.  reset clears both channels. */
+ * them.  reset clears the channel read (the other channel's timings stay). */
 int cfd_timing_read_channel(int channel, double *ms, long long *sweeps, int reset);
 
 #ifdef __cplusplus

@@ -454,13 +454,17 @@ def test_project_and_clean_divergence_bitexact(golden):
 @pytest.mark.parametrize("ny,nx", [(3, 3), (3, 50), (4, 7), (66, 30), (67, 30), (130, 17), (180, 600),
                                    (194, 33), (258, 70), (322, 51), (323, 20), (36, 1200),
                                    (514, 9), (515, 9), (1030, 40), (1027, 64), (2060, 66), (130, 131),
-                                   (70, 1023), (1100, 97), (300, 66), (130, 67)])
+                                   (70, 1023), (1100, 97), (300, 66), (130, 67),
+                                   (200, 50000), (66, 45000)])
 def test_clean_divergence_lexicographic_shapes(ny, nx):
     """The serial lexicographic phi sweep of clean_divergence_fast (v5.py:250-253)
     on ragged shapes: one and several waves per band, a band edge inside a wave,
     a single-row last band (row above and below both from memory), several bands;
     one and two iterations.  nx >= 64 takes the diagonal wavefront (bands of up
-    to 1024 rows, 16 waves): 1027 and 2060 rows end in a one- and a ten-row band."""
+    to 1024 rows, 16 waves): 1027 and 2060 rows end in a one- and a ten-row band.
+    Short, very wide grids (200 x 50000, 66 x 45000) run one wave per band,
+    whose launch needs no dynamic LDS (r05 advisor: it asked for more than a CU
+    holds and failed)."""
     rng = np.random.default_rng(ny * 1000 + nx)
     u0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)
     v0 = rng.uniform(-1, 1, (ny, nx)).astype(np.float32)

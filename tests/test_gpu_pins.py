@@ -544,6 +544,49 @@ def test_persistent_forced_expiry_fails_loudly():
     assert K.persistent_failures() == 0
 
 
+def test_health_check_is_per_stream():
+    """Two solvers on two streams (v5.py:599-613's health check per solver):
+    a neighbour-wait expiry forced in solver A's step (1-tick poll bound, on
+    stream A) is counted in stream A's failure word only.  Stream B's status
+    reads 0 and leaves A's count alone; A's then reads 1 and A's
+    monitor_simulation_health fails.  Reading B's status is an async copy on
+    B plus a wait for B: work queued on stream A is still running after it."""
+    from cfd_simulations_amd.solver import OptimizedTurbulentConfig, OptimizedTurbulentSolver, \
+        monitor_simulation_health
+    torch.cuda.synchronize()
+    assert K.persistent_failures() == 0
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    cfg = OptimizedTurbulentConfig(use_fast_pressure=False, pressure_iterations=64)
+    with torch.cuda.stream(sa):
+        a = OptimizedTurbulentSolver(cfg)
+    with torch.cuda.stream(sb):
+        b = OptimizedTurbulentSolver(cfg)
+    torch.cuda.synchronize()
+    call("cfd_set_persistent_launch", 1, 1)
+    try:
+        with torch.cuda.stream(sa):
+            a.time_step()
+    finally:
+        call("cfd_set_persistent_launch", 1, 0)
+    with torch.cuda.stream(sb):
+        b.time_step()
+    sa.synchronize()
+    assert K.persistent_failures(sb) == 0
+    assert K.persistent_failures(sa) == 1
+    assert K.persistent_failures(sa) == 0  # read and cleared
+    assert torch.isfinite(b.u).all() and torch.isfinite(b.phi).all()
+    # the failed step's phi is NaN: A's own health check fails on it
+    with torch.cuda.stream(sa):
+        assert monitor_simulation_health(a, 1) is False
+    # no device-wide synchronisation: stream A stays busy while B's status is read
+    with torch.cuda.stream(sa):
+        torch.cuda._sleep(400_000_000)
+    assert K.persistent_failures(sb) == 0
+    assert not sa.query(), "reading stream B's status waited for stream A"
+    sa.synchronize()
+    call("cfd_set_persistent_launch", 0, 0)
+
+
 # ------------------------------------------- zero-start solve, fused first pass
 def test_jacobi3d_1024_zero_start_bitexact(div1024):
     """cfd_jacobi3d_zero_f32 at the bench geometry: phi = zeros then 2..9 and
