@@ -176,8 +176,10 @@ def cpu_baseline(shape, iters_total_hint, gs=False):
 
 def cpu_baseline_all_cores(shape, gs=False):
     """The oracle's OpenMP C restatement (bit-identical to the serial one) on
-    every thread OpenMP is given here (OMP_NUM_THREADS; 16 on the GPU box's CPU
-    share): the all-core CPU comparison point for the 3-D workloads."""
+    every thread OpenMP is given here: OMP_NUM_THREADS, which the GPU box sets
+    to its CPU share of 16 (the host's logical CPUs -- 256 on the MI355X node --
+    are shared by the node's GPU slots; os.cpu_count() reports them all).  The
+    line states both numbers; `cores` is the threads actually used."""
     import oracle
     nz = min(shape[0], 256)
     sample = (nz, shape[1], shape[2])
@@ -194,9 +196,12 @@ def cpu_baseline_all_cores(shape, gs=False):
         what = "oracle_jacobi3d_f32_mt"
     t = time.perf_counter() - t0
     cells = (sample[0] - 2) * (sample[1] - 2) * (sample[2] - 2) * it
-    return {"value": cells / t / 1e9, "unit": "Gcell-updates/s", "cores": oracle.threads(), "kind": "port",
+    nthr = oracle.threads()
+    return {"value": cells / t / 1e9, "unit": "Gcell-updates/s", "cores": nthr, "kind": "port",
             "sample": f"{sample[0]}x{sample[1]}x{sample[2]} slab of the grid, {it} iterations, {what} (C, "
-                      f"OpenMP over planes); {t:.2f} s"}
+                      f"OpenMP over planes); {t:.2f} s; {nthr} threads = OMP_NUM_THREADS "
+                      f"({os.environ.get('OMP_NUM_THREADS', 'unset')}: this job's CPU share) of the host's "
+                      f"{os.cpu_count()} logical CPUs"}
 
 
 def cavity_bench():
@@ -416,6 +421,9 @@ def spawn_ranks(args, argv, run=None, device_count=None):
     return (run or subprocess.run)(cmd, env=env).returncode
 
 
+T_START = time.perf_counter()
+
+
 def main():
     global ARGS
     ARGS = parse()
@@ -457,6 +465,12 @@ def main():
         os.environ.setdefault("NCCL_MAX_P2P_NCHANNELS", "16")
         dist.init_process_group("nccl", device_id=dev)
 
+    def progress(what):
+        # N-rank runs: a line per phase on stderr (a long silent phase reads as a hang)
+        if use_slab:
+            print(f"bench.py rank {rank}/{world}: {what} ({time.perf_counter() - T_START:.1f} s)",
+                  file=sys.stderr, flush=True)
+
     shape, dt_name, iters_default, bpc = WORKLOADS[ARGS.workload]
     if ARGS.grid:
         grid = tuple(int(x) for x in ARGS.grid.split(","))
@@ -494,7 +508,9 @@ def main():
                 K.solve_pressure_gauss_seidel3d(phi, div, h, h, h, dt, None, iters, GS_TOL, workspace=gs_ws,
                                                 iters_done=gs_done, phi_tmp=tmp)
         else:
+            progress("attaching the slab transport")
             comm = make_comm(S, rank, world)
+            progress(f"transport up ({TRANSPORT}); allocating the {plan.nz_total}-plane slab")
             sj = S.SlabRBGS3D(plan, ny, nx, h, h, h, dt, comm, device=dev)
             sj.div.copy_(torch.randn(sj.div.shape, generator=g, device=dev, dtype=torch.float32))
             gs_done = sj.iters_done
@@ -529,9 +545,12 @@ def main():
                     # pass starts from the zeros and forms the RHS workspace
                     K.solve_pressure_jacobi3d_zero(phi, div, h, dt, iters, phi_tmp=tmp, rhs_ws=rhs)
         else:
+            progress("attaching the slab transport")
             comm = make_comm(S, rank, world)
+            progress(f"transport up ({TRANSPORT}); allocating the {plan.nz_total}-plane slab")
             sj = S.SlabJacobi3D(plan, ny, nx, h, dt, comm, device=dev, rhs_workspace=not ARGS.no_rhs_ws)
             sj.div.copy_(torch.randn(sj.div.shape, generator=g, device=dev, dtype=torch.float32))
+            progress("slab allocated and attached")
 
             def step():
                 sj.solve(iters, overlap=not ARGS.no_overlap)
@@ -563,13 +582,18 @@ def main():
 
     verified = None
     if use_slab and len(shape) == 3 and not ARGS.no_verify:
+        progress("verifying the slab solve against the one-GPU solve")
         verified = (verify_slabs_rbgs if gs else verify_slabs)(S, K, dist, comm, world, rank, dev)
+        progress(f"verification {'bit-exact' if verified else 'MISMATCH'}")
 
     if ARGS.sweep_tiles and world == 1 and len(shape) == 3 and not gs:
         tile_sweep(K, call, div, phi, tmp, h, dt, bpc, cells_rank, rhs)
 
-    for _ in range(ARGS.warmup):
+    for w in range(ARGS.warmup):
         step()
+        if use_slab:  # (untimed) one line per warm-up step of an N-rank run
+            torch.cuda.synchronize()
+            progress(f"warm-up step {w + 1}/{ARGS.warmup} done")
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -581,6 +605,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    progress("timed steps done")
     ms = ctypes.c_double()
     nsw = ctypes.c_longlong()
     call("cfd_timing_read", ctypes.byref(ms), ctypes.byref(nsw), 1)
@@ -668,6 +693,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if use_slab and len(shape) == 3:
+        if hasattr(comm, "status"):
+            comm.status()  # raises if a neighbour wait expired during the run
         comm.close()
     if use_slab:
         dist.destroy_process_group()

@@ -104,6 +104,7 @@ PROTOTYPES = {
     "cfd_comm_init_ipc": (c_int, [c_int, c_int, ctypes.POINTER(c_void_p)]),
     "cfd_comm_ipc_blob_bytes": (c_size_t, []),
     "cfd_comm_ipc_export": (c_int, [P, P, P, c_size_t, P]),
+    "cfd_comm_ipc_export_ghost": (c_int, [P, P, P, c_size_t, c_size_t, P]),
     "cfd_comm_ipc_import": (c_int, [P, P, c_int]),
     "cfd_comm_status": (c_int, [P, ctypes.POINTER(c_int)]),
     "cfd_slab_jacobi3d_f32": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -116,6 +116,19 @@ constexpr int kCeGatherWord = 256;       // gather ring (u64 granules) at byte 1
 constexpr size_t kCeFlagBytes = 4 * (size_t)kCeGatherWord + 8 * (size_t)kCeRing * kCeMaxRanks;
 constexpr uint32_t kCeMagic = 0x43464445u;  // "CFDE"
 
+// Landing buffers (r06).  hipIpcOpenMemHandle of an allocation past 2 GiB
+// never returns on this stack (r06 probe, scripts/ipc_size_probe.py: 2046 MiB
+// maps, 2050 MiB hangs the importing process) -- the 1024^3 grid at two ranks
+// holds 2.2 GB arrays.  A rank whose pair is that large (or any rank with
+// CFD_CE_LANDING=1) exports instead a small landing buffer of 2 slots x 2
+// sides x G planes: its neighbours' copies land there, and after the sync
+// kernel its compute stream copies the slot into the ghost planes.  Slots
+// alternate with the exchange count of each direction (the sender's count
+// and the receiver's are equal), so the neighbours' exchange k + 2, which
+// needs this rank's exchange k + 1 -- sent after this rank's landing copy k
+// on the compute stream -- never overwrites a slot still being copied.
+constexpr size_t kIpcMapMax = (size_t)2 << 30;  // allocations at or past this are not mapped
+
 // What a rank exports for its peers (host bytes, cfd_comm_ipc_blob_bytes)
 struct CeBlob {
     uint32_t magic, version;
@@ -124,6 +137,8 @@ struct CeBlob {
     uint64_t buf_off[2];         // byte offset of the array in its allocation
     uint64_t buf_n[2];           // elements of each array
     hipIpcMemHandle_t flags_h;   // the flag block
+    hipIpcMemHandle_t land_h;    // the landing buffer (land_n > 0)
+    uint64_t land_n;             // elements per (slot, side) of the landing buffer; 0: none
 };
 
 struct CeState {
@@ -146,11 +161,21 @@ struct CeState {
         float *mine[2];
         size_t n;
         std::vector<CeBlob> blobs;  // every rank's export of this pair
+        float *land = nullptr;      // this rank's landing buffer (land_n > 0)
+        size_t land_n = 0;
     };
     std::vector<Attachment> att;
     int cur = -1;                   // the attachment of the solve in progress
     float *pend[2] = {nullptr, nullptr};  // exported, not yet imported
     size_t pend_n = 0;
+    float *pend_land = nullptr;
+    size_t pend_land_n = 0;
+    std::vector<float *> lands;     // every landing buffer allocated (freed with the comm)
+    // the exchange of the pass in flight (exchange_ce -> ce_sync): the array,
+    // its owned planes, ghost depth and plane size
+    float *x_a = nullptr;
+    int x_nzl = 0, x_G = 0;
+    size_t x_plane = 0;
     unsigned sent[2] = {0, 0}, recvd[2] = {0, 0}, gathered = 0;
     // solves begun per direction: every rank begins the same solves, so the
     // neighbour's ready word reaches this count when it has begun this one
@@ -483,6 +508,13 @@ static int ce_peer_buf(SlabComm *c, int peer, int bi, float **buf, size_t *n) {
     }
     const CeBlob &b = at.blobs[peer];
     char *base = nullptr;
+    if (b.land_n) {  // the peer takes its ghosts through its landing buffer
+        int rc = ce_map(ce, peer, b.land_h, &base);
+        if (rc) return rc;
+        *buf = reinterpret_cast<float *>(base);
+        *n = 4 * (size_t)b.land_n;
+        return CFD_OK;
+    }
     int rc = ce_map(ce, peer, b.buf_h[bi], &base);
     if (rc) return rc;
     *buf = reinterpret_cast<float *>(base + b.buf_off[bi]);
@@ -508,11 +540,21 @@ static int exchange_ce(SlabComm *c, const float *a, int nzl, int G, size_t plane
         size_t pn = 0;
         int rc = ce_peer_buf(c, peer, bi, &dst, &pn);
         if (rc) return rc;
-        CFD_REQUIRE(pn >= 2 * n, "slab (copy engines): rank %d's buffer is smaller than its ghosts", peer);
         // to lo: our first owned planes -> its last (hi) ghost planes, its
         // from-hi word; to hi: our last owned planes -> its first ghost planes
         const float *src = d == 0 ? a + n : a + (size_t)nzl * plane;
-        if (d == 0) dst += pn - n;
+        const size_t land_n = at.blobs[peer].land_n;
+        if (land_n) {
+            // its landing buffer: slot (this exchange's count) & 1, side hi (d
+            // = 0: our planes are its hi ghosts) or lo
+            CFD_REQUIRE(land_n >= n, "slab (copy engines): rank %d's landing buffer is smaller than its ghosts",
+                        peer);
+            const unsigned k = ce.sent[d] + 1;
+            dst += ((size_t)(k & 1u) * 2 + (d == 0 ? 1 : 0)) * land_n;
+        } else {
+            CFD_REQUIRE(pn >= 2 * n, "slab (copy engines): rank %d's buffer is smaller than its ghosts", peer);
+            if (d == 0) dst += pn - n;
+        }
         unsigned *word = ce.peer_flags[peer] + (d == 0 ? kCeFromHi : kCeFromLo);
         CFD_CHECK_HIP(hipStreamWaitEvent(ce.xs[d], ready, 0));
         if (ce.need_ready[d]) {  // the neighbour has begun this solve (ce_begin)
@@ -526,6 +568,10 @@ static int exchange_ce(SlabComm *c, const float *a, int nzl, int G, size_t plane
         CFD_CHECK_HIP(hipStreamWriteValue32(ce.xs[d], word, ++ce.sent[d], 0));
         ce.used[d] = true;
     }
+    ce.x_a = const_cast<float *>(a);
+    ce.x_nzl = nzl;
+    ce.x_G = G;
+    ce.x_plane = plane;
     return CFD_OK;
 }
 
@@ -549,6 +595,20 @@ static int ce_sync(SlabComm *c, hipStream_t s, int lo, int hi, float *maxc, int 
     if (!a.want_lo && !a.want_hi && !a.cnt) return CFD_OK;
     hipLaunchKernelGGL(k_ce_sync, dim3(1), dim3(64), 0, s, a);
     CFD_LAUNCH_CHECK();
+    const CeState::Attachment &at = ce.att[ce.cur];
+    if (at.land_n && ce.x_a) {
+        // the neighbours' planes landed in this rank's landing slots: into the
+        // ghost planes of the exchanged array, behind the sync on s
+        const size_t n = (size_t)ce.x_G * ce.x_plane;
+        CFD_REQUIRE(at.land_n >= n, "slab (copy engines): landing buffer smaller than the ghosts");
+        if (a.want_lo)
+            CFD_CHECK_HIP(hipMemcpyAsync(ce.x_a, at.land + (size_t)(a.want_lo & 1u) * 2 * at.land_n,
+                                         n * sizeof(float), hipMemcpyDeviceToDevice, s));
+        if (a.want_hi)
+            CFD_CHECK_HIP(hipMemcpyAsync(ce.x_a + (size_t)(ce.x_nzl + ce.x_G) * ce.x_plane,
+                                         at.land + ((size_t)(a.want_hi & 1u) * 2 + 1) * at.land_n,
+                                         n * sizeof(float), hipMemcpyDeviceToDevice, s));
+    }
     return CFD_OK;
 }
 
@@ -682,31 +742,58 @@ int cfd_comm_init_ipc(int nranks, int rank, void **comm) {
 size_t cfd_comm_ipc_blob_bytes(void) { return sizeof(CeBlob); }
 
 int cfd_comm_ipc_export(void *comm, const float *phi, const float *phi_tmp, size_t n, void *blob) {
+    return cfd_comm_ipc_export_ghost(comm, phi, phi_tmp, n, 0, blob);
+}
+
+int cfd_comm_ipc_export_ghost(void *comm, const float *phi, const float *phi_tmp, size_t n, size_t ghost_elems,
+                              void *blob) {
     SlabComm *c = reinterpret_cast<SlabComm *>(comm);
     CFD_REQUIRE(c && c->ce && phi && phi_tmp && phi != phi_tmp && n > 0 && blob,
                 "comm_ipc_export: needs a copy-engine comm, two distinct buffers and a blob");
+    CFD_REQUIRE(2 * ghost_elems <= n, "comm_ipc_export: %zu ghost elements per side of a %zu-element array",
+                ghost_elems, n);
     CeState &ce = *c->ce;
     CeBlob b;
     memset(&b, 0, sizeof b);
     b.magic = kCeMagic;
-    b.version = 1;
+    b.version = 2;
     b.rank = c->rank;
     b.nranks = c->nranks;
     const float *bufs[2] = {phi, phi_tmp};
+    static const bool force_landing = [] {  // CFD_CE_LANDING=1: landing buffers at any size (tests)
+        const char *e = getenv("CFD_CE_LANDING");
+        return e && atoi(e) == 1;
+    }();
+    bool big = false;
     for (int i = 0; i < 2; ++i) {
         hipDeviceptr_t base = nullptr;
         size_t size = 0;
         CFD_CHECK_HIP(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)bufs[i]));
         const size_t off = (size_t)((const char *)bufs[i] - (const char *)base);
         CFD_REQUIRE(off + n * sizeof(float) <= size, "comm_ipc_export: buffer %d overruns its allocation", i);
+        big |= size >= kIpcMapMax;
         CFD_CHECK_HIP(hipIpcGetMemHandle(&b.buf_h[i], (void *)base));
         b.buf_off[i] = off;
         b.buf_n[i] = n;
+    }
+    CFD_REQUIRE(!big || ghost_elems > 0, "comm_ipc_export: an allocation of 2 GiB or more cannot be mapped by "
+                "the peers (hipIpcOpenMemHandle hangs past 2 GiB); export it with its ghost size "
+                "(cfd_comm_ipc_export_ghost) so that its ghosts arrive through a landing buffer");
+    float *land = nullptr;
+    const size_t land_n = (big || force_landing) ? ghost_elems : 0;
+    if (land_n) {
+        CFD_CHECK_HIP(hipMalloc((void **)&land, 4 * land_n * sizeof(float)));
+        CFD_CHECK_HIP(hipMemset(land, 0, 4 * land_n * sizeof(float)));
+        ce.lands.push_back(land);
+        CFD_CHECK_HIP(hipIpcGetMemHandle(&b.land_h, land));
+        b.land_n = land_n;
     }
     CFD_CHECK_HIP(hipIpcGetMemHandle(&b.flags_h, ce.flags));
     ce.pend[0] = const_cast<float *>(phi);
     ce.pend[1] = const_cast<float *>(phi_tmp);
     ce.pend_n = n;
+    ce.pend_land = land;
+    ce.pend_land_n = land_n;
     memcpy(blob, &b, sizeof b);
     return CFD_OK;
 }
@@ -720,7 +807,7 @@ int cfd_comm_ipc_import(void *comm, const void *blobs, int nblobs) {
     std::vector<CeBlob> in((size_t)nblobs);
     memcpy(in.data(), blobs, sizeof(CeBlob) * (size_t)nblobs);
     for (int r = 0; r < nblobs; ++r)
-        CFD_REQUIRE(in[r].magic == kCeMagic && in[r].version == 1 && in[r].rank == r &&
+        CFD_REQUIRE(in[r].magic == kCeMagic && in[r].version == 2 && in[r].rank == r &&
                         in[r].nranks == c->nranks,
                     "comm_ipc_import: blob %d is not rank %d's export of a %d-rank comm", r, r, c->nranks);
     // every rank's flag block, mapped once (it lives as long as the comm)
@@ -740,7 +827,7 @@ int cfd_comm_ipc_import(void *comm, const void *blobs, int nblobs) {
                                 hipMemcpyHostToDevice));
     }
     // a re-attached pair replaces its entry (its peers' buffers may be new)
-    CeState::Attachment at{{ce.pend[0], ce.pend[1]}, ce.pend_n, std::move(in)};
+    CeState::Attachment at{{ce.pend[0], ce.pend[1]}, ce.pend_n, std::move(in), ce.pend_land, ce.pend_land_n};
     int k = 0;
     while (k < (int)ce.att.size() && !(ce.att[k].mine[0] == at.mine[0] && ce.att[k].mine[1] == at.mine[1])) ++k;
     if (k == (int)ce.att.size())
@@ -748,6 +835,8 @@ int cfd_comm_ipc_import(void *comm, const void *blobs, int nblobs) {
     else
         ce.att[k] = std::move(at);
     ce.pend[0] = ce.pend[1] = nullptr;
+    ce.pend_land = nullptr;
+    ce.pend_land_n = 0;
     // the z-neighbours' buffers are mapped now (others on first use)
     ce.cur = k;
     for (int r : {c->rank - 1, c->rank + 1}) {
@@ -787,6 +876,7 @@ int cfd_comm_destroy(void *comm) {
             if (ce.xs[d]) (void)hipStreamDestroy(ce.xs[d]);
             if (ce.xev[d]) (void)hipEventDestroy(ce.xev[d]);
         }
+        for (float *p : ce.lands) (void)hipFree(p);
         if (ce.flags) (void)hipFree(ce.flags);
         if (ce.peers_dev) (void)hipFree(ce.peers_dev);
         if (ce.status) (void)hipFree(ce.status);

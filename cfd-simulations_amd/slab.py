@@ -185,11 +185,14 @@ class CopyEngineComm:
         self.handle = handle
         self.rank, self.nranks, self.group = rank, nranks, group
 
-    def attach(self, phi: torch.Tensor, phi_tmp: torch.Tensor):
+    def attach(self, phi: torch.Tensor, phi_tmp: torch.Tensor, ghost_elems: int = 0):
         """Export this rank's two field buffers, gather every rank's blob (a
         collective over the process group), map the neighbours' buffers.  A
         comm holds every pair attached so far (a re-attached pair replaces its
-        entry); a solve uses the pair its phi / phi_tmp belong to."""
+        entry); a solve uses the pair its phi / phi_tmp belong to.
+        ghost_elems = ghost planes per side x ny x nx: a pair of 2 GiB or more
+        then takes its ghosts through a landing buffer (its allocation cannot
+        be IPC-mapped, cfd_comm_ipc_export_ghost)."""
         import ctypes
         if phi.shape != phi_tmp.shape or phi.dtype != torch.float32 or not phi.is_cuda:
             raise ValueError("attach: two float32 device arrays of one shape")
@@ -197,7 +200,7 @@ class CopyEngineComm:
         blob = (ctypes.c_char * nb)()
         err = None
         try:
-            call("cfd_comm_ipc_export", self.handle, ptr(phi), ptr(phi_tmp), phi.numel(),
+            call("cfd_comm_ipc_export_ghost", self.handle, ptr(phi), ptr(phi_tmp), phi.numel(), int(ghost_elems),
                  ctypes.addressof(blob))
         except Exception as e:  # noqa: BLE001 -- every rank learns of it below
             err = e
@@ -305,7 +308,7 @@ class SlabJacobi3D:
         self.mask = None if mask is None else mask.to(torch.uint8).contiguous()
         self.comm = comm
         if hasattr(comm, "attach"):
-            comm.attach(self.phi, self.tmp)
+            comm.attach(self.phi, self.tmp, plan.ghost * ny * nx)
         # high priority: its own HW queue (ROCclr pools queues per priority), so
         # the exchange is dispatched beside the interior launch, not behind it
         self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1)
@@ -352,7 +355,7 @@ class SlabRBGS3D:
         self.ws = None
         self.comm = comm
         if hasattr(comm, "attach"):
-            comm.attach(self.phi, self.tmp)
+            comm.attach(self.phi, self.tmp, plan.ghost * ny * nx)
         # high priority: its own HW queue (ROCclr pools queues per priority), so
         # the exchange is dispatched beside the interior launch, not behind it
         self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1)

@@ -370,6 +370,15 @@ int cfd_comm_init(const void *unique_id, int nranks, int rank, void **comm);
 int cfd_comm_init_ipc(int nranks, int rank, void **comm);
 size_t cfd_comm_ipc_blob_bytes(void);
 int cfd_comm_ipc_export(void *comm, const float *phi, const float *phi_tmp, size_t n, void *blob);
+/* The same with the pair's ghost size: ghost_elems = ghost planes per side x
+ * ny x nx.  A pair whose allocation is 2 GiB or more is never mapped by the
+ * peers (hipIpcOpenMemHandle does not return past 2 GiB here, r06): its rank
+ * exports a landing buffer of 4 x ghost_elems floats instead, the neighbours'
+ * copies land there and the rank's compute stream copies them into the ghost
+ * planes after each sync (same bits; CFD_CE_LANDING=1 forces it at any size).
+ * cfd_comm_ipc_export (ghost_elems = 0) refuses such a pair. */
+int cfd_comm_ipc_export_ghost(void *comm, const float *phi, const float *phi_tmp, size_t n,
+                              size_t ghost_elems, void *blob);
 int cfd_comm_ipc_import(void *comm, const void *blobs, int nblobs);
 int cfd_comm_status(void *comm, int *timeouts);
 int cfd_comm_destroy(void *comm);

@@ -43,6 +43,17 @@ def test_bench_two_ranks_shared_gpu_jacobi():
 
 
 @pytest.mark.timeout(480)
+def test_bench_two_ranks_shared_gpu_jacobi_1024():
+    """The default workload at two ranks: 2.2 GB slab arrays, past what
+    hipIpcOpenMemHandle maps (2 GiB; it never returned, r06), so the ghosts
+    arrive through the ranks' landing buffers."""
+    d, out = _run(["--steps", "2", "--warmup", "1"])
+    assert d["n_gpus"] == 2 and d["config"]["grid"] == [1024, 1024, 1024]
+    assert d["config"]["halo"].startswith("copy engines"), d["config"]
+    assert d["config"]["multi_gpu_parity"].startswith("bit-exact"), (d["config"], out[-3000:])
+
+
+@pytest.mark.timeout(480)
 def test_bench_two_ranks_shared_gpu_rbgs():
     d, out = _run(["--workload", "rbgs3d_1024", "--grid", "128,128,128", "--steps", "2", "--warmup", "1"])
     assert d["n_gpus"] == 2

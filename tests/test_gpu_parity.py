@@ -789,22 +789,28 @@ def test_slab_copy_engine_single_rank(overlap, ghost):
         comm.close()
 
 
+@pytest.mark.parametrize("landing", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-def test_slab_copy_engine_multiprocess(world):
+def test_slab_copy_engine_multiprocess(world, landing):
     """The copy-engine transport between real processes: `world` ranks, each
     its own process on this GPU (torch.distributed.run, gloo for the IPC
     handle blobs), mapping each other's buffers and flag blocks.  Jacobi
     (ghost 1 and 3, zero and nonzero start, overlap on / off) and red-black GS
     (one and two iterations per pass, fixed count and early stop through the
     gathered global maxima): the gathered owned planes equal the single-domain
-    oracle bit for bit (scripts/multirank_check.py)."""
+    oracle bit for bit (scripts/multirank_check.py).  landing: every rank takes
+    its ghosts through its landing buffer (CFD_CE_LANDING=1, the path of pairs
+    of 2 GiB or more, which IPC cannot map: the 1024^3 grid at two ranks)."""
+    import os
     import subprocess
     import sys
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(29600 + world), str(ROOT / "scripts" /
-                                                                                "multirank_check.py"),
-           "--share-gpu", "--transport", "ce", "--quick", "--size", "48"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT))
+           "--master-addr", "127.0.0.1", "--master-port", str(29600 + world + 10 * landing),
+           str(ROOT / "scripts" / "multirank_check.py"), "--share-gpu", "--transport", "ce", "--quick", "--size", "48"]
+    env = dict(os.environ)
+    if landing:
+        env["CFD_CE_LANDING"] = "1"
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(ROOT), env=env)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "MULTIRANK OK" in out, out[-4000:]
 
