@@ -325,8 +325,21 @@ __device__ inline v2f_t lds2s(const float *row, int lane, int h) {
 // pair of -div * dt_inv (formed once per row as it enters the queue, the
 // product level4 forms per update); level4's operation order and edge rule,
 // so the same bits.
+// The GS stencil constants as packed pairs held in VGPRs (GsPk): as scalar
+// operands of the packed ops they were four SGPR pairs live across the whole
+// march, which pushed the lane masks out to VGPR lanes (r05: 59 in-loop
+// v_readlane / v_writelane); the row waves have VGPRs to spare (154 of 168).
+struct GsPk {
+    v2f_t cx, cy, cz, cd, ndt;  // ndt = -dt_inv: the rhs pair -div * dt_inv as div * ndt (same bits)
+};
+__device__ inline GsPk gs_pk(const TbrArgs &a) {
+    GsPk k{v2f_t{a.cx, a.cx}, v2f_t{a.cy, a.cy}, v2f_t{a.cz, a.cz}, v2f_t{a.cd, a.cd},
+           v2f_t{-a.dt_inv, -a.dt_inv}};
+    asm volatile("" : "+v"(k.cx), "+v"(k.cy), "+v"(k.cz), "+v"(k.cd), "+v"(k.ndt));
+    return k;
+}
 __device__ inline v2f_t level2(v2f_t C, v2f_t O, float wl, float er, v2f_t N, v2f_t S, v2f_t U, v2f_t D,
-                               v2f_t rhs, int h, int x, int nx, bool upd, const TbrArgs &a, bool own,
+                               v2f_t rhs, int h, int x, int nx, bool upd, const GsPk &a, bool own,
                                float &chg) {
     if (!upd) return C;
     const v2f_t E = h ? v2f_t{O.y, er} : v2f_t{O.x, O.y};
@@ -752,6 +765,13 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                 for (int m = T0S ? 1 : 0; m < l; ++m) t += (NR - 2 * m) * RS;
                 return t;
             };
+            [[maybe_unused]] const GsPk gk = MODE == kRbgs ? gs_pk(a) : GsPk{};
+            const uint32_t lds_st_p0 = lds_addr(st_p0), lds_st_p1 = lds_addr(st_p1);
+            const uint32_t lds_st_r0 = lds_addr(st_r0), lds_st_r1 = lds_addr(st_r1);
+            (void)lds_st_p0;
+            (void)lds_st_p1;
+            (void)lds_st_r0;
+            (void)lds_st_r1;
             const uint32_t lbA0 = lds_addr(smem) + 4u * (uint32_t)(wv * RS + 4 + 4 * lane);
             const uint32_t lbU0 = lds_addr(smem) + 4u * (uint32_t)(wv * RS);
             const uint32_t lbP00 = lds_addr(st_p0) + 4u * (uint32_t)(wv * 256 + 4 * lane);
@@ -1010,8 +1030,8 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     if constexpr (RDMA && MODE == kRbgs) {
                         // -div * dt_inv on the pairs (each element the scalar form)
                         P4 d = ldsp(rdr + (rr[j] - 1) * 256 + 4 * lane);
-                        d.e = -d.e * a.dt_inv;
-                        d.o = -d.o * a.dt_inv;
+                        d.e = d.e * gk.ndt;  // (-x) * y == -(x * y): the same bits as -div * dt_inv
+                        d.o = d.o * gk.ndt;
                         Rq[j][RS0] = d;
                     } else if constexpr (RDMA) {
                         Rq[j][RS0] = toV(torhs(lds4(rdr + (rr[j] - 1) * 256 + 4 * lane)));
@@ -1038,10 +1058,16 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     const v4i32 rp = SD ? rsrc4(sd_in, z + 3 >= 0 && z + 3 <= nz - 1) : plane_rsrc4(a.in, z + 3, nz, plane);
                     const v4i32 rd = SD ? rsrc4(sd_div, z + 2 >= 0 && z + 2 <= nz - 1) : plane_rsrc4(a.div, z + 2, nz, plane);
+                    // destinations as 32-bit LDS addresses (the staging rows'
+                    // generic pointers, hoisted out of the march, were 64-bit
+                    // SGPR pairs with a null-check select each: r05's in-loop
+                    // SGPR spills to VGPR lanes)
+                    const uint32_t lpr = E ? lds_st_p0 : lds_st_p1, lrr = E ? lds_st_r0 : lds_st_r1;
 #pragma unroll
                     for (int j = 0; j < RPW; ++j) {
-                        if (!ZERO) dma_row(rp, bo[j], const_cast<float *>(pr) + (rr[j] - 1) * 256);
-                        if constexpr (RDMA) dma_row(rd, bo[j], const_cast<float *>(rdr) + (rr[j] - 1) * 256);
+                        const uint32_t ro_ = 1024u * (uint32_t)(rr[j] - 1);
+                        if (!ZERO) dma_row_at(rp, bo[j], lpr + ro_);
+                        if constexpr (RDMA) dma_row_at(rd, bo[j], lrr + ro_);
                     }
                 }
                 // phase R: level l of plane p = z - l + 1, one (level, row)
@@ -1127,14 +1153,16 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             const v2f_t Up = l == 1 ? pick2(V[j][vs(1)], h) : Q[j][l - 1][qs(l - 1, 2)];
                             const v2f_t Dp = l == 1 ? pick2(V[j][vs(-1)], h) : Q[j][l - 1][qs(l - 1, 0)];
                             const LdsIn in = fetch(l, j);
-                            float wl = dpp_from_lower(Op.y), er = dpp_from_upper(Op.x);
-                            if (lane == 0) wl = in.wl;
-                            if (lane == 63) er = in.er;
+                            // lanes 0 / 63 take the x-halo cells as the DPP
+                            // shifts' `old` operand: no lane-mask select (the
+                            // two lane masks were SGPR pairs held across the
+                            // march)
+                            const float wl = dpp_from_lower_old(in.wl, Op.y), er = dpp_from_upper_old(in.er, Op.x);
                             // every lane computes (one beyond nx reads zeros and is
                             // never stored: its LDS writes and HBM store are masked)
                             const v2f_t v = level2(Cp, Op, wl, er, in.N, in.S, Up, Dp,
                                                    pick2(Rq[j][ROTR ? slk(R - l + 1, K) : l - 1], h), h, x, nx,
-                                                   irow[j] && !fx, a, orow[j] && p >= z0 && p < z1, chgl[slot(l)]);
+                                                   irow[j] && !fx, gk, orow[j] && p >= z0 && p < z1, chgl[slot(l)]);
                             if (l < K) {
                                 if constexpr (ROT) {
                                     Q[j][l][sl3(R - l + 1)] = v;
@@ -1163,10 +1191,9 @@ __global__ __launch_bounds__((NWR + 1) * 64) void jacobi3d_tbr(TbrArgs a) {
                             const float4 U = f4_of(l == 1 ? V[j][vs(1)] : Q[j][l - 1][qs(l - 1, 2)]);
                             const float4 D = f4_of(l == 1 ? V[j][vs(-1)] : Q[j][l - 1][qs(l - 1, 0)]);
                             const LdsIn in = fetch(l, j);
-                            float wl = dpp_from_lower(c.w);
-                            float er = dpp_from_upper(c.x);
-                            if (lane == 0) wl = in.wl;
-                            if (lane == 63) er = in.er;
+                            // (lanes 0 / 63: the x-halo cells, as the GS branch)
+                            const float wl = dpp_from_lower_old(in.wl, c.w);
+                            const float er = dpp_from_upper_old(in.er, c.x);
                             float lm = 0.f;
                             // every lane (see the GS branch)
                             const float4 v = level4<MODE, PREL, K == 4>(c, wl, er, in.N, in.S, U, D,
