@@ -454,6 +454,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) voi
                     tq[c] = M::tau_tol(vm, b2, rb2, dt, a.k);
                 }
             }
+            if constexpr (SUPG && VEC == 2 && sizeof(T) == 4) {
+                // the lane's two cells as packed pairs (v_pk_add / v_pk_mul
+                // on the Cells' register pairs): each element is the scalar
+                // code's operation, in its order (conv_supg_sel, laplacian,
+                // the u* / v* update below), so the bits are the same; the
+                // selects stay per element
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                const f2 U = {uc[0], uc[1]}, V = {vc[0], vc[1]};
+                const f2 UE = {uE[0], uE[1]}, UW = {uW[0], uW[1]}, VE = {vE[0], vE[1]}, VW = {vW[0], vW[1]};
+                const f2 UN = {Up.x[0], Up.x[1]}, US = {Um.x[0], Um.x[1]};
+                const f2 VN = {Vp.x[0], Vp.x[1]}, VS = {Vm.x[0], Vm.x[1]};
+                const f2 two = {2.0f, 2.0f};
+                // the second differences, shared by SUPG and the Laplacian
+                const f2 ux2 = (UE - two * U) + UW, uy2 = (UN - two * U) + US;
+                const f2 vx2 = (VE - two * V) + VW, vy2 = (VN - two * V) + VS;
+                const f2 t = {tq[0], tq[1]};
+                const f2 csu = U * ((UE - UW) * a.k.c1x) + V * ((UN - US) * a.k.c1y);
+                const f2 csv = U * ((VE - VW) * a.k.c1x) + V * ((VN - VS) * a.k.c1y);
+                f2 cdu = csu - t * (U * (ux2 * a.k.c2x) + V * (uy2 * a.k.c2y));
+                f2 cdv = csv - t * (U * (vx2 * a.k.c2x) + V * (vy2 * a.k.c2y));
+                asm volatile("" : "+v"(cdu), "+v"(cdv));  // formed unconditionally (conv_supg_sel)
+                const f2 NU = NUA ? f2{NUc.x[0], NUc.x[1]} : f2{a.nu_s, a.nu_s};
+                const f2 lu = NU * (ux2 * a.k.lx + uy2 * a.k.ly);
+                const f2 lv = NU * (vx2 * a.k.lx + vy2 * a.k.ly);
+                const bool in0 = x0 >= 1 && x0 <= nx - 2, in1 = x0 + 1 >= 1 && x0 + 1 <= nx - 2;
+                // a face cell: conv = lap = tau = 0 (np.zeros_like rings)
+                const f2 cu = {in0 && t.x > 0.0f ? cdu.x : (in0 ? csu.x : 0.0f),
+                               in1 && t.y > 0.0f ? cdu.y : (in1 ? csu.y : 0.0f)};
+                const f2 cv = {in0 && t.x > 0.0f ? cdv.x : (in0 ? csv.x : 0.0f),
+                               in1 && t.y > 0.0f ? cdv.y : (in1 ? csv.y : 0.0f)};
+                const f2 lu0 = {in0 ? lu.x : 0.0f, in1 ? lu.y : 0.0f}, lv0 = {in0 ? lv.x : 0.0f, in1 ? lv.y : 0.0f};
+                const f2 dt2 = {dt, dt};
+                const f2 uo2 = U + dt2 * (-cu + lu0), vo2 = V + dt2 * (-cv + lv0);
+                uo.x[0] = uo2.x;
+                uo.x[1] = uo2.y;
+                vo.x[0] = vo2.x;
+                vo.x[1] = vo2.y;
+                to.x[0] = in0 ? t.x : 0.0f;
+                to.x[1] = in1 ? t.y : 0.0f;
+            } else {
 #pragma unroll
             for (int c = 0; c < VEC; ++c) {
                 const T nu = NUA ? NUc.x[c] : a.nu_s;
@@ -473,6 +513,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) voi
                 uo.x[c] = uc[c] + dt * (-(in ? cu : T(0)) + (in ? lu : T(0)));
                 vo.x[c] = vc[c] + dt * (-(in ? cv : T(0)) + (in ? lv : T(0)));
                 to.x[c] = in ? t : T(0);
+            }
             }
         } else {
 #pragma unroll
