@@ -71,7 +71,8 @@ static Tuning process_defaults() {
         t.gs_persist = env_int("CFD_GS_PERSIST", t.gs_persist) != 0;
         t.j2_persist = env_int("CFD_J2_PERSIST", t.j2_persist) != 0;
         const int jn = env_int("CFD_J2P_NI", t.j2p_ni);
-        t.j2p_ni = jn == 4 || jn == 6 || jn == 8 ? jn : t.j2p_ni;
+        t.j2p_ni = jn == 4 || jn == 6 || jn == 8 || jn == 10 ? jn : t.j2p_ni;
+        t.j2p_pairs = env_int("CFD_J2P_PAIRS", t.j2p_pairs) != 0;
         t.gs_pairs = env_int("CFD_GS_PAIRS", t.gs_pairs) != 0;
         const int pv = env_int("CFD_PRED_VARIANT", t.pred_variant);
         t.pred_variant = pv >= 0 && pv <= 2 ? pv : t.pred_variant;
@@ -360,11 +361,14 @@ int cfd_set_small2d_gs_persistent(int mode) {
 }
 
 int cfd_set_small2d_jacobi_persistent(int on, int sweeps_per_block) {
-    CFD_REQUIRE(on >= 0 && on <= 2, "small-grid Jacobi persistent: on must be 0 (default), 1 (off) or 2 (on)");
-    CFD_REQUIRE(sweeps_per_block == 0 || sweeps_per_block == 4 || sweeps_per_block == 6 || sweeps_per_block == 8,
-                "small-grid Jacobi persistent: sweeps per block must be 0 (default), 4, 6 or 8");
+    CFD_REQUIRE(on >= 0 && on <= 3,
+                "small-grid Jacobi persistent: on must be 0 (default), 1 (off), 2 (on) or 3 (on, one exchange per sweep)");
+    CFD_REQUIRE(sweeps_per_block == 0 || sweeps_per_block == 4 || sweeps_per_block == 6 || sweeps_per_block == 8 ||
+                    sweeps_per_block == 10,
+                "small-grid Jacobi persistent: sweeps per block must be 0 (default), 4, 6, 8 or 10");
     const Tuning d = process_defaults();
-    tuning().j2_persist = on ? on == 2 : d.j2_persist;
+    tuning().j2_persist = on ? on >= 2 : d.j2_persist;
+    tuning().j2p_pairs = on >= 2 ? on == 2 : d.j2p_pairs;
     tuning().j2p_ni = sweeps_per_block ? sweeps_per_block : d.j2p_ni;
     return CFD_OK;
 }

@@ -24,9 +24,11 @@ struct Tuning {
     // small-grid 2-D Jacobi: sweeps per launch (1..8), rows per wave, cells per lane
     int j2s_k = 4, j2s_rw = 1, j2s_vec = 1;
     // small-grid 2-D Jacobi (f32) as one persistent launch (jacobi2d_persist)
-    // when every tile fits on the chip at once, j2p_ni (4, 6, 8) sweeps per
-    // block; 0 = one launch per j2s_k sweeps
-    int j2_persist = 1, j2p_ni = 8;
+    // when every tile fits on the chip at once, at most j2p_ni (4, 6, 8, 10)
+    // sweeps per block, the levels in pairs per LDS exchange (j2p_pairs); 0 =
+    // one launch per j2s_k sweeps
+    int j2_persist = 1, j2p_ni = 10;
+    bool j2p_pairs = true;
     // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per
     // workgroup, iterations per launch (1..4)
     int gs_rw = 2, gs_vec = 1, gs_wpb = 4, gs_ni = 4;

@@ -494,8 +494,11 @@ int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows);
 int cfd_set_small2d_gs_persistent(int mode);
 /* Small-grid float32 Jacobi (cfd_jacobi2d_f32 on a grid the launch-per-pass
  * kernel would take, more sweeps than one block) as one persistent launch:
- * on = 0 default (on), 1 off, 2 on; sweeps_per_block 0 = default (8), or
- * 4, 6, 8.  Its exchange ring lives in a library-owned device buffer. */
+ * on = 0 default (on), 1 off, 2 on (two sweeps per LDS exchange inside a
+ * tile), 3 on with one exchange per sweep; sweeps_per_block 0 = default (10),
+ * or 4, 6, 8, 10: the most sweeps per block, up to this, whose tiles all fit
+ * on the chip at once.  Its exchange ring lives in a library-owned device
+ * buffer. */
 int cfd_set_small2d_jacobi_persistent(int on, int sweeps_per_block);
 /* Both persistent small-grid solves (the GS above and the Jacobi below) are
  * plain launches after the library's own occupancy check by default
@@ -531,7 +534,8 @@ int cfd_release_thread_resources(void);
 /* Diagnostics: the persistent GS writes 4 timestamps (100 MHz device clock)
  * per tile and block into buf -- block start, halo received, tile ready,
  * levels done; layout [block][tile][4] u64 -- when bytes covers the solve
- * (NULL: off, the default). */
+ * (NULL: off, the default).  The persistent Jacobi (r06) writes block start,
+ * halo received, levels done, published into the same buffer. */
 int cfd_set_small2d_gs_trace(void *buf, size_t bytes);
 /* Diagnostics, in a library built with -DCFD_TBR_TRACE (scripts/build_variant.sh;
  * a no-op otherwise): the 3-D tall-tile kernels' workgroup 0 records, per wave,

@@ -347,18 +347,21 @@ def test_jacobi2d_small_shapes_bitexact(k, rw, vec):
     assert np.array_equal(host(phi), ref)
 
 
-@pytest.mark.parametrize("ni", [4, 6, 8])
+@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("ni", [4, 6, 8, 10])
 @pytest.mark.parametrize("shape,iters,pre", [((180, 600), 1500, True), ((180, 600), 37, False),
                                              ((36, 120), 9, True), ((53, 131), 17, False), ((3, 70), 12, True),
-                                             ((97, 64), 25, False)])
-def test_jacobi2d_persistent_bitexact(ni, shape, iters, pre):
+                                             ((97, 64), 25, False), ((53, 131), 23, True)])
+def test_jacobi2d_persistent_bitexact(ni, shape, iters, pre, mode):
     """The small-grid Jacobi as one persistent launch (jacobi2d_persist): the
     cylinder's grid at the reference's 1500 sweeps, ragged grids (tiles cut
     by the edges, one tile row, a one-row interior), sweep counts that are no
-    multiple of the block, with and without the RHS workspace; the mask
-    covers interior and edge cells (edge ones become 0 too), phi starts
-    non-zero."""
-    call("cfd_set_small2d_jacobi_persistent", 2, ni)
+    multiple of the block (odd remainders: a last single sweep after the
+    pairs), with and without the RHS workspace; the mask covers interior and
+    edge cells (edge ones become 0 too, also where the edge row is a tile's
+    last row), phi starts non-zero.  mode 2: two sweeps per LDS exchange (the
+    default), 3: one."""
+    call("cfd_set_small2d_jacobi_persistent", mode, ni)
     rng = np.random.default_rng(ni * 1000 + iters)
     div = rng.standard_normal(shape).astype(np.float32)
     phi0 = rng.standard_normal(shape).astype(np.float32)
