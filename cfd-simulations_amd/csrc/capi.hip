@@ -81,7 +81,7 @@ static Tuning process_defaults() {
         const int pr = env_int("CFD_PRED_ROWS", t.pred_rows);
         t.pred_rows = pr >= 0 ? pr : t.pred_rows;
         const int ni = env_int("CFD_GS_SMALL_NI", t.gs_ni);
-        t.gs_ni = ni >= 1 && ni <= 4 ? ni : t.gs_ni;
+        t.gs_ni = ni >= 1 && ni <= 5 ? ni : t.gs_ni;
         return t;
     }();
     return d;
@@ -330,8 +330,8 @@ int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec
 }
 
 int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows) {
-    CFD_REQUIRE(iters_per_launch >= 0 && iters_per_launch <= 4,
-                "small-grid GS iterations per launch must be 0 (default) or 1..4");
+    CFD_REQUIRE(iters_per_launch >= 0 && iters_per_launch <= 5,
+                "small-grid GS iterations per launch must be 0 (default) or 1..5");
     CFD_REQUIRE(shared_rows >= 0 && shared_rows <= 2, "small-grid GS shared_rows must be 0 (default), 1 or 2");
     const Tuning d = process_defaults();
     tuning().gs_ni = iters_per_launch ? iters_per_launch : d.gs_ni;

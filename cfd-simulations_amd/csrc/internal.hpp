@@ -30,8 +30,9 @@ struct Tuning {
     int j2_persist = 1, j2p_ni = 10;
     bool j2p_pairs = true;
     // small-grid 2-D red-black GS: rows per wave, cells per lane, waves per
-    // workgroup, iterations per launch (1..4)
-    int gs_rw = 2, gs_vec = 1, gs_wpb = 4, gs_ni = 4;
+    // workgroup, iterations per block (1..5: the persistent solve's, at most
+    // that whose tiles fit; the launch-per-block path takes at most 4)
+    int gs_rw = 2, gs_vec = 1, gs_wpb = 4, gs_ni = 5;
     // small-grid GS: rows shared in a 16-wave workgroup (rbgs2d_wg) instead of
     // per-wave halo rows (rbgs2d_small).  r02 at 600 x 180, us per iteration
     // by iterations per launch 2 / 3 / 4: shared 3.04 / 2.33 / 1.97; per-wave

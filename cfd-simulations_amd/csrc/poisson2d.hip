@@ -1286,7 +1286,7 @@ int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny,
             }
             // else P iterations per launch (the last
             // launch shorter), then the rollback of a stop inside a launch
-            const int P = tuning().gs_ni;
+            const int P = tuning().gs_ni < 4 ? tuning().gs_ni : 4;
             CFD_CHECK_HIP(hipMemsetAsync(w->maxc + iterations, 0, sizeof(float) * kGsSlots * (size_t)iterations, s));
             for (int it = 0; it < iterations;) {
                 const int m = iterations - it >= P ? P : iterations - it;

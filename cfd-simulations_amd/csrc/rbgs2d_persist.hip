@@ -70,7 +70,7 @@ constexpr int kPGSlots = kPLag + 2;                    // granule planes (block 
 constexpr int kPMSlots = 8;                            // per-block flag ring (>= kPLag + 2)
 static_assert(kPMSlots >= kPLag + 2, "flag ring too short for the lag");
 constexpr int kPMaxTiles = 256;                        // one tile per CU at most
-constexpr int kPMaxNI = 4;
+constexpr int kPMaxNI = 5;
 
 struct PersistArgs {
     const float *in;
@@ -104,7 +104,10 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
     constexpr int L = 2 * NI, HL = L, SOUT = 64 - 2 * HL, OUT = kPT0 - 2 * L;
     constexpr int MT = kPMaxTiles / 64;  // maxima granules per lane and iteration (wave 0)
     static_assert(OUT >= 2, "too many levels for the tile");
-    __shared__ float S[2][kPT0][64];
+    // two buffers of the tile's rows; tile row i at S[.][i + 2], two zero
+    // rows above and below (the halo-row reads need no test: each test was a
+    // branch on a spilled lane mask, ~12 of an iteration's ~67 VALU, r06)
+    __shared__ float S[2][kPT0 + 4][64];
     __shared__ int busy[NI];  // some own cell changed by >= tol in iteration q of the block
     __shared__ int sh_stop;
     const int lane = threadIdx.x & 63;
@@ -122,6 +125,14 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         broken = broken || (unsigned long long)(wall_clock64() - t0) > a.spin;
         return broken;
     };
+
+    if (w == 0) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            S[b][0][lane] = S[b][1][lane] = 0.f;
+            S[b][kPT0 + 2][lane] = S[b][kPT0 + 3][lane] = 0.f;
+        }
+    }
 
     float A[kPRW], RH[kPRW];
     bool U0[kPRW], U1[kPRW], own[kPRW], inner[kPRW];
@@ -276,7 +287,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
 #pragma unroll
         for (int q = 0; q < NI; ++q) hot[q] = false;
 #pragma unroll
-        for (int j = 0; j < kPRW; ++j) S[0][kPRW * w + j][lane] = A[j];
+        for (int j = 0; j < kPRW; ++j) S[0][kPRW * w + 2 + j][lane] = A[j];
         lds_barrier_p();
         if (a.trace && k >= 0 && w == 0 && lane == 0) a.trace[((size_t)k * a.ntiles + bid) * 4 + 2] = wall_clock64();
         typedef float f2 __attribute__((ext_vector_type(2)));
@@ -297,10 +308,8 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                     if (k >= kPLag) issue_maxima(k - kPLag);
                 }
                 if (i0 + 1 >= l + 1 && i0 < kPT0 - (l + 1)) {  // wave-uniform: an own row live at l + 1
-                    const float dn2 = i0 >= 2 ? S[rb][i0 - 2][lane] : 0.f;
-                    const float dn1 = i0 >= 1 ? S[rb][i0 - 1][lane] : 0.f;
-                    const float up1 = i0 + 2 < kPT0 ? S[rb][i0 + 2][lane] : 0.f;
-                    const float up2 = i0 + 3 < kPT0 ? S[rb][i0 + 3][lane] : 0.f;
+                    const float dn2 = S[rb][i0][lane], dn1 = S[rb][i0 + 1][lane];
+                    const float up1 = S[rb][i0 + 4][lane], up2 = S[rb][i0 + 5][lane];
                     // level l (colour 0): rows i0-1, i0 (pair lo) and i0+1, i0+2 (pair hi)
                     const f2 cl = {dn1, A[0]}, ch2 = {A[1], up1};
                     const f2 nl = ((a.cx * (f2{dpp_from_upper(dn1), dpp_from_upper(A[0])} +
@@ -339,8 +348,8 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                         // last interior row nothing is updated)
                         hot[p - 1] = dmax >= tolv;
                     }
-                    S[wb][i0][lane] = A[0];
-                    S[wb][i0 + 1][lane] = A[1];
+                    S[wb][i0 + 2][lane] = A[0];
+                    S[wb][i0 + 3][lane] = A[1];
                 }
                 if (p < m) lds_barrier_p();
             }
@@ -357,8 +366,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                 if (k >= kPLag) issue_maxima(k - kPLag);
             }
             if (i0 + 1 >= l && i0 < kPT0 - l) {  // wave-uniform: some row live
-                const float up = i0 + 2 < kPT0 ? S[rb][i0 + 2][lane] : 0.f;
-                const float dn = i0 > 0 ? S[rb][i0 - 1][lane] : 0.f;
+                const float up = S[rb][i0 + 4][lane], dn = S[rb][i0 + 1][lane];
                 const f2 a2 = {A[0], A[1]};
                 const f2 e2 = {dpp_from_upper(A[0]), dpp_from_upper(A[1])};
                 const f2 w2 = {dpp_from_lower(A[0]), dpp_from_lower(A[1])};
@@ -377,7 +385,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
 #pragma unroll
                 for (int j = 0; j < kPRW; ++j) {
                     A[j] = B[j];
-                    S[wb][i0 + j][lane] = B[j];
+                    S[wb][i0 + 2 + j][lane] = B[j];
                 }
             }
             if (l < 2 * m) lds_barrier_p();
@@ -403,6 +411,12 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         if (a.trace && k >= 0 && w == 0 && lane == 0) a.trace[((size_t)k * a.ntiles + bid) * 4 + 3] = wall_clock64();
     };
 
+    // diagnostics: in trace row nb, the kernel's entry, loop start, loop end and exit
+    auto mark_end = [&](int e, unsigned long long t) {
+        if (a.trace && w == 0 && lane == 0) a.trace[((size_t)nb * a.ntiles + bid) * 4 + e] = t;
+    };
+    mark_end(0, t0);
+    mark_end(1, wall_clock64());
     int stop = -1;  // first iteration meeting the tolerance (workgroup-uniform)
     if (w == 0) sh_stop = -1;
     if (w == 0 && lane < NI) busy[lane] = 0;
@@ -422,6 +436,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
             }
         }
     }
+    mark_end(2, wall_clock64());
     if (check && stop < 0) {
         // the last block's maxima, then the blocks no in-loop check covered
         lds_barrier_p();
@@ -454,6 +469,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         if (own[j]) a.out[off[j]] = A[j];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ws->flags[1] = stop >= 0 ? stop + 1 : a.niters;
     if (broken) atomicOr(&a.ws->flags[3], 1);
+    mark_end(3, wall_clock64());
 }
 
 // phi <- out (the solve's result), and the count; after an expired poll phi
@@ -514,7 +530,6 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
                          float cy, float cd, float dt_inv, float tol, float *phi_tmp, RbgsWs *ws,
                          size_t ws_bytes, int iterations, int *iters_done, hipStream_t s, int *rc) {
     *rc = CFD_OK;
-    const int NI = tuning().gs_ni;
     if (!tuning().gs_persist || !tuning().gs_wg || !phi_tmp || iterations < 1 || ny < 3 || nx < 3) return 0;
     const size_t base = align256(rbgs_base_bytes(iterations));
     if (ws_bytes < base + rbgs2d_persist_extra_bytes(ny, nx)) return 0;
@@ -526,10 +541,39 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     a.ws = ws;
     a.ny = ny;
     a.nx = nx;
-    a.ntiles = tiles_for(NI, ny, nx, &a.nseg);
     a.niters = iterations;
+    // every tile must be resident at once (they wait on each other): the most
+    // iterations per block, at most gs_ni, whose tiles all fit on the chip
+    // (5 at 600 x 180: 210 tiles; the block's fixed cost, the hand-off, is
+    // spread over 5 iterations instead of 4)
+    const bool pairs = tuning().gs_pairs != 0;
+#define CFD_PERS_N(F)                                         \
+    switch (NI) {                                             \
+        case 5: F(5); break;                                  \
+        case 4: F(4); break;                                  \
+        case 3: F(3); break;                                  \
+        case 2: F(2); break;                                  \
+        default: F(1); break;                                 \
+    }
+#define CFD_RES(N_)                                                                        \
+    resident = pairs ? (mask ? resident_tiles<true, N_, true>() : resident_tiles<false, N_, true>()) \
+                     : (mask ? resident_tiles<true, N_, false>() : resident_tiles<false, N_, false>())
+    int NI = tuning().gs_ni;
+    for (; NI >= 1; --NI) {
+        int resident = 0;
+        CFD_PERS_N(CFD_RES)
+        if (resident < 0) {
+            *rc = CFD_E_HIP;
+            set_error("rbgs2d persistent: occupancy query failed");
+            return 1;
+        }
+        a.ntiles = tiles_for(NI, ny, nx, &a.nseg);
+        if (a.ntiles <= resident && a.ntiles <= kPMaxTiles) break;
+    }
+#undef CFD_RES
+    if (NI < 1) return 0;  // the launch-per-block path
     {
-        const size_t need = 32 * (size_t)a.ntiles * (size_t)((iterations + NI - 1) / NI);
+        const size_t need = 32 * (size_t)a.ntiles * (size_t)((iterations + NI - 1) / NI + 1);
         a.trace = tuning().gs_trace_bytes >= need ? reinterpret_cast<unsigned long long *>(tuning().gs_trace) : nullptr;
     }
     a.cx = cx;
@@ -542,27 +586,6 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     const size_t gbytes = align256(sizeof(unsigned long long) * kPGSlots * (size_t)ny * nx);
     a.M = reinterpret_cast<unsigned long long *>(p + gbytes);
     const size_t mbytes = sizeof(unsigned long long) * kPMSlots * (size_t)a.ntiles;
-    // every tile must be resident at once (they wait on each other)
-    int resident = 0;
-    const bool pairs = tuning().gs_pairs != 0;
-#define CFD_PERS_N(F)                                         \
-    switch (NI) {                                             \
-        case 4: F(4); break;                                  \
-        case 3: F(3); break;                                  \
-        case 2: F(2); break;                                  \
-        default: F(1); break;                                 \
-    }
-#define CFD_RES(N_)                                                                        \
-    resident = pairs ? (mask ? resident_tiles<true, N_, true>() : resident_tiles<false, N_, true>()) \
-                     : (mask ? resident_tiles<true, N_, false>() : resident_tiles<false, N_, false>())
-    CFD_PERS_N(CFD_RES)
-#undef CFD_RES
-    if (resident < 0) {
-        *rc = CFD_E_HIP;
-        set_error("rbgs2d persistent: occupancy query failed");
-        return 1;
-    }
-    if (a.ntiles > resident || a.ntiles > kPMaxTiles) return 0;  // the launch-per-block path
     // a stale granule of an earlier solve carries a valid-looking tag: reset the rings
     if (hipMemsetAsync(p, 0, gbytes + mbytes, s) != hipSuccess) {
         *rc = CFD_E_HIP;

@@ -482,7 +482,9 @@ int cfd_reset_tuning(void);
  * gs_vec (1, 4), waves per workgroup gs_wpb (4, 16).  0 = the default. */
 int cfd_set_small2d_shape(int j2_k, int j2_rw, int j2_vec, int gs_rw, int gs_vec, int gs_wpb);
 /* Small-grid red-black GS: iterations (colour-pair levels) fused per launch,
- * 1..4 (0 = the default); a stop inside a launch is rolled back on the device.
+ * 1..5 (0 = the default, 5); a stop inside a launch is rolled back on the
+ * device.  The persistent solve takes the most up to this whose tiles all fit
+ * on the chip; the launch-per-block path at most 4.
  * shared_rows: 1 = each wave recomputes its halo rows (rbgs2d_small), 2 = the
  * rows of a 16-wave workgroup are shared through LDS (rbgs2d_wg), 0 = default. */
 int cfd_set_small2d_gs_iters(int iters_per_launch, int shared_rows);

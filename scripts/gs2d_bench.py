@@ -79,12 +79,14 @@ def trace_phases(solve, args, ni):
     out_rows, sout = 32 - 2 * L, 64 - 2 * L
     ntiles = -(-args.nx // sout) * -(-(args.ny - 2) // out_rows)
     nb = -(-args.iters // ni)
-    buf = torch.zeros(nb * ntiles * 4, dtype=torch.int64, device="cuda")
+    buf = torch.zeros((nb + 1) * ntiles * 4, dtype=torch.int64, device="cuda")
     call("cfd_set_small2d_gs_trace", buf.data_ptr(), buf.numel() * 8)
     solve()
     torch.cuda.synchronize()
     call("cfd_set_small2d_gs_trace", None, 0)
-    t = buf.cpu().numpy().reshape(nb, ntiles, 4).astype(np.float64) * 0.01  # us
+    t = buf.cpu().numpy().reshape(nb + 1, ntiles, 4).astype(np.float64) * 0.01  # us
+    ends = t[nb]  # per tile: kernel entry, loop start, loop end, exit
+    t = t[:nb]
     done = t[:, :, 3] > 0
     blocks = int(done.all(axis=1).sum())
     t = t[2:blocks]
@@ -92,7 +94,13 @@ def trace_phases(solve, args, ni):
     return {"blocks": blocks, "period": q(np.diff(t[:, :, 0], axis=0)), "halo_wait": q(t[:, :, 1] - t[:, :, 0]),
             "tile_ready": q(t[:, :, 2] - t[:, :, 1]), "levels": q(t[:, :, 3] - t[:, :, 2]),
             "publish_gap": q(t[1:, :, 0] - t[:-1, :, 3]),
-            "start_skew_p50": q(t[:, :, 0].max(axis=1) - t[:, :, 0].min(axis=1))}
+            "start_skew_p50": q(t[:, :, 0].max(axis=1) - t[:, :, 0].min(axis=1)),
+            "mean_period": round(float((t[-1, :, 0] - t[0, :, 0]).mean() / (t.shape[0] - 1)), 3),
+            "entry_spread": round(float(ends[:, 0].max() - ends[:, 0].min()), 2),
+            "prologue_max": round(float((ends[:, 1] - ends[:, 0]).max()), 2),
+            "loop": round(float(ends[:, 2].max() - ends[:, 1].min()), 1),
+            "epilogue_max": round(float((ends[:, 3] - ends[:, 2]).max()), 2),
+            "kernel": round(float(ends[:, 3].max() - ends[:, 0].min()), 1)}
 
 
 if __name__ == "__main__":

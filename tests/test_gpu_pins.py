@@ -309,13 +309,14 @@ def test_rbgs2d_small_shapes_bitexact(shape, iters, tol):
 
 
 @pytest.mark.parametrize("persistent", [1, 2, 3])
-@pytest.mark.parametrize("ni", [2, 3, 4])
+@pytest.mark.parametrize("ni", [2, 3, 4, 5])
 @pytest.mark.parametrize("iters,tol", [(37, 0.0), (400, 3e-5), (401, 1.5e-5)])
 def test_rbgs2d_shared_rows_cylinder_grid(ni, iters, tol, persistent):
-    """The shared-row small-grid GS with 2..4 iterations per block on the v5
-    cylinder's grid shape, one launch per block (rbgs2d_wg, persistent = 1)
-    or the whole solve as one persistent launch (rbgs2d_persist, 2, the
-    default): several tiles in x and y, solid cells, counts not a multiple of
+    """The shared-row small-grid GS with 2..5 iterations per block on the v5
+    cylinder's grid shape, one launch per block (rbgs2d_wg, persistent = 1,
+    at most 4 per launch) or the whole solve as one persistent launch
+    (rbgs2d_persist, 2, the default; 5 per block, 210 tiles, is its default
+    here): several tiles in x and y, solid cells, counts not a multiple of
     the block depth, early stops of both parities."""
     call("cfd_set_small2d_gs_iters", ni, 2)
     call("cfd_set_small2d_gs_persistent", persistent)
@@ -710,7 +711,7 @@ def test_rbgs3d_stop_at_every_iteration(levels):
 
 
 @pytest.mark.parametrize("mode", [2, 3])
-@pytest.mark.parametrize("ni", [1, 2, 3, 4])
+@pytest.mark.parametrize("ni", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("masked", [True, False])
 def test_rbgs2d_persistent_stop_at_every_iteration(ni, masked, mode):
     """The persistent small-grid GS (one launch, tiles handing their edge
