@@ -509,8 +509,13 @@ int jacobi2d_persist_solve(float *phi, const float *src, bool pre, const uint8_t
     }
     char *p = static_cast<char *>(ring_acquire(dev, gbytes + 256, s, rc));
     if (!p) return 1;
-    a.G = reinterpret_cast<unsigned long long *>(p);
-    a.status = reinterpret_cast<int *>(p + gbytes);
+    // the status words first, at a place no grid size moves: behind the
+    // granules they sat where a larger grid's solve had left granules, so a
+    // smaller grid after a larger one on the same ring read garbage there
+    // (its last workgroup never found itself last; an expired poll then went
+    // unreported, r06)
+    a.status = reinterpret_cast<int *>(p);
+    a.G = reinterpret_cast<unsigned long long *>(p + 256);
     // Granule tags carry a per-ring solve epoch, so a granule left by an earlier
     // solve never matches a poll of this one.  The ring is zeroed only when it
     // is new or the 16-bit epoch wraps (a plane a run of short solves leaves

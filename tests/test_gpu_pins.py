@@ -352,7 +352,8 @@ def test_jacobi2d_small_shapes_bitexact(k, rw, vec):
 @pytest.mark.parametrize("ni", [4, 6, 8, 10])
 @pytest.mark.parametrize("shape,iters,pre", [((180, 600), 1500, True), ((180, 600), 37, False),
                                              ((36, 120), 9, True), ((53, 131), 17, False), ((3, 70), 12, True),
-                                             ((97, 64), 25, False), ((53, 131), 23, True)])
+                                             ((97, 64), 25, False), ((53, 131), 23, True),
+                                             ((180, 1200), 47, True)])
 def test_jacobi2d_persistent_bitexact(ni, shape, iters, pre, mode):
     """The small-grid Jacobi as one persistent launch (jacobi2d_persist): the
     cylinder's grid at the reference's 1500 sweeps, ragged grids (tiles cut
@@ -360,8 +361,9 @@ def test_jacobi2d_persistent_bitexact(ni, shape, iters, pre, mode):
     multiple of the block (odd remainders: a last single sweep after the
     pairs), with and without the RHS workspace; the mask covers interior and
     edge cells (edge ones become 0 too, also where the edge row is a tile's
-    last row), phi starts non-zero.  mode 2: two sweeps per LDS exchange (the
-    default), 3: one."""
+    last row), phi starts non-zero; 180 x 1200: 10 or 8 sweeps per block
+    would not fit on the chip, so the solve takes 6.  mode 2: two sweeps per
+    LDS exchange (the default), 3: one."""
     call("cfd_set_small2d_jacobi_persistent", mode, ni)
     rng = np.random.default_rng(ni * 1000 + iters)
     div = rng.standard_normal(shape).astype(np.float32)
@@ -548,6 +550,30 @@ def test_persistent_forced_expiry_fails_loudly():
     assert K.persistent_failures() == 0
 
 
+def test_jacobi2d_persistent_status_after_a_larger_grid():
+    """The persistent Jacobi's status words (poll expired, workgroups done)
+    must not move with the grid: a larger grid's solve, then a smaller one's
+    on the same library-owned ring with a forced expiry, must still report
+    it (phi all NaN, one failure), and a normal solve after it is exact."""
+    rng = np.random.default_rng(12)
+    big = rng.standard_normal((180, 1200)).astype(np.float32)
+    div = rng.standard_normal((180, 600)).astype(np.float32)
+    phi = torch.zeros(big.shape, dtype=torch.float32, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(big), 20 / 599, np.float32(5e-5), None, 300)
+    assert np.array_equal(host(phi), oracle.jacobi2d(big, dx=20 / 599, dt=np.float32(5e-5), iters=300))
+    assert K.persistent_failures() == 0
+    call("cfd_set_persistent_launch", 0, 1)
+    phi = torch.zeros(div.shape, dtype=torch.float32, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), None, 300)
+    assert np.isnan(host(phi)).all()
+    assert K.persistent_failures() == 1
+    call("cfd_set_persistent_launch", 0, 0)
+    phi = torch.zeros(div.shape, dtype=torch.float32, device=DEV)
+    K.solve_pressure_jacobi(phi, dev(div), 20 / 599, np.float32(5e-5), None, 300)
+    assert np.array_equal(host(phi), oracle.jacobi2d(div, dx=20 / 599, dt=np.float32(5e-5), iters=300))
+    assert K.persistent_failures() == 0
+
+
 def test_health_check_is_per_stream():
     """Two solvers on two streams (v5.py:599-613's health check per solver):
     a neighbour-wait expiry forced in solver A's step (1-tick poll bound, on
@@ -708,6 +734,25 @@ def test_rbgs3d_stop_at_every_iteration(levels):
             assert np.array_equal(host(phi), ref), (c, N)
             seen.add(n_ref)
     assert len(seen) >= 10, seen
+
+
+@pytest.mark.parametrize("iters,tol", [(23, 0.0), (300, 2e-5)])
+def test_rbgs2d_persistent_fewer_iterations_per_block_when_tiles_do_not_fit(iters, tol):
+    """180 x 1000: 5 iterations per block would need 23 x 15 = 345 tiles, more
+    than the chip holds at once; the persistent solve takes the most that fit
+    (4: 21 x 12 = 252 tiles) instead of the launch-per-block path."""
+    call("cfd_set_small2d_gs_iters", 5, 2)
+    call("cfd_set_small2d_gs_persistent", 2)
+    rng = np.random.default_rng(91)
+    div = rng.standard_normal((180, 1000)).astype(np.float32) * np.float32(1e-3)
+    mask = rng.random(div.shape) < 0.03
+    ref, n_ref = oracle.rbgs2d(div, dx=0.05, dy=0.05, dt=np.float32(1e-2), iters=iters, tol=tol, mask=mask)
+    phi = torch.zeros_like(dev(div))
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.solve_pressure_gauss_seidel_fast(phi, dev(div), 0.05, 0.05, np.float32(1e-2), dev(mask), iters, tol,
+                                       iters_done=done)
+    assert int(host(done)[0]) == n_ref
+    assert np.array_equal(host(phi), ref)
 
 
 @pytest.mark.parametrize("mode", [2, 3])
