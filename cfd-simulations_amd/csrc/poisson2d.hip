@@ -1267,23 +1267,32 @@ int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny,
     const float dt_inv = 1.0f / dt;  // 1.0 / np.float32 -> float32
     const float tol = (float)tolerance;
     RbgsWs *w = reinterpret_cast<RbgsWs *>(ws);
-    int rc = launch_rbgs_init(w, iterations, tol, iters_done, s);
+    int rc = CFD_OK;
+    const bool vec_ok = (nx % 4 == 0) && aligned16(phi) && aligned16(div);
+    const bool fused = phi_tmp && tuning().j2_blocking != 1 && vec_ok && aligned16(phi_tmp);
+    if (ny >= 3 && nx >= 3 && iterations > 0 && fused && rbgs2d_small_grid(ny, nx)) {
+        // small grid (the v5 cylinder): one persistent launch when the
+        // workspace holds its rings and every tile is resident at once.  It
+        // needs neither the workspace init (its failure word lives in the
+        // rings, reset with them; it writes the count) nor phi_tmp's edge
+        // rows (its finish copies rows 1 .. ny - 2 back): two launches fewer
+        const int tk = timing_begin(s);
+        if (rbgs2d_persist_solve(phi, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, phi_tmp, w, ws_bytes, iterations,
+                                 iters_done, s, &rc)) {
+            timing_end(tk, s, iterations);
+            return rc;
+        }
+        timing_cancel(tk);  // (the fallback below times itself)
+    }
+    rc = launch_rbgs_init(w, iterations, tol, iters_done, s);
     if (rc) return rc;
     if (ny < 3 || nx < 3 || iterations == 0) return CFD_OK;
-    const bool vec_ok = (nx % 4 == 0) && aligned16(phi) && aligned16(div);
     const int tk = timing_begin(s);
-    if (phi_tmp && tuning().j2_blocking != 1 && vec_ok && aligned16(phi_tmp)) {
+    if (fused) {
         // fused: one out-of-place pass per iteration (both colours), ping-pong
         if ((rc = fix_edge_rows<float>(phi, phi_tmp, nullptr, ny, nx, s))) return rc;
         float *a = phi, *b = phi_tmp;
         if (rbgs2d_small_grid(ny, nx)) {
-            // small grid (the v5 cylinder): one persistent launch when the
-            // workspace holds its rings and every tile is resident at once
-            if (rbgs2d_persist_solve(phi, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, phi_tmp, w, ws_bytes,
-                                     iterations, iters_done, s, &rc)) {
-                timing_end(tk, s, iterations);
-                return rc;
-            }
             // else P iterations per launch (the last
             // launch shorter), then the rollback of a stop inside a launch
             const int P = tuning().gs_ni < 4 ? tuning().gs_ni : 4;

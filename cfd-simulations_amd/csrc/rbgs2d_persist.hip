@@ -80,6 +80,7 @@ struct PersistArgs {
     unsigned long long *G;  // kPGSlots planes of ny * nx granules
     unsigned long long *M;  // kPMSlots x ntiles flag granules
     RbgsWs *ws;
+    int *bad;  // a poll expired (a ring word, zeroed with the rings per solve)
     unsigned long long *trace;  // optional: 4 timestamps per tile and block
     unsigned long long spin;    // poll bound, 100 MHz ticks
     int ny, nx, nseg, ntiles, niters;
@@ -468,24 +469,30 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
     for (int j = 0; j < kPRW; ++j)
         if (own[j]) a.out[off[j]] = A[j];
     if (blockIdx.x == 0 && threadIdx.x == 0) a.ws->flags[1] = stop >= 0 ? stop + 1 : a.niters;
-    if (broken) atomicOr(&a.ws->flags[3], 1);
+    if (broken) atomicOr(a.bad, 1);
     mark_end(3, wall_clock64());
 }
 
-// phi <- out (the solve's result), and the count; after an expired poll phi
-// becomes all NaN instead (it cannot pass for a solution), the count -1, and
-// the device's failure counter (cfd_persistent_status) counts the solve
-__global__ void rbgs_persist_finish(const RbgsWs *__restrict__ ws, float *__restrict__ phi,
-                                    const float *__restrict__ src, size_t n, int *iters_done, int *fail) {
+// phi's rows 1 .. ny - 2 <- out's (the solve's result; rows 0 and ny - 1 never
+// change, so phi keeps its own and out needs none), and the count; after an
+// expired poll phi becomes all NaN instead (it cannot pass for a solution),
+// the count -1, and the device's failure counter (cfd_persistent_status)
+// counts the solve.  nx % 4 == 0 (the float4 path's condition).
+__global__ void rbgs_persist_finish(const RbgsWs *__restrict__ ws, const int *__restrict__ badp, float *__restrict__ phi,
+                                    const float *__restrict__ src, int ny, int nx, int *iters_done, int *fail) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    const size_t n4 = n / 4;
-    const bool bad = ws->flags[3] != 0;
+    const bool bad = *badp != 0;
     const float4 nan4 = make_float4(__int_as_float(0x7fc00000), __int_as_float(0x7fc00000),
                                     __int_as_float(0x7fc00000), __int_as_float(0x7fc00000));
-    for (size_t k = t0; k < n4; k += stride)
-        reinterpret_cast<float4 *>(phi)[k] = bad ? nan4 : reinterpret_cast<const float4 *>(src)[k];
-    for (size_t k = 4 * n4 + t0; k < n; k += stride) phi[k] = bad ? nan4.x : src[k];
+    if (bad) {
+        const size_t n4 = (size_t)ny * nx / 4;
+        for (size_t k = t0; k < n4; k += stride) reinterpret_cast<float4 *>(phi)[k] = nan4;
+    } else {
+        const size_t b4 = (size_t)nx / 4, e4 = (size_t)(ny - 1) * nx / 4;
+        for (size_t k = b4 + t0; k < e4; k += stride)
+            reinterpret_cast<float4 *>(phi)[k] = reinterpret_cast<const float4 *>(src)[k];
+    }
     if (t0 == 0 && iters_done) *iters_done = bad ? -1 : ws->flags[1];
     if (t0 == 0 && bad && fail) atomicAdd(fail, 1);
 }
@@ -586,8 +593,10 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     const size_t gbytes = align256(sizeof(unsigned long long) * kPGSlots * (size_t)ny * nx);
     a.M = reinterpret_cast<unsigned long long *>(p + gbytes);
     const size_t mbytes = sizeof(unsigned long long) * kPMSlots * (size_t)a.ntiles;
-    // a stale granule of an earlier solve carries a valid-looking tag: reset the rings
-    if (hipMemsetAsync(p, 0, gbytes + mbytes, s) != hipSuccess) {
+    a.bad = reinterpret_cast<int *>(p + gbytes + mbytes);  // (within the extra bytes' last 256)
+    // a stale granule of an earlier solve carries a valid-looking tag: reset
+    // the rings (and the failure word)
+    if (hipMemsetAsync(p, 0, gbytes + mbytes + sizeof(int), s) != hipSuccess) {
         *rc = CFD_E_HIP;
         set_error("rbgs2d persistent: ring reset failed");
         return 1;
@@ -607,8 +616,8 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
         return 1;
     }
     const size_t n = (size_t)ny * nx;
-    hipLaunchKernelGGL(rbgs_persist_finish, dim3(ceil_div((long)(n / 4 + 1), 256)), dim3(256), 0, s, ws, phi,
-                       phi_tmp, n, iters_done, persist_fail_word(s));
+    hipLaunchKernelGGL(rbgs_persist_finish, dim3(ceil_div((long)(n / 4 + 1), 256)), dim3(256), 0, s, ws, a.bad, phi,
+                       phi_tmp, ny, nx, iters_done, persist_fail_word(s));
     const hipError_t e2 = hipGetLastError();
     if (e2 != hipSuccess) {
         *rc = CFD_E_HIP;
