@@ -41,6 +41,8 @@ PROTOTYPES = {
                                P, P, P, P]),
     "cfd_rbgs2d_f32_ws": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_float, c_int, c_double,
                                   P, P, c_size_t, P, P]),
+    "cfd_rbgs2d_zero_f32_ws": (c_int, [P, P, P, c_int, c_int, c_double, c_double, c_float, c_int, c_double,
+                                  P, P, c_size_t, P, P]),
     "cfd_rbgs3d_f32": (c_int, [P, P, P, c_int, c_int, c_int, c_double, c_double, c_double, c_float,
                                c_int, c_double, P, P, P, P]),
     "cfd_supg_tau2d_f32": (c_int, [P, P, P, c_float, P, c_int, c_int, c_double, c_double, c_float, P]),

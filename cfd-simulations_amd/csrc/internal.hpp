@@ -174,7 +174,8 @@ int launch_rbgs_finish(RbgsWs *ws, float *phi, const float *phi_tmp, size_t n,
 size_t rbgs2d_persist_extra_bytes(int ny, int nx);
 int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int ny, int nx, float cx,
                          float cy, float cd, float dt_inv, float tol, float *phi_tmp, RbgsWs *ws,
-                         size_t ws_bytes, int iterations, int *iters_done, hipStream_t s, int *rc);
+                         size_t ws_bytes, int iterations, int *iters_done, hipStream_t s, int *rc,
+                         bool zero = false);
 constexpr int kGsSlotRows = 16;  // rbgs2d_small's per-iteration maxima slots
 inline size_t rbgs_base_bytes(int iterations) {
     return 16 + sizeof(float) * (size_t)(1 + kGsSlotRows) * (size_t)(iterations > 0 ? iterations : 1);

@@ -1254,9 +1254,9 @@ int cfd_rbgs2d_f32(float *phi, const float *div, const uint8_t *mask, int ny, in
                              cfd_rbgs_workspace_bytes(iterations), iters_done, stream);
 }
 
-int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
-                      double dy, float dt, int iterations, double tolerance, float *phi_tmp, void *ws,
-                      size_t ws_bytes, int *iters_done, void *stream) {
+static int rbgs2d_f32_solve(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
+                            double dy, float dt, int iterations, double tolerance, float *phi_tmp, void *ws,
+                            size_t ws_bytes, int *iters_done, void *stream, bool zero) {
     CFD_REQUIRE(phi && div && ws, "rbgs2d: null pointer");
     CFD_REQUIRE(ny >= 1 && nx >= 1 && iterations >= 0, "rbgs2d: bad arguments");
     hipStream_t s = as_stream(stream);
@@ -1278,12 +1278,13 @@ int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny,
         // rows (its finish copies rows 1 .. ny - 2 back): two launches fewer
         const int tk = timing_begin(s);
         if (rbgs2d_persist_solve(phi, div, mask, ny, nx, cx, cy, cd, dt_inv, tol, phi_tmp, w, ws_bytes, iterations,
-                                 iters_done, s, &rc)) {
+                                 iters_done, s, &rc, zero)) {
             timing_end(tk, s, iterations);
             return rc;
         }
         timing_cancel(tk);  // (the fallback below times itself)
     }
+    if (zero) CFD_CHECK_HIP(hipMemsetAsync(phi, 0, sizeof(float) * (size_t)ny * nx, s));
     rc = launch_rbgs_init(w, iterations, tol, iters_done, s);
     if (rc) return rc;
     if (ny < 3 || nx < 3 || iterations == 0) return CFD_OK;
@@ -1331,6 +1332,20 @@ int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny,
     }
     timing_end(tk, s, iterations);
     return CFD_OK;
+}
+
+int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
+                      double dy, float dt, int iterations, double tolerance, float *phi_tmp, void *ws,
+                      size_t ws_bytes, int *iters_done, void *stream) {
+    return rbgs2d_f32_solve(phi, div, mask, ny, nx, dx, dy, dt, iterations, tolerance, phi_tmp, ws, ws_bytes,
+                            iters_done, stream, false);
+}
+
+int cfd_rbgs2d_zero_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny, int nx, double dx,
+                           double dy, float dt, int iterations, double tolerance, float *phi_tmp, void *ws,
+                           size_t ws_bytes, int *iters_done, void *stream) {
+    return rbgs2d_f32_solve(phi, div, mask, ny, nx, dx, dy, dt, iterations, tolerance, phi_tmp, ws, ws_bytes,
+                            iters_done, stream, true);
 }
 
 }  // extern "C"

@@ -84,6 +84,7 @@ struct PersistArgs {
     unsigned long long *trace;  // optional: 4 timestamps per tile and block
     unsigned long long spin;    // poll bound, 100 MHz ticks
     int ny, nx, nseg, ntiles, niters;
+    int zero;  // phi = zeros first (v5.py:337): read nothing of `in`
     float cx, cy, cd, dt_inv, tol;
 };
 
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         const int i = kPRW * w + j, y = ytop + i;
         const bool in_ = valid && y >= 0 && y <= a.ny - 1;
         off[j] = (size_t)min(max(y, 0), a.ny - 1) * a.nx + (valid ? x : 0);
-        const float v = a.in[off[j]];
+        const float v = a.zero ? 0.f : a.in[off[j]];
         const float d = a.div[off[j]];
         const bool mk = MASK ? a.mask[off[j]] != 0 : false;
         const bool edge = y <= 0 || y >= a.ny - 1;
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         if (B == 0) {
 #pragma unroll
             for (int j = 0; j < kPRW; ++j)
-                if (inner[j]) A[j] = a.in[off[j]];
+                if (inner[j]) A[j] = a.zero ? 0.f : a.in[off[j]];
         } else {
             fetch(B, true);
         }
@@ -479,7 +480,8 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
 // the count -1, and the device's failure counter (cfd_persistent_status)
 // counts the solve.  nx % 4 == 0 (the float4 path's condition).
 __global__ void rbgs_persist_finish(const RbgsWs *__restrict__ ws, const int *__restrict__ badp, float *__restrict__ phi,
-                                    const float *__restrict__ src, int ny, int nx, int *iters_done, int *fail) {
+                                    const float *__restrict__ src, int ny, int nx, int zero, int *iters_done,
+                                    int *fail) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const bool bad = *badp != 0;
@@ -492,6 +494,13 @@ __global__ void rbgs_persist_finish(const RbgsWs *__restrict__ ws, const int *__
         const size_t b4 = (size_t)nx / 4, e4 = (size_t)(ny - 1) * nx / 4;
         for (size_t k = b4 + t0; k < e4; k += stride)
             reinterpret_cast<float4 *>(phi)[k] = reinterpret_cast<const float4 *>(src)[k];
+        if (zero) {  // a zero start: rows 0 and ny - 1 are zeros too
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (size_t k = t0; k < b4; k += stride) {
+                reinterpret_cast<float4 *>(phi)[k] = z4;
+                reinterpret_cast<float4 *>(phi)[e4 + k] = z4;
+            }
+        }
     }
     if (t0 == 0 && iters_done) *iters_done = bad ? -1 : ws->flags[1];
     if (t0 == 0 && bad && fail) atomicAdd(fail, 1);
@@ -535,7 +544,7 @@ size_t rbgs2d_persist_extra_bytes(int ny, int nx) {
 
 int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int ny, int nx, float cx,
                          float cy, float cd, float dt_inv, float tol, float *phi_tmp, RbgsWs *ws,
-                         size_t ws_bytes, int iterations, int *iters_done, hipStream_t s, int *rc) {
+                         size_t ws_bytes, int iterations, int *iters_done, hipStream_t s, int *rc, bool zero) {
     *rc = CFD_OK;
     if (!tuning().gs_persist || !tuning().gs_wg || !phi_tmp || iterations < 1 || ny < 3 || nx < 3) return 0;
     const size_t base = align256(rbgs_base_bytes(iterations));
@@ -549,6 +558,7 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     a.ny = ny;
     a.nx = nx;
     a.niters = iterations;
+    a.zero = zero ? 1 : 0;
     // every tile must be resident at once (they wait on each other): the most
     // iterations per block, at most gs_ni, whose tiles all fit on the chip
     // (5 at 600 x 180: 210 tiles; the block's fixed cost, the hand-off, is
@@ -617,7 +627,7 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     }
     const size_t n = (size_t)ny * nx;
     hipLaunchKernelGGL(rbgs_persist_finish, dim3(ceil_div((long)(n / 4 + 1), 256)), dim3(256), 0, s, ws, a.bad, phi,
-                       phi_tmp, ny, nx, iters_done, persist_fail_word(s));
+                       phi_tmp, ny, nx, a.zero, iters_done, persist_fail_word(s));
     const hipError_t e2 = hipGetLastError();
     if (e2 != hipSuccess) {
         *rc = CFD_E_HIP;

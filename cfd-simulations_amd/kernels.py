@@ -153,8 +153,11 @@ def compute_gradient_fast(phi, dx, dy):
 
 
 def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iterations, tolerance,
-                                     workspace=None, iters_done=None, phi_tmp=None):
+                                     workspace=None, iters_done=None, phi_tmp=None, zero_start=False):
     """v5.py:202-226: red-black GS, in place on ``phi``; returns ``phi``.
+    ``zero_start``: phi = zeros first (v5.py:337) inside the solve
+    (cfd_rbgs2d_zero_f32_ws: the persistent small-grid solve reads nothing of
+    phi; other paths zero-fill it first).
     ``iters_done`` (optional int32 device scalar) receives the iteration count.
     float32: ``phi_tmp`` (same-size scratch field, allocated if omitted) lets
     every iteration run as one fused out-of-place pass; the result still lands
@@ -171,11 +174,13 @@ def solve_pressure_gauss_seidel_fast(phi, div_u_star, dx, dy, dt, mask, iteratio
         ws = torch.empty(need, dtype=torch.uint8, device=phi.device)
     _like(phi, div_u_star, "div_u_star")
     if phi.dtype == torch.float64:
+        if zero_start:
+            phi.zero_()
         call("cfd_rbgs2d_f64", ptr(phi), ptr(div_u_star), ptr(m), ny, nx, float(dx), float(dy),
              float(np.float32(dt)), int(iterations), float(tolerance), ptr(ws), ptr(iters_done), stream_handle())
         return phi
     tmp = torch.empty_like(phi) if phi_tmp is None else _like(phi, phi_tmp, "phi_tmp")
-    call("cfd_rbgs2d_f32_ws", ptr(_f32(phi, "phi")), ptr(_f32(div_u_star, "div_u_star")), ptr(m), ny, nx,
+    call("cfd_rbgs2d_zero_f32_ws" if zero_start else "cfd_rbgs2d_f32_ws", ptr(_f32(phi, "phi")), ptr(_f32(div_u_star, "div_u_star")), ptr(m), ny, nx,
          float(dx), float(dy), float(np.float32(dt)), int(iterations), float(tolerance), ptr(_f32(tmp, "phi_tmp")),
          ptr(ws), ws.numel() * ws.element_size(), ptr(iters_done), stream_handle())
     return phi

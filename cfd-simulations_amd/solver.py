@@ -222,12 +222,12 @@ class OptimizedTurbulentSolver:
 
     def solve_pressure_fast(self, div_u_star):  # v5.py:328-347
         cfg = self.config
-        if cfg.use_fast_pressure:
-            self.phi.zero_()
+        if cfg.use_fast_pressure:  # phi = zeros (v5.py:337) inside the solve
             K.solve_pressure_gauss_seidel_fast(self.phi, div_u_star, cfg.dx, cfg.dy, cfg.dt,
                                                self._mask_u8, cfg.pressure_iterations,
                                                cfg.pressure_tolerance, workspace=self._gs_ws,
-                                               iters_done=self._gs_done, phi_tmp=self._phi_tmp)
+                                               iters_done=self._gs_done, phi_tmp=self._phi_tmp,
+                                               zero_start=True)
         else:  # phi = zeros (v5.py:337) inside the solve
             K.solve_pressure_jacobi(self.phi, div_u_star, cfg.dx, cfg.dt, self._mask_u8,
                                     cfg.pressure_iterations, phi_tmp=self._phi_tmp, rhs_ws=self._rhs_ws,

@@ -150,6 +150,15 @@ size_t cfd_rbgs2d_workspace_bytes(int ny, int nx, int iterations);
 int cfd_rbgs2d_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny, int nx,
                       double dx, double dy, float dt, int iterations, double tolerance,
                       float *phi_tmp, void *ws, size_t ws_bytes, int *iters_done, void *stream);
+/* The reference's GS solve with its zero fill (v5.py:337: phi = zeros, then
+ * the iterations of cfd_rbgs2d_f32_ws; the same bits).  The persistent
+ * small-grid solve starts from the zeros itself (it reads nothing of phi and
+ * writes every cell); other paths zero-fill phi first.  Replaces
+ * solve_pressure_fast's np.zeros + solve_pressure_gauss_seidel_fast
+ * (v5.py:337-342). */
+int cfd_rbgs2d_zero_f32_ws(float *phi, const float *div, const uint8_t *mask, int ny, int nx,
+                           double dx, double dy, float dt, int iterations, double tolerance,
+                           float *phi_tmp, void *ws, size_t ws_bytes, int *iters_done, void *stream);
 /* 3-D red-black generalisation: colour c updates (z+i+j) parity == (1+c)%2.
  * The fused 3-D path runs cfd_get_rbgs3d_levels() half-sweeps per HBM pass
  * (default 4: two iterations; cfd_set_jacobi3d_blocking(2..4, ...) sets it),

@@ -736,6 +736,31 @@ def test_rbgs3d_stop_at_every_iteration(levels):
     assert len(seen) >= 10, seen
 
 
+@pytest.mark.parametrize("persistent", [1, 2])
+@pytest.mark.parametrize("iters,tol", [(37, 0.0), (400, 3e-5), (0, 0.0)])
+def test_rbgs2d_zero_start_bitexact(iters, tol, persistent):
+    """cfd_rbgs2d_zero_f32_ws (solve_pressure_fast's np.zeros + GS,
+    v5.py:337-342) on the cylinder's grid shape: phi holds garbage (NaN rows
+    included) before the call and must end as the oracle's solve from zeros,
+    edge rows zero too; the persistent solve (2) reads nothing of phi, the
+    launch-per-block path (1) zero-fills it first."""
+    call("cfd_set_small2d_gs_persistent", persistent)
+    rng = np.random.default_rng(44)
+    div = rng.standard_normal((180, 600)).astype(np.float32) * np.float32(1e-3)
+    mask = rng.random(div.shape) < 0.03
+    ref, n_ref = oracle.rbgs2d(div, dx=0.05, dy=0.05, dt=np.float32(1e-2), iters=iters, tol=tol, mask=mask)
+    junk = rng.standard_normal(div.shape).astype(np.float32)
+    junk[0, :] = np.nan
+    junk[-1, 3] = np.inf
+    phi = dev(junk)
+    done = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.solve_pressure_gauss_seidel_fast(phi, dev(div), 0.05, 0.05, np.float32(1e-2), dev(mask), iters, tol,
+                                       iters_done=done, zero_start=True)
+    if iters:
+        assert int(host(done)[0]) == n_ref
+    assert np.array_equal(host(phi), ref)
+
+
 @pytest.mark.parametrize("iters,tol", [(23, 0.0), (300, 2e-5)])
 def test_rbgs2d_persistent_fewer_iterations_per_block_when_tiles_do_not_fit(iters, tol):
     """180 x 1000: 5 iterations per block would need 23 x 15 = 345 tiles, more
