@@ -84,7 +84,6 @@ struct PersistArgs {
     unsigned long long *trace;  // optional: 4 timestamps per tile and block
     unsigned long long spin;    // poll bound, 100 MHz ticks
     int ny, nx, nseg, ntiles, niters;
-    int zero;  // phi = zeros first (v5.py:337): read nothing of `in`
     float cx, cy, cd, dt_inv, tol;
 };
 
@@ -144,7 +143,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         const int i = kPRW * w + j, y = ytop + i;
         const bool in_ = valid && y >= 0 && y <= a.ny - 1;
         off[j] = (size_t)min(max(y, 0), a.ny - 1) * a.nx + (valid ? x : 0);
-        const float v = a.zero ? 0.f : a.in[off[j]];
+        const float v = a.in ? a.in[off[j]] : 0.f;
         const float d = a.div[off[j]];
         const bool mk = MASK ? a.mask[off[j]] != 0 : false;
         const bool edge = y <= 0 || y >= a.ny - 1;
@@ -460,7 +459,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
         if (B == 0) {
 #pragma unroll
             for (int j = 0; j < kPRW; ++j)
-                if (inner[j]) A[j] = a.zero ? 0.f : a.in[off[j]];
+                if (inner[j]) A[j] = a.in ? a.in[off[j]] : 0.f;
         } else {
             fetch(B, true);
         }
@@ -550,7 +549,8 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     const size_t base = align256(rbgs_base_bytes(iterations));
     if (ws_bytes < base + rbgs2d_persist_extra_bytes(ny, nx)) return 0;
     PersistArgs a;
-    a.in = phi;
+    a.in = zero ? nullptr : phi;  // null: a zero start (v5.py:337), nothing of phi read (a field
+                                  // of its own cost the loop SGPR spills: 57 -> 65 VALU per iteration)
     a.out = phi_tmp;
     a.div = div;
     a.mask = mask;
@@ -558,7 +558,6 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     a.ny = ny;
     a.nx = nx;
     a.niters = iterations;
-    a.zero = zero ? 1 : 0;
     // every tile must be resident at once (they wait on each other): the most
     // iterations per block, at most gs_ni, whose tiles all fit on the chip
     // (5 at 600 x 180: 210 tiles; the block's fixed cost, the hand-off, is
@@ -627,7 +626,7 @@ int rbgs2d_persist_solve(float *phi, const float *div, const uint8_t *mask, int 
     }
     const size_t n = (size_t)ny * nx;
     hipLaunchKernelGGL(rbgs_persist_finish, dim3(ceil_div((long)(n / 4 + 1), 256)), dim3(256), 0, s, ws, a.bad, phi,
-                       phi_tmp, ny, nx, a.zero, iters_done, persist_fail_word(s));
+                       phi_tmp, ny, nx, zero ? 1 : 0, iters_done, persist_fail_word(s));
     const hipError_t e2 = hipGetLastError();
     if (e2 != hipSuccess) {
         *rc = CFD_E_HIP;
