@@ -266,6 +266,10 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
     const int nb = (a.niters + NI - 1) / NI;
     bool hot[NI];  // per lane: an own cell changed by >= tol (a NaN change never counts, as in v5.py:221)
     const bool own_rows = kPRW * w + 1 >= L && kPRW * w < kPT0 - L;  // wave-uniform
+    // the PAIRS levels' stop-test condition as a scalar int: as a bool it
+    // stayed a 64-bit lane mask, spilled to VGPR lanes (two v_readlane per
+    // use, twice per iteration)
+    const int chk_own = __builtin_amdgcn_readfirstlane(check && own_rows ? 1 : 0);
     // PAIRS: the colour masks as VGPR bit masks (v_bfi_b32 selects) and the
     // stop threshold as a per-lane VGPR (tol on a lane of own cells, NaN
     // elsewhere: no compare is true).  As 64-bit lane masks they outgrew the
@@ -308,7 +312,8 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                     publish_flags(k - 1);
                     if (k >= kPLag) issue_maxima(k - kPLag);
                 }
-                if (i0 + 1 >= l + 1 && i0 < kPT0 - (l + 1)) {  // wave-uniform: an own row live at l + 1
+                // wave-uniform: an own row live at l + 1 (a scalar int, as chk_own)
+                if (__builtin_amdgcn_readfirstlane(i0 + 1 >= l + 1 && i0 < kPT0 - (l + 1) ? 1 : 0)) {
                     const float dn2 = S[rb][i0][lane], dn1 = S[rb][i0 + 1][lane];
                     const float up1 = S[rb][i0 + 4][lane], up2 = S[rb][i0 + 5][lane];
                     // level l (colour 0): rows i0-1, i0 (pair lo) and i0+1, i0+2 (pair hi)
@@ -330,7 +335,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                     // for a cell the colour leaves alone; fmaxf drops a NaN
                     // change (it never counts, v5.py:221)
                     float dmax = 0.f;
-                    if (check && own_rows) {
+                    if (chk_own) {
                         const f2 d0 = f2{q1, q2} - f2{cl[1], ch2[0]};
                         dmax = fmaxf(fmaxf(fabsf(d0[0]), fabsf(d0[1])), dmax);
                     }
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(1024) void rbgs2d_persist(PersistArgs a) {
                                     a.cy * (f2{q2, q3} + f2{q0, q1})) - rh) * a.cd;
                     A[0] = bsel(mU10, nv[0], c2[0]);
                     A[1] = bsel(mU11, nv[1], c2[1]);
-                    if (check && own_rows) {
+                    if (chk_own) {
                         const f2 d1 = f2{A[0], A[1]} - c2;
                         dmax = fmaxf(fmaxf(fabsf(d1[0]), fabsf(d1[1])), dmax);
                         // own[0] covers own[1] wherever row i0 + 1 can change
